@@ -1,0 +1,170 @@
+/*
+ * rs_simplify.h -- C ABI of librs_simplify, the MI355X-native R1CS constraint-simplification
+ * back end for circom (--O1 / --O2 / --O2round N).
+ *
+ * This is the drop-in seam.  In the reference (circom 2.2.2, /root/reference) the path is the
+ * body of
+ *     constraint_list::constraint_simplification::simplification(&mut Simplifier)
+ *         -> (ConstraintStorage, SignalMap, usize)
+ *     constraint_list/src/constraint_simplification.rs:442-730
+ * called only from Simplifier::simplify_constraints (constraint_list/src/lib.rs:131-144).
+ * The reference has no FFI and no plugin registry; these entry points are what a Rust shim in
+ * constraint_list would bind with `extern "C"` (see INTEGRATION.md for the binding).
+ *
+ * Conventions
+ *   - Field elements are 4 little-endian u64 limbs, canonical (< p).  The field is one of the
+ *     eight circom primes (program_structure/src/utils/constants.rs:3-13) or a custom odd prime
+ *     < 2^256 (used by tests, e.g. the reference unit tests' F_257).
+ *   - Linear combinations are CSR blocks.  Column 0 is the constant-one signal (the reference's
+ *     ArithmeticExpression::constant_coefficient(), algebra.rs:155-157).  Within a row the columns
+ *     must be distinct; order is free.  Rows must be clean (no zero coefficient), as
+ *     DAG::clean_constraints guarantees for every row the reference hands to simplification()
+ *     (dag/src/constraint_correctness_analysis.rs:146-157); RS_E_INVALID otherwise.
+ *   - All entry points are synchronous and blocking; one call at a time per engine.
+ *   - Errors: 0 on success, a negative RS_E_* code otherwise; rs_last_error() explains.  The
+ *     reference panics on the same internal invariants (e.g. algebra.rs:1114).
+ */
+#ifndef RS_SIMPLIFY_H
+#define RS_SIMPLIFY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_ABI_VERSION 1
+
+enum rs_status {
+  RS_OK = 0,
+  RS_E_INVALID = -1,    /* malformed input (shape, unclean row, unknown prime, ...)          */
+  RS_E_OOM_DEVICE = -2, /* device allocation failed                                           */
+  RS_E_HIP = -3,        /* a HIP runtime call failed                                          */
+  RS_E_RCCL = -4,       /* reserved: collective failure (multi-GPU)                           */
+  RS_E_INTERNAL = -5,   /* an invariant the reference asserts was violated                    */
+  RS_E_NODEVICE = -6    /* no usable gfx950 device: the library never falls back to the CPU   */
+};
+
+/* program_structure/src/utils/constants.rs:3-13, the --prime names of circom/src/input_user.rs */
+enum rs_prime {
+  RS_PRIME_BN128 = 0,
+  RS_PRIME_BLS12381 = 1,
+  RS_PRIME_GOLDILOCKS = 2,
+  RS_PRIME_GRUMPKIN = 3,
+  RS_PRIME_PALLAS = 4,
+  RS_PRIME_VESTA = 5,
+  RS_PRIME_SECQ256R1 = 6,
+  RS_PRIME_BLS12377 = 7,
+  RS_PRIME_CUSTOM = 255
+};
+
+/* One CSR matrix of linear combinations (HashMap<usize, BigInt> per row in the reference). */
+typedef struct rs_lc {
+  uint64_t n_rows;
+  uint64_t nnz;
+  uint64_t *ptr; /* n_rows + 1 offsets                                         */
+  uint32_t *col; /* nnz signal ids                                             */
+  uint64_t *val; /* nnz * 4 limbs (little endian, canonical)                   */
+} rs_lc;
+
+/*
+ * The Simplifier bundle (constraint_list/src/lib.rs:110-129) as plain arrays.
+ *   cons_eq / eq / linear : Simplifier.{cons_equalities, equalities, linear} -- linear rows,
+ *                           only their C part (A = B = empty), in the reference's list order
+ *                           (DFS order of dag/src/map_to_constraint_list.rs:12-44).
+ *   nl_a / nl_b / nl_c    : the non-linear rows of the DAG encoding in EncodingIterator DFS
+ *                           order (constraint_list/src/lib.rs:65-108); same n_rows each.
+ *   forbidden             : Simplifier.forbidden = {0} u outputs u public inputs u custom-gate
+ *                           signals (dag/src/lib.rs:174, 179-204; map_to_constraint_list.rs:22-24).
+ */
+typedef struct rs_input {
+  uint32_t prime_id;     /* enum rs_prime                                                  */
+  uint64_t prime[4];     /* only read when prime_id == RS_PRIME_CUSTOM                      */
+  uint64_t max_signal;   /* Simplifier.max_signal (= number of labels)                      */
+  uint64_t n_pub_out;
+  uint64_t n_pub_in;
+  uint64_t n_priv_in;
+  uint64_t n_forbidden;
+  uint32_t *forbidden;
+  rs_lc cons_eq;
+  rs_lc eq;
+  rs_lc linear;
+  rs_lc nl_a;
+  rs_lc nl_b;
+  rs_lc nl_c;
+} rs_input;
+
+/* SimplificationFlags (dag/src/lib.rs:546-554) + execution knobs. */
+typedef struct rs_flags {
+  uint32_t flag_s;             /* --O1: no linear elimination (apply_linear = !flag_s)      */
+  uint32_t use_old_heuristics; /* --use_old_simplification_heuristics                        */
+  uint64_t no_rounds;          /* UINT64_MAX for --O2, N for --O2round N, 0 for --O1         */
+  uint32_t emit_substitution_log; /* --simplification_substitution (reserved)                */
+  int32_t device;              /* HIP device ordinal                                        */
+} rs_flags;
+
+/*
+ * Result: (ConstraintStorage, SignalMap, no_private_inputs_witness) of simplification().
+ * Constraints are in storage order with ORIGINAL signal ids (the caller applies label_to_wire,
+ * exactly like ConstraintList::r1cs does with apply_correspondence, r1cs_porting.rs:23-33).
+ */
+typedef struct rs_output {
+  uint64_t n_constraints;
+  rs_lc a, b, c;                  /* owned by the library; free with rs_output_free         */
+  uint64_t n_labels;              /* = max_signal                                           */
+  int64_t *label_to_wire;         /* n_labels entries, -1 = not a wire                      */
+  uint64_t n_wires;               /* = SignalMap.len()                                      */
+  uint64_t no_private_inputs_witness;
+} rs_output;
+
+/* Phase timings of the last rs_engine_run (milliseconds, HIP events + host clock). */
+typedef struct rs_stats {
+  double total_ms;             /* device-resident input -> device-resident output             */
+  double eq_ms;                /* eq + const-eq renaming                                     */
+  double cluster_ms;           /* union-find clustering (all rounds)                         */
+  double elim_ms;              /* per-cluster elimination + normalisation + composition      */
+  double subst_ms;             /* substitution application (non-linear rows, rounds >= 2)    */
+  double final_ms;             /* compaction, rebuild_witness, output assembly               */
+  double apply_kernel_ms;      /* device time of the dominant substitution kernel            */
+  uint64_t apply_kernel_launches;
+  uint64_t apply_bytes;        /* algorithmic bytes moved by that kernel (sum over launches) */
+  uint64_t rounds;             /* linear-elimination rounds executed                         */
+  uint64_t n_clusters;
+  uint64_t n_substitutions;
+  uint64_t max_cluster;
+} rs_stats;
+
+typedef struct rs_engine rs_engine;
+
+const char *rs_last_error(void);
+int rs_abi_version(void);
+
+/* One-shot: host input -> host output (H2D, simplification on the GPU, D2H). */
+int rs_simplify(const rs_input *in, const rs_flags *fl, rs_output **out);
+void rs_output_free(rs_output *out);
+
+/* Engine API used by the benchmark: stage the input in HBM once, run many times. */
+int rs_engine_create(int device, rs_engine **eng);
+int rs_engine_load(rs_engine *eng, const rs_input *in);   /* H2D copy of the host input        */
+int rs_engine_run(rs_engine *eng, const rs_flags *fl);    /* the timed region                   */
+int rs_engine_fetch(rs_engine *eng, rs_output **out);     /* D2H of the last result             */
+int rs_engine_stats(rs_engine *eng, rs_stats *st);
+void rs_engine_destroy(rs_engine *eng);
+
+/* --O0 .r1cs -> rs_input (host arrays owned by the library; free with rs_input_free).
+ * Classifies rows exactly like dag/src/map_to_constraint_list.rs:12-44. */
+int rs_read_r1cs_o0(const char *path, rs_input **in);
+void rs_input_free(rs_input *in);
+/* Writes the simplified .r1cs (constraint_list/src/r1cs_porting.rs:4-124). */
+int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out);
+/* Rewrites an --O0 .sym with the witness column of `out` (constraint_list/src/sym_porting.rs). */
+int rs_write_sym(const char *o0_sym, const char *path, const rs_output *out);
+
+/* Seeded synthetic --O0 systems for benchmarks/tests (see DESIGN.md "Workloads").
+ * kind: 0 = mixed (metric circuit), 1 = purely linear, 2 = chain (deep substitution chains). */
+int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id, rs_input **in);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS_SIMPLIFY_H */

@@ -1,0 +1,269 @@
+"""ctypes mirror of include/rs_simplify.h plus converters between oracle/pyref.py systems and the
+C ABI.  Shared by the oracle tests, the GPU parity tests and bench.py."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import random
+import sys
+from typing import List
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import pyref as R  # noqa: E402
+
+U64_MAX = (1 << 64) - 1
+PRIME_IDS = {"bn128": 0, "bls12381": 1, "goldilocks": 2, "grumpkin": 3, "pallas": 4,
+             "vesta": 5, "secq256r1": 6, "bls12377": 7}
+
+
+class RsLc(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("nnz", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
+                ("col", C.POINTER(C.c_uint32)), ("val", C.POINTER(C.c_uint64))]
+
+
+class RsInput(C.Structure):
+    _fields_ = [("prime_id", C.c_uint32), ("prime", C.c_uint64 * 4), ("max_signal", C.c_uint64),
+                ("n_pub_out", C.c_uint64), ("n_pub_in", C.c_uint64), ("n_priv_in", C.c_uint64),
+                ("n_forbidden", C.c_uint64), ("forbidden", C.POINTER(C.c_uint32)),
+                ("cons_eq", RsLc), ("eq", RsLc), ("linear", RsLc),
+                ("nl_a", RsLc), ("nl_b", RsLc), ("nl_c", RsLc)]
+
+
+class RsFlags(C.Structure):
+    _fields_ = [("flag_s", C.c_uint32), ("use_old_heuristics", C.c_uint32),
+                ("no_rounds", C.c_uint64), ("emit_substitution_log", C.c_uint32),
+                ("device", C.c_int32)]
+
+
+class RsOutput(C.Structure):
+    _fields_ = [("n_constraints", C.c_uint64), ("a", RsLc), ("b", RsLc), ("c", RsLc),
+                ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int64)),
+                ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64)]
+
+
+class RsStats(C.Structure):
+    _fields_ = [("total_ms", C.c_double), ("eq_ms", C.c_double), ("cluster_ms", C.c_double),
+                ("elim_ms", C.c_double), ("subst_ms", C.c_double), ("final_ms", C.c_double),
+                ("apply_kernel_ms", C.c_double), ("apply_kernel_launches", C.c_uint64),
+                ("apply_bytes", C.c_uint64), ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
+                ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
+
+
+def flags(level="O2", rounds=None, old=False, device=0) -> RsFlags:
+    f = RsFlags()
+    if level == "O1":
+        f.flag_s, f.no_rounds = 1, 0
+    elif level == "O2":
+        f.flag_s, f.no_rounds = 0, U64_MAX if rounds is None else rounds
+    else:
+        raise ValueError(level)
+    f.use_old_heuristics = 1 if old else 0
+    f.device = device
+    return f
+
+
+# --------------------------------------------------------------------------- pyref <-> C ABI
+def _limbs(v: int):
+    return [(v >> (64 * i)) & U64_MAX for i in range(4)]
+
+
+class _Block:
+    def __init__(self, maps: List[dict]):
+        ptr = [0]
+        cols, vals = [], []
+        for m in maps:
+            for k in sorted(m):
+                cols.append(k)
+                vals.extend(_limbs(m[k]))
+            ptr.append(len(cols))
+        self.ptr = np.array(ptr, dtype=np.uint64)
+        self.col = np.array(cols if cols else [0], dtype=np.uint32)
+        self.val = np.array(vals if vals else [0, 0, 0, 0], dtype=np.uint64)
+        self.lc = RsLc(len(maps), len(cols), self.ptr.ctypes.data_as(C.POINTER(C.c_uint64)),
+                       self.col.ctypes.data_as(C.POINTER(C.c_uint32)),
+                       self.val.ctypes.data_as(C.POINTER(C.c_uint64)))
+
+
+class InputHolder:
+    """Keeps the numpy arrays behind an RsInput alive."""
+
+    def __init__(self, sys_: "R.System", prime_name: str | None = None):
+        cons_eq, eq, lin, nonlin = R.classify(sys_)
+        self.blocks = [_Block([c.c for c in cons_eq]), _Block([c.c for c in eq]),
+                       _Block([c.c for c in lin]), _Block([c.a for c in nonlin]),
+                       _Block([c.b for c in nonlin]), _Block([c.c for c in nonlin])]
+        self.forb = np.array(sorted(sys_.forbidden), dtype=np.uint32)
+        inp = RsInput()
+        if prime_name is not None:
+            inp.prime_id = PRIME_IDS[prime_name]
+        else:
+            inp.prime_id = 255
+        for i, l in enumerate(_limbs(sys_.p)):
+            inp.prime[i] = l
+        inp.max_signal = sys_.max_signal
+        inp.n_pub_out, inp.n_pub_in, inp.n_priv_in = sys_.n_pub_out, sys_.n_pub_in, sys_.n_priv_in
+        inp.n_forbidden = len(self.forb)
+        inp.forbidden = self.forb.ctypes.data_as(C.POINTER(C.c_uint32))
+        inp.cons_eq, inp.eq, inp.linear, inp.nl_a, inp.nl_b, inp.nl_c = [b.lc for b in self.blocks]
+        self.inp = inp
+
+
+def _read_block(b: RsLc) -> List[dict]:
+    n = b.n_rows
+    if n == 0:
+        return []
+    ptr = np.ctypeslib.as_array(b.ptr, shape=(n + 1,))
+    nnz = int(ptr[n])
+    col = np.ctypeslib.as_array(b.col, shape=(max(nnz, 1),))
+    val = np.ctypeslib.as_array(b.val, shape=(max(nnz, 1) * 4,))
+    out = []
+    for r in range(n):
+        m = {}
+        for e in range(int(ptr[r]), int(ptr[r + 1])):
+            v = 0
+            for i in range(4):
+                v |= int(val[4 * e + i]) << (64 * i)
+            m[int(col[e])] = v
+        out.append(m)
+    return out
+
+
+def output_to_py(o: RsOutput):
+    """-> (list of pyref.Con, signal_map dict label->wire, n_wires, no_private_inputs_witness)."""
+    a, b, c = _read_block(o.a), _read_block(o.b), _read_block(o.c)
+    cons = [R.Con(a[i], b[i], c[i]) for i in range(o.n_constraints)]
+    l2w = np.ctypeslib.as_array(o.label_to_wire, shape=(max(o.n_labels, 1),))[: o.n_labels]
+    sm = {i: int(w) for i, w in enumerate(l2w) if w >= 0}
+    return cons, sm, int(o.n_wires), int(o.no_private_inputs_witness)
+
+
+def same_result(res: "R.Result", got) -> str | None:
+    """None if equal, else a description of the first difference."""
+    cons, sm, nw, npiw = got
+    if sm != res.signal_map:
+        return f"signal_map differs: {len(sm)} vs {len(res.signal_map)} wires"
+    if nw != len(res.signal_map):
+        return "n_wires differs"
+    if npiw != res.no_private_inputs_witness:
+        return f"no_private_inputs_witness {npiw} vs {res.no_private_inputs_witness}"
+    if len(cons) != len(res.constraints):
+        return f"#constraints {len(cons)} vs {len(res.constraints)}"
+    for i, (x, y) in enumerate(zip(cons, res.constraints)):
+        if (x.a, x.b, x.c) != (y.a, y.b, y.c):
+            return f"constraint {i} differs: {x} vs {y}"
+    return None
+
+
+# --------------------------------------------------------------------------- oracle library
+_ORACLE = None
+
+
+def oracle_lib():
+    global _ORACLE
+    if _ORACLE is None:
+        path = os.path.join(ROOT, "oracle", "_ref", "librefcpu.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        lib = C.CDLL(path)
+        lib.refcpu_simplify.argtypes = [C.POINTER(RsInput), C.POINTER(RsFlags), C.c_int,
+                                        C.POINTER(C.POINTER(RsOutput)), C.POINTER(C.c_double),
+                                        C.POINTER(C.c_uint64)]
+        lib.refcpu_simplify.restype = C.c_int
+        lib.refcpu_output_free.argtypes = [C.POINTER(RsOutput)]
+        lib.refcpu_last_error.restype = C.c_char_p
+        lib.refcpu_field_op.argtypes = [C.c_uint64 * 4, C.c_int, C.c_uint64 * 4, C.c_uint64 * 4,
+                                        C.c_uint64 * 4]
+        _ORACLE = lib
+    return _ORACLE
+
+
+def oracle_run(inp: RsInput, fl: RsFlags, threads=1):
+    lib = oracle_lib()
+    out = C.POINTER(RsOutput)()
+    ms = C.c_double()
+    rounds = C.c_uint64()
+    rc = lib.refcpu_simplify(C.byref(inp), C.byref(fl), threads, C.byref(out), C.byref(ms),
+                             C.byref(rounds))
+    if rc != 0:
+        raise RuntimeError(f"refcpu rc={rc}: {lib.refcpu_last_error().decode()}")
+    try:
+        return output_to_py(out.contents), ms.value, rounds.value
+    finally:
+        lib.refcpu_output_free(out)
+
+
+# --------------------------------------------------------------------------- random systems
+def gen_system(seed: int, p: int, n_sig: int = 60, n_rows: int = 80, n_out: int = 2,
+               n_pub: int = 2, big_cluster: int = 0, density: float = 1.0) -> "R.System":
+    """Seeded random --O0 system that exercises every branch of the path: eq clusters of size 1
+    and > 1 with forbidden ends, duplicate/forbidden constant equalities, linear clusters for
+    process_3 and (big_cluster >= 350) process_4, non-linear rows that turn linear in round 1 and
+    in later rounds, constant-A reductions and coefficient cancellations (small p)."""
+    rng = random.Random(seed)
+    S = n_sig + 1
+    n_priv = max(1, min(4, n_sig - n_out - n_pub))
+
+    def coef():
+        r = rng.random()
+        if r < 0.35:
+            return 1
+        if r < 0.55:
+            return p - 1
+        if r < 0.7:
+            return pow(2, rng.randrange(1, 8), p)
+        return rng.randrange(1, p)
+
+    def sig():
+        return rng.randrange(1, S)
+
+    def lc(nmin, nmax, const_prob=0.3):
+        m = {}
+        for _ in range(rng.randint(nmin, nmax)):
+            m[sig()] = coef()
+        if rng.random() < const_prob:
+            m[0] = coef()
+        return {k: v for k, v in m.items() if v % p}
+
+    rows = []
+    for _ in range(n_rows):
+        r = rng.random()
+        if r < 0.22:        # equality x - y (scaled)
+            x, y = sig(), sig()
+            if x == y:
+                continue
+            k = coef()
+            rows.append(R.Con({}, {}, {x: k, y: (p - k) % p}))
+        elif r < 0.30:      # constant equality
+            m = {sig(): coef()}
+            if rng.random() < 0.6:
+                m[0] = coef()
+            rows.append(R.Con({}, {}, m))
+        elif r < 0.62:      # linear
+            m = lc(2, int(2 + 4 * density))
+            if len([k for k in m if k]) >= 2:
+                rows.append(R.Con({}, {}, m))
+        else:               # quadratic
+            a = lc(1, 2, 0.15)
+            b = lc(1, 3, 0.2)
+            if rng.random() < 0.08:
+                a = {0: coef()}
+            c = lc(0, 3, 0.2)
+            if a or b:
+                rows.append(R.Con(a, b, c))
+    if big_cluster:
+        base = rng.randrange(1, max(2, S - 8))
+        for i in range(big_cluster):
+            m = {}
+            for _ in range(rng.randint(2, 4)):
+                m[1 + (base + rng.randrange(0, 24) + i // 2) % (S - 1)] = coef()
+            if rng.random() < 0.3:
+                m[0] = coef()
+            m = {k: v for k, v in m.items() if v}
+            if len([k for k in m if k]) >= 3:
+                rows.append(R.Con({}, {}, m))
+    forb = {0} | set(range(1, n_out + n_pub + 1))
+    return R.System(p, S, n_out, n_pub, n_priv, forb, rows)
