@@ -1,0 +1,12 @@
+"""circom_cvm_amd: MI355X-native R1CS constraint simplification for circom (--O1/--O2).
+
+The product is librs_simplify.so (HIP kernels for gfx950 + a C++ host orchestrator behind the C ABI
+of include/rs_simplify.h).  This package is the thin Python mirror of the reference's
+Simplifier -> ConstraintList interface (constraint_list/src/lib.rs:110-202) used by the tests and
+the benchmark."""
+from .abi import (Engine, Input, Output, RsError, RsFlags, RsInput, RsOutput, RsStats, check, lib,
+                  make_flags)
+from .simplifier import ConstraintList, Simplifier
+
+__all__ = ["Engine", "Input", "Output", "RsError", "RsFlags", "RsInput", "RsOutput", "RsStats",
+           "check", "lib", "make_flags", "Simplifier", "ConstraintList"]

@@ -1,0 +1,212 @@
+"""ctypes binding of include/rs_simplify.h (librs_simplify.so, built in-tree for gfx950).
+
+The library is the product: there is no Python or CPU fallback.  Loading fails loudly when the
+shared object is missing, and every compute entry point returns RS_E_NODEVICE without a gfx950
+GPU."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "librs_simplify.so")
+
+U64_MAX = (1 << 64) - 1
+PRIME_IDS = {"bn128": 0, "bls12381": 1, "goldilocks": 2, "grumpkin": 3, "pallas": 4,
+             "vesta": 5, "secq256r1": 6, "bls12377": 7}
+RS_PRIME_CUSTOM = 255
+ERRORS = {0: "RS_OK", -1: "RS_E_INVALID", -2: "RS_E_OOM_DEVICE", -3: "RS_E_HIP",
+          -4: "RS_E_RCCL", -5: "RS_E_INTERNAL", -6: "RS_E_NODEVICE"}
+
+
+class RsLc(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("nnz", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
+                ("col", C.POINTER(C.c_uint32)), ("val", C.POINTER(C.c_uint64))]
+
+
+class RsInput(C.Structure):
+    _fields_ = [("prime_id", C.c_uint32), ("prime", C.c_uint64 * 4), ("max_signal", C.c_uint64),
+                ("n_pub_out", C.c_uint64), ("n_pub_in", C.c_uint64), ("n_priv_in", C.c_uint64),
+                ("n_forbidden", C.c_uint64), ("forbidden", C.POINTER(C.c_uint32)),
+                ("cons_eq", RsLc), ("eq", RsLc), ("linear", RsLc),
+                ("nl_a", RsLc), ("nl_b", RsLc), ("nl_c", RsLc)]
+
+
+class RsFlags(C.Structure):
+    _fields_ = [("flag_s", C.c_uint32), ("use_old_heuristics", C.c_uint32),
+                ("no_rounds", C.c_uint64), ("emit_substitution_log", C.c_uint32),
+                ("device", C.c_int32)]
+
+
+class RsOutput(C.Structure):
+    _fields_ = [("n_constraints", C.c_uint64), ("a", RsLc), ("b", RsLc), ("c", RsLc),
+                ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int64)),
+                ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64)]
+
+
+class RsStats(C.Structure):
+    _fields_ = [("total_ms", C.c_double), ("eq_ms", C.c_double), ("cluster_ms", C.c_double),
+                ("elim_ms", C.c_double), ("subst_ms", C.c_double), ("final_ms", C.c_double),
+                ("apply_kernel_ms", C.c_double), ("apply_kernel_launches", C.c_uint64),
+                ("apply_bytes", C.c_uint64), ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
+                ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# (name, restype, argtypes) of every symbol include/rs_simplify.h declares
+SYMBOLS = [
+    ("rs_last_error", C.c_char_p, []),
+    ("rs_abi_version", C.c_int, []),
+    ("rs_simplify", C.c_int, [C.POINTER(RsInput), C.POINTER(RsFlags), C.POINTER(C.POINTER(RsOutput))]),
+    ("rs_output_free", None, [C.POINTER(RsOutput)]),
+    ("rs_engine_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("rs_engine_load", C.c_int, [C.c_void_p, C.POINTER(RsInput)]),
+    ("rs_engine_run", C.c_int, [C.c_void_p, C.POINTER(RsFlags)]),
+    ("rs_engine_fetch", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(RsOutput))]),
+    ("rs_engine_stats", C.c_int, [C.c_void_p, C.POINTER(RsStats)]),
+    ("rs_engine_destroy", None, [C.c_void_p]),
+    ("rs_read_r1cs_o0", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(RsInput))]),
+    ("rs_input_free", None, [C.POINTER(RsInput)]),
+    ("rs_write_r1cs", C.c_int, [C.c_char_p, C.POINTER(RsInput), C.POINTER(RsOutput)]),
+    ("rs_write_sym", C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(RsOutput)]),
+    ("rs_synth", C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(RsInput))]),
+]
+
+_LIB = None
+
+
+class RsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    """The loaded librs_simplify.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SYMBOLS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int):
+    if rc != 0:
+        raise RsError(rc, lib().rs_last_error().decode(errors="replace"))
+
+
+def make_flags(level: str = "O2", rounds: int | None = None, old: bool = False, device: int = 0) -> RsFlags:
+    """--O1 / --O2 / --O2round N (circom/src/input_user.rs:286-306)."""
+    f = RsFlags()
+    if level == "O1" or rounds == 0:
+        f.flag_s, f.no_rounds = 1, 0
+    elif level == "O2":
+        f.flag_s, f.no_rounds = 0, U64_MAX if rounds is None else rounds
+    else:
+        raise ValueError(level)
+    f.use_old_heuristics = 1 if old else 0
+    f.device = device
+    return f
+
+
+class Engine:
+    """HBM-resident simplification engine (rs_engine_*)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        check(lib().rs_engine_create(device, C.byref(self._h)))
+
+    def load(self, inp: RsInput):
+        check(lib().rs_engine_load(self._h, C.byref(inp)))
+
+    def run(self, flags: RsFlags):
+        check(lib().rs_engine_run(self._h, C.byref(flags)))
+
+    def stats(self) -> RsStats:
+        s = RsStats()
+        check(lib().rs_engine_stats(self._h, C.byref(s)))
+        return s
+
+    def fetch(self):
+        out = C.POINTER(RsOutput)()
+        check(lib().rs_engine_fetch(self._h, C.byref(out)))
+        return Output(out)
+
+    def close(self):
+        if self._h:
+            lib().rs_engine_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Output:
+    """Owns an rs_output*."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    @property
+    def c(self) -> RsOutput:
+        return self.ptr.contents
+
+    def free(self):
+        if self.ptr:
+            lib().rs_output_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Input:
+    """Owns an rs_input* made by the library (r1cs reader or synthetic generator)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    @property
+    def c(self) -> RsInput:
+        return self.ptr.contents
+
+    @staticmethod
+    def read_r1cs(path: str) -> "Input":
+        p = C.POINTER(RsInput)()
+        check(lib().rs_read_r1cs_o0(path.encode(), C.byref(p)))
+        return Input(p)
+
+    @staticmethod
+    def synth(kind: int, rows: int, seed: int, prime: str = "bn128") -> "Input":
+        p = C.POINTER(RsInput)()
+        check(lib().rs_synth(kind, rows, seed, PRIME_IDS[prime], C.byref(p)))
+        return Input(p)
+
+    def rows(self) -> int:
+        c = self.c
+        return int(c.cons_eq.n_rows + c.eq.n_rows + c.linear.n_rows + c.nl_a.n_rows)
+
+    def free(self):
+        if self.ptr:
+            lib().rs_input_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

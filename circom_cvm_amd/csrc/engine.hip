@@ -1,0 +1,1375 @@
+// engine.hip -- librs_simplify: the MI355X back end of circom's --O1/--O2 simplification.
+//
+// Host orchestration of constraint_list/src/constraint_simplification.rs:442-730 around the HIP
+// kernels of kernels.hpp.  Every step says which part of simplification() it restates.  All
+// field arithmetic runs on the GPU; the host keeps the ordered bookkeeping the reference keeps
+// in Rust collections (cluster arena order, the non-linear signal map of rounds >= 2) and the
+// lists of forbidden-only constraints (lconst), which only ever need fix_constraint.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include <cstring>
+#include <rocprim/device/device_scan.hpp>
+
+#include "host_common.hpp"
+#include "kernels.hpp"
+
+namespace rs {
+
+const uint64_t kPrimes[8][4] = {
+    {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL, 0x30644e72e131a029ULL},
+    {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL, 0x73eda753299d7d48ULL},
+    {0xffffffff00000001ULL, 0, 0, 0},
+    {0x3c208c16d87cfd47ULL, 0x97816a916871ca8dULL, 0xb85045b68181585dULL, 0x30644e72e131a029ULL},
+    {0x992d30ed00000001ULL, 0x224698fc094cf91bULL, 0x0000000000000000ULL, 0x4000000000000000ULL},
+    {0x8c46eb2100000001ULL, 0x224698fc0994a8ddULL, 0x0000000000000000ULL, 0x4000000000000000ULL},
+    {0xffffffffffffffffULL, 0x00000000ffffffffULL, 0x0000000000000000ULL, 0xffffffff00000001ULL},
+    {0x0a11800000000001ULL, 0x59aa76fed0000001ULL, 0x60b44d1e5c37b001ULL, 0x12ab655e9a2ca556ULL}};
+
+static thread_local std::string g_err;
+void set_error(const std::string &m) { g_err = m; }
+
+struct RsError : std::runtime_error {
+  int code;
+  RsError(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+#define HC(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess)                                                                      \
+      throw RsError(e_ == hipErrorOutOfMemory ? RS_E_OOM_DEVICE : RS_E_HIP,                   \
+                    std::string(#x) + ": " + hipGetErrorString(e_));                          \
+  } while (0)
+
+static inline double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------ device buffer arena
+struct Arena {
+  struct B {
+    void *p = nullptr;
+    size_t cap = 0;
+  };
+  std::map<std::string, B> bufs;
+  template <class T>
+  T *get(const std::string &name, size_t n) {
+    size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    B &b = bufs[name];
+    if (b.cap < bytes) {
+      if (b.p) HC(hipFree(b.p));
+      size_t cap = std::max(bytes, b.cap + b.cap / 4);
+      HC(hipMalloc(&b.p, cap));
+      b.cap = cap;
+    }
+    return (T *)b.p;
+  }
+  ~Arena() {
+    for (auto &kv : bufs)
+      if (kv.second.p) (void)hipFree(kv.second.p);
+  }
+};
+
+template <class K, class... Args>
+static void launch(hipStream_t st, K kernel, uint64_t n, Args... args) {
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks == 0) blocks = 1;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, st, args...);
+  HC(hipGetLastError());
+}
+
+// host view of ragged rows (keys only unless vals requested)
+struct HostRows {
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> len;
+  std::vector<uint32_t> key;
+};
+
+struct HostCon {  // canonical, sorted keys
+  std::vector<uint32_t> k[3];
+  std::vector<uint64_t> v[3];
+};
+
+}  // namespace rs
+
+using namespace rs;
+
+struct rs_engine {
+  int device = 0;
+  hipStream_t st = nullptr;
+  Arena A;
+  bool loaded = false;
+  bool have_result = false;
+  FieldP F;
+  uint64_t prime[4];
+  uint32_t prime_id = 0;
+  uint64_t S = 0, n_pub_out = 0, n_pub_in = 0, n_priv_in = 0;
+  std::vector<uint32_t> forbidden;
+  // loaded input (canonical, rows sorted)
+  struct Blk {
+    uint64_t *ptr = nullptr;
+    uint32_t *key = nullptr;
+    Fe *val = nullptr;
+    uint64_t n = 0, nnz = 0;
+  } ce, eq, lin, na, nb, nc;
+  // result
+  uint64_t out_n_dev = 0;  // constraints gathered on device
+  uint64_t out_nnz[3] = {0, 0, 0};
+  std::vector<HostCon> out_host_tail;  // lconst rows appended after the device rows
+  uint64_t n_wires = 0, npiw = 0;
+  rs_stats stats{};
+  std::vector<int32_t> sig2cl;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace rs {
+
+static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, const char *name) {
+  dst.n = src.n_rows;
+  dst.nnz = src.n_rows ? src.ptr[src.n_rows] : 0;
+  std::string nm(name);
+  dst.ptr = E->A.get<uint64_t>(nm + ".ptr", dst.n + 1);
+  dst.key = E->A.get<uint32_t>(nm + ".key", dst.nnz);
+  dst.val = E->A.get<Fe>(nm + ".val", dst.nnz);
+  if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, E->st));
+  else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), E->st));
+  if (dst.nnz) {
+    HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, E->st));
+    HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, E->st));
+  }
+}
+
+// ---------------------------------------------------------------- scans
+static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, uint64_t n, const char *tag) {
+  if (n == 0) return 0;
+  size_t tb = 0;
+  HC(rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), E->st));
+  void *tmp = E->A.get<uint8_t>(std::string("scan.tmp.") + tag, tb);
+  HC(rocprim::exclusive_scan(tmp, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), E->st));
+  uint64_t last_in = 0, last_out = 0;
+  HC(hipMemcpyAsync(&last_in, in + n - 1, 8, hipMemcpyDeviceToHost, E->st));
+  HC(hipMemcpyAsync(&last_out, out + n - 1, 8, hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+  return last_in + last_out;
+}
+
+__global__ void k_u32_to_u64(const uint32_t *in, uint64_t *out, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = in[i];
+}
+__global__ void k_iota_u32(uint32_t *p, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) p[i] = (uint32_t)i;
+}
+// copy rows (ptr CSR, canonical) into a ragged layout with `extra` spare slots per row (Montgomery)
+__global__ void k_make_ragged(FieldP F, const uint64_t *ptr, const uint32_t *key, const Fe *val, uint64_t n,
+                              uint64_t extra, uint64_t *off, uint32_t *len, uint32_t *okey, Fe *oval) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    uint64_t b = ptr[r], e = ptr[r + 1];
+    uint64_t o = b + extra * r;
+    off[r] = o;
+    len[r] = (uint32_t)(e - b);
+    for (uint64_t i = b; i < e; ++i) {
+      okey[o + (i - b)] = key[i];
+      oval[o + (i - b)] = fto_mont(F, val[i]);
+    }
+  }
+}
+// view of selected rows: off/len gathered from a source view
+__global__ void k_view_rows(const uint64_t *soff, const uint32_t *slen, const uint32_t *ids, uint64_t n,
+                            uint64_t *off, uint32_t *len) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    off[i] = soff[ids[i]];
+    len[i] = slen[ids[i]];
+  }
+}
+__global__ void k_set_offsets(const uint64_t *base_scan, uint64_t base, uint64_t *off, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) off[i] = base + base_scan[i];
+}
+__global__ void k_flag_linear(const uint32_t *la, const uint32_t *lb, uint64_t n, uint64_t *flag_lin, uint64_t *flag_nl) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    bool lin = la[i] == 0 && lb[i] == 0;
+    flag_lin[i] = lin ? 1 : 0;
+    flag_nl[i] = lin ? 0 : 1;
+  }
+}
+__global__ void k_scatter_ids(const uint64_t *flag, const uint64_t *pos, uint64_t n, uint32_t *ids) {
+  for (uint64_t i = gtid(); i < n; i += gstride())
+    if (flag[i]) ids[pos[i]] = (uint32_t)i;
+}
+__global__ void k_set_rank(const uint32_t *sig, const int32_t *rank, uint64_t n, int32_t *rank_of) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) rank_of[sig[i]] = rank[i];
+}
+__global__ void k_turn_flags(const int32_t *turn, uint64_t n, uint64_t *flag) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) flag[i] = turn[i] >= 0 ? 1 : 0;
+}
+__global__ void k_commit_round(const uint8_t *touched, const int32_t *turn, uint64_t n, DRows a, DRows b, DRows c,
+                               DRows oa, DRows ob, DRows oc) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    if (!touched[r]) continue;
+    if (turn[r] >= 0) {  // extracted: the linear content is kept in the round's view; storage emptied
+      a.len[r] = 0;
+      b.len[r] = 0;
+      c.off[r] = oc.off[r];
+      c.len[r] = oc.len[r];
+      continue;
+    }
+    a.off[r] = oa.off[r]; a.len[r] = oa.len[r];
+    b.off[r] = ob.off[r]; b.len[r] = ob.len[r];
+    c.off[r] = oc.off[r]; c.len[r] = oc.len[r];
+  }
+}
+__global__ void k_zero_c(const uint32_t *ids, uint64_t n, uint32_t *clen) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) clen[ids[i]] = 0;
+}
+__global__ void k_nonempty_flags(const uint32_t *la, const uint32_t *lb, const uint32_t *lc, uint64_t n, uint64_t *flag) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) flag[i] = (la[i] | lb[i] | lc[i]) ? 1 : 0;
+}
+
+__global__ void k_compact_keys(DRows V, const uint64_t *doff, uint32_t *out) {
+  for (uint64_t r = gtid(); r < V.n; r += gstride())
+    for (uint32_t i = 0; i < V.len[r]; ++i) out[doff[r] + i] = V.key[V.off[r] + i];
+}
+
+// ---------------------------------------------------------------- host clustering
+// build_clusters (constraint_simplification.rs:45-99): arena order + dest ++ src lists.
+static void host_clusters(rs_engine *E, const HostRows &R, uint64_t n, std::vector<uint32_t> &perm,
+                          std::vector<uint64_t> &cl_off) {
+  std::vector<int32_t> &sig2cl = E->sig2cl;
+  if (sig2cl.size() < E->S) sig2cl.assign(E->S, -1);
+  std::vector<int32_t> head, tail, c2c, next(n, -1);
+  std::vector<uint32_t> touched;
+  head.reserve(n);
+  tail.reserve(n);
+  c2c.reserve(n);
+  auto findr = [&](int32_t org) {
+    int32_t cur = org;
+    while (cur != c2c[cur]) cur = c2c[cur];
+    while (org != cur) {
+      int32_t nx = c2c[org];
+      c2c[org] = cur;
+      org = nx;
+    }
+    return cur;
+  };
+  for (uint64_t r = 0; r < n; ++r) {
+    uint32_t L = R.len[r];
+    if (L == 0) continue;
+    const uint32_t *k = R.key.data() + R.off[r];
+    int32_t dest = (int32_t)head.size();
+    head.push_back((int32_t)r);
+    tail.push_back((int32_t)r);
+    c2c.push_back(dest);
+    for (uint32_t i = 0; i < L; ++i) {  // keys sorted & unique; skip the constant key
+      uint32_t s = k[i];
+      if (s == 0) continue;
+      int32_t prev = sig2cl[s];
+      if (prev < 0) touched.push_back(s);
+      sig2cl[s] = dest;
+      if (prev >= 0) {
+        int32_t cd = findr(dest), cs = findr(prev);
+        if (cs != cd) {
+          next[tail[cd]] = head[cs];
+          tail[cd] = tail[cs];
+          head[cs] = -1;
+          c2c[cs] = cd;
+        }
+      }
+    }
+  }
+  for (uint32_t s : touched) sig2cl[s] = -1;
+  perm.clear();
+  cl_off.clear();
+  cl_off.push_back(0);
+  for (size_t slot = 0; slot < head.size(); ++slot) {
+    if (head[slot] < 0) continue;
+    for (int32_t r = head[slot]; r >= 0; r = next[r]) perm.push_back((uint32_t)r);
+    cl_off.push_back(perm.size());
+  }
+}
+
+// D2H of the keys of a ragged view (C parts)
+static void fetch_keys(rs_engine *E, const DRows &V, HostRows &H) {
+  H.off.resize(V.n);
+  H.len.resize(V.n);
+  if (V.n == 0) return;
+  HC(hipMemcpyAsync(H.off.data(), V.off, 8 * V.n, hipMemcpyDeviceToHost, E->st));
+  HC(hipMemcpyAsync(H.len.data(), V.len, 4 * V.n, hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+  // compact into a dense key array: gather on device
+  uint64_t tot = 0;
+  std::vector<uint64_t> doff(V.n);
+  for (uint64_t r = 0; r < V.n; ++r) { doff[r] = tot; tot += H.len[r]; }
+  H.key.resize(tot);
+  if (tot == 0) { for (uint64_t r = 0; r < V.n; ++r) H.off[r] = doff[r]; return; }
+  uint64_t *d_doff = E->A.get<uint64_t>("fk.doff", V.n);
+  uint32_t *d_key = E->A.get<uint32_t>("fk.key", tot);
+  HC(hipMemcpyAsync(d_doff, doff.data(), 8 * V.n, hipMemcpyHostToDevice, E->st));
+  launch(E->st, k_compact_keys, V.n, V, (const uint64_t *)d_doff, d_key);
+  HC(hipMemcpyAsync(H.key.data(), d_key, 4 * tot, hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+  H.off = doff;
+}
+
+// D2H canonical content of pool maps (leftovers or RHS)
+static void fetch_pool_maps(rs_engine *E, const std::vector<uint64_t> &off, const std::vector<uint32_t> &len,
+                            const uint32_t *pk, const Fe *pv, std::vector<uint32_t> &keys, std::vector<uint64_t> &vals,
+                            std::vector<uint64_t> &optr) {
+  uint64_t n = off.size();
+  optr.assign(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) optr[i + 1] = optr[i] + len[i];
+  uint64_t tot = optr[n];
+  keys.resize(tot);
+  vals.resize(4 * tot);
+  if (tot == 0) return;
+  uint64_t *d_off = E->A.get<uint64_t>("fp.off", n);
+  uint32_t *d_len = E->A.get<uint32_t>("fp.len", n);
+  uint64_t *d_optr = E->A.get<uint64_t>("fp.optr", n + 1);
+  uint32_t *d_k = E->A.get<uint32_t>("fp.k", tot);
+  uint64_t *d_v = E->A.get<uint64_t>("fp.v", 4 * tot);
+  HC(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, E->st));
+  HC(hipMemcpyAsync(d_len, len.data(), 4 * n, hipMemcpyHostToDevice, E->st));
+  HC(hipMemcpyAsync(d_optr, optr.data(), 8 * (n + 1), hipMemcpyHostToDevice, E->st));
+  launch(E->st, k_pool_to_canon, n, E->F, (const uint64_t *)d_off, (const uint32_t *)d_len, (const uint64_t *)d_optr, n,
+         pk, pv, d_k, d_v);
+  HC(hipMemcpyAsync(keys.data(), d_k, 4 * tot, hipMemcpyDeviceToHost, E->st));
+  HC(hipMemcpyAsync(vals.data(), d_v, 32 * tot, hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+}
+
+static bool is_zero4(const uint64_t *v) { return (v[0] | v[1] | v[2] | v[3]) == 0; }
+
+// fix_constraint for a host lconst row (always linear: only zero removal)
+static void host_fix(HostCon &c) {
+  for (int q = 0; q < 3; ++q) {
+    size_t w = 0;
+    for (size_t i = 0; i < c.k[q].size(); ++i)
+      if (!is_zero4(&c.v[q][4 * i])) {
+        c.k[q][w] = c.k[q][i];
+        for (int t = 0; t < 4; ++t) c.v[q][4 * w + t] = c.v[q][4 * i + t];
+        ++w;
+      }
+    c.k[q].resize(w);
+    c.v[q].resize(4 * w);
+  }
+  if (c.k[0].empty() || c.k[1].empty()) {
+    c.k[0].clear(); c.v[0].clear();
+    c.k[1].clear(); c.v[1].clear();
+  }
+}
+
+// ---------------------------------------------------------------- elimination driver
+struct ElimOut {
+  uint64_t n_clusters = 0;
+  std::vector<uint64_t> cl_off;
+  std::vector<uint32_t> n_sub, n_left;
+};
+
+struct Pool {
+  uint32_t *pk = nullptr;
+  Fe *pv = nullptr;
+  unsigned long long *top = nullptr;
+  uint64_t cap = 0;
+};
+
+static Pool get_pool(rs_engine *E, uint64_t want) {
+  Pool P;
+  P.cap = want;
+  P.pk = E->A.get<uint32_t>("pool.k", want);
+  P.pv = E->A.get<Fe>("pool.v", want);
+  P.top = E->A.get<unsigned long long>("pool.top", 1);
+  return P;
+}
+
+// Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
+// the arena hold the substitutions (h_*) and leftovers (l_*), sub_of/deleted are updated.
+static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
+                                      int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted) {
+  double t0 = now_ms();
+  HostRows H;
+  fetch_keys(E, view, H);
+  std::vector<uint32_t> perm;
+  host_clusters(E, H, view.n, perm, eo.cl_off);
+  eo.n_clusters = eo.cl_off.size() - 1;
+  E->stats.n_clusters += eo.n_clusters;
+  for (uint64_t c = 0; c < eo.n_clusters; ++c)
+    E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, eo.cl_off[c + 1] - eo.cl_off[c]);
+  double t1 = now_ms();
+  E->stats.cluster_ms += t1 - t0;
+  uint64_t n_slots = perm.size();
+  uint32_t *d_perm = E->A.get<uint32_t>("el.perm", n_slots);
+  uint64_t *d_cl = E->A.get<uint64_t>("el.cl", eo.n_clusters + 1);
+  if (n_slots) HC(hipMemcpyAsync(d_perm, perm.data(), 4 * n_slots, hipMemcpyHostToDevice, E->st));
+  HC(hipMemcpyAsync(d_cl, eo.cl_off.data(), 8 * (eo.n_clusters + 1), hipMemcpyHostToDevice, E->st));
+  uint64_t tot_nnz = 0;
+  for (uint64_t i = 0; i < n_slots; ++i) tot_nnz += H.len[perm[i]];
+  uint64_t want = std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots));
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    P = get_pool(E, want);
+    HC(hipMemsetAsync(P.top, 0, 8, E->st));
+    HC(hipMemsetAsync(d_err, 0, 4, E->st));
+    ElimArgs a;
+    a.F = E->F;
+    a.rows = view;
+    a.perm = d_perm;
+    a.cl_off = d_cl;
+    a.n_clusters = eo.n_clusters;
+    a.forb = d_forb;
+    a.old_heur = old_heur;
+    a.holder_idx = E->A.get<int32_t>("el.holder_idx", E->S);
+    a.occ = E->A.get<int32_t>("el.occ", E->S);
+    a.rep_pos = E->A.get<int32_t>("el.rep_pos", E->S);
+    a.noov = E->A.get<int32_t>("el.noov", E->S);
+    a.del = E->A.get<uint8_t>("el.del", E->S);
+    a.h_sig = E->A.get<uint32_t>("el.h_sig", n_slots);
+    a.h_coef = E->A.get<Fe>("el.h_coef", n_slots);
+    a.h_off = E->A.get<uint64_t>("el.h_off", n_slots);
+    a.h_len = E->A.get<uint32_t>("el.h_len", n_slots);
+    a.tmp = E->A.get<uint32_t>("el.tmp", n_slots);
+    a.ftmp = E->A.get<Fe>("el.ftmp", n_slots);
+    a.dead = E->A.get<uint8_t>("el.dead", n_slots);
+    a.order = E->A.get<uint32_t>("el.order", n_slots);
+    a.l_off = E->A.get<uint64_t>("el.l_off", n_slots);
+    a.l_len = E->A.get<uint32_t>("el.l_len", n_slots);
+    a.n_sub = E->A.get<uint32_t>("el.n_sub", eo.n_clusters);
+    a.n_left = E->A.get<uint32_t>("el.n_left", eo.n_clusters);
+    a.sub_of = sub_of;
+    a.deleted = deleted;
+    a.pk = P.pk;
+    a.pv = P.pv;
+    a.pool_top = P.top;
+    a.pool_cap = P.cap;
+    a.err = d_err;
+    if (eo.n_clusters) {
+      uint64_t blocks = (eo.n_clusters + 63) / 64;
+      hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a);
+      HC(hipGetLastError());
+    }
+    int err = 0;
+    HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
+    HC(hipStreamSynchronize(E->st));
+    if (err & 8) { want *= 2; continue; }
+    if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
+    eo.n_sub.resize(eo.n_clusters);
+    eo.n_left.resize(eo.n_clusters);
+    if (eo.n_clusters) {
+      HC(hipMemcpyAsync(eo.n_sub.data(), a.n_sub, 4 * eo.n_clusters, hipMemcpyDeviceToHost, E->st));
+      HC(hipMemcpyAsync(eo.n_left.data(), a.n_left, 4 * eo.n_clusters, hipMemcpyDeviceToHost, E->st));
+      HC(hipStreamSynchronize(E->st));
+    }
+    for (auto x : eo.n_sub) E->stats.n_substitutions += x;
+    E->stats.elim_ms += now_ms() - t1;
+    return;
+  }
+  throw RsError(RS_E_OOM_DEVICE, "substitution pool exhausted");
+}
+
+// leftovers (cluster order, then push order) -> host lconst
+static void collect_leftovers(rs_engine *E, const ElimOut &eo, const Pool &P, std::vector<HostCon> &lconst) {
+  std::vector<uint64_t> slots;
+  for (uint64_t c = 0; c < eo.n_clusters; ++c)
+    for (uint32_t i = 0; i < eo.n_left[c]; ++i) slots.push_back(eo.cl_off[c] + i);
+  if (slots.empty()) return;
+  uint64_t n = slots.size();
+  std::vector<uint64_t> all_off(eo.cl_off.back());
+  std::vector<uint32_t> all_len(eo.cl_off.back());
+  HC(hipMemcpyAsync(all_off.data(), E->A.get<uint64_t>("el.l_off", 1), 8 * all_off.size(), hipMemcpyDeviceToHost, E->st));
+  HC(hipMemcpyAsync(all_len.data(), E->A.get<uint32_t>("el.l_len", 1), 4 * all_len.size(), hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+  std::vector<uint64_t> off(n);
+  std::vector<uint32_t> len(n);
+  for (uint64_t i = 0; i < n; ++i) { off[i] = all_off[slots[i]]; len[i] = all_len[slots[i]]; }
+  std::vector<uint32_t> keys;
+  std::vector<uint64_t> vals, optr;
+  fetch_pool_maps(E, off, len, P.pk, P.pv, keys, vals, optr);
+  for (uint64_t i = 0; i < n; ++i) {
+    HostCon c;
+    c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
+    c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
+    lconst.push_back(std::move(c));
+  }
+}
+
+// ---------------------------------------------------------------- the run
+static void engine_run(rs_engine *E, const rs_flags *fl) {
+  const uint64_t S = E->S;
+  hipStream_t st = E->st;
+  E->stats = rs_stats{};
+  double T0 = now_ms();
+  bool apply_linear = !fl->flag_s;
+  uint64_t no_rounds = fl->no_rounds;
+  Arena &A = E->A;
+  int *d_err = A.get<int>("err", 1);
+  HC(hipMemsetAsync(d_err, 0, 4, st));
+
+  // forbidden bitmap, deleted, scratch defaults
+  uint8_t *d_forb = A.get<uint8_t>("forb", S);
+  uint8_t *d_deleted = A.get<uint8_t>("deleted", S);
+  HC(hipMemsetAsync(d_forb, 0, S, st));
+  HC(hipMemsetAsync(d_deleted, 0, S, st));
+  {
+    uint32_t *d_fl = A.get<uint32_t>("forb.list", E->forbidden.size());
+    HC(hipMemcpyAsync(d_fl, E->forbidden.data(), 4 * E->forbidden.size(), hipMemcpyHostToDevice, st));
+    launch(st, k_mark_list, E->forbidden.size(), (const uint32_t *)d_fl, (uint64_t)E->forbidden.size(), d_forb);
+  }
+  for (const char *nm : {"el.holder_idx", "el.occ", "el.noov", "el.rep_pos"})
+    HC(hipMemsetAsync(A.get<int32_t>(nm, S), 0xff, 4 * S, st));
+  HC(hipMemsetAsync(A.get<uint8_t>("el.del", S), 0, S, st));
+  int32_t *sub_of = A.get<int32_t>("sub_of", S);
+  HC(hipMemsetAsync(sub_of, 0xff, 4 * S, st));
+
+  std::vector<HostCon> lconst;
+
+  // ======================= eq_simplification (:198-251) + renaming of linear / cons_eq rows
+  int32_t *eq_rep = A.get<int32_t>("eq_rep", S);
+  HC(hipMemsetAsync(eq_rep, 0xff, 4 * S, st));
+  {
+    uint32_t *uf = A.get<uint32_t>("uf", S);
+    uint32_t *cnt = A.get<uint32_t>("eq.cnt", S);
+    int32_t *maxrow = A.get<int32_t>("eq.maxrow", S);
+    uint32_t *minf = A.get<uint32_t>("eq.minf", S);
+    uint32_t *minr = A.get<uint32_t>("eq.minr", S);
+    uint8_t *in_eq = A.get<uint8_t>("eq.in", S);
+    uint32_t *bf = A.get<uint32_t>("eq.bf", E->eq.n);
+    uint32_t *bfn = A.get<uint32_t>("eq.bfn", 1);
+    launch(st, k_iota_u32, S, uf, S);
+    HC(hipMemsetAsync(cnt, 0, 4 * S, st));
+    HC(hipMemsetAsync(maxrow, 0xff, 4 * S, st));
+    HC(hipMemsetAsync(minf, 0xff, 4 * S, st));
+    HC(hipMemsetAsync(minr, 0xff, 4 * S, st));
+    HC(hipMemsetAsync(in_eq, 0, S, st));
+    HC(hipMemsetAsync(bfn, 0, 4, st));
+    if (E->eq.n) {
+      launch(st, k_eq_union, E->eq.n, (const uint64_t *)E->eq.ptr, (const uint32_t *)E->eq.key, E->eq.n, uf, d_err);
+      launch(st, k_eq_stats, E->eq.n, (const uint64_t *)E->eq.ptr, (const uint32_t *)E->eq.key, E->eq.n, uf,
+             (const uint8_t *)d_forb, cnt, maxrow, minf, minr, in_eq);
+      launch(st, k_eq_assign, E->eq.n, (const uint64_t *)E->eq.ptr, (const uint32_t *)E->eq.key, E->eq.n, uf,
+             (const uint8_t *)d_forb, (const uint32_t *)minf, (const uint32_t *)minr, eq_rep, d_deleted, bf, bfn);
+    }
+    // eq cons (forbidden-only constraints), ordered by cluster index (= max row) then signal
+    uint64_t nf = E->forbidden.size();
+    uint32_t *fl_d = A.get<uint32_t>("forb.list", nf);
+    uint32_t *g_root = A.get<uint32_t>("eq.g_root", nf);
+    HC(hipMemsetAsync(g_root, 0, 4 * nf, st));
+    launch(st, k_gather_u32, nf, (const uint32_t *)uf, (const uint32_t *)fl_d, g_root, nf);
+    std::vector<uint32_t> root(nf), bfv;
+    uint32_t nbf = 0;
+    HC(hipMemcpyAsync(root.data(), g_root, 4 * nf, hipMemcpyDeviceToHost, st));
+    HC(hipMemcpyAsync(&nbf, bfn, 4, hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    struct EqCon {
+      int64_t order;
+      uint32_t f;
+      HostCon c;
+    };
+    std::vector<EqCon> eqc;
+    auto fetch1 = [&](const void *dptr, size_t bytes, void *h) {
+      HC(hipMemcpyAsync(h, dptr, bytes, hipMemcpyDeviceToHost, st));
+    };
+    for (uint64_t i = 0; i < nf; ++i) {
+      uint32_t f = E->forbidden[i];
+      uint8_t in = 0;
+      fetch1(in_eq + f, 1, &in);
+      HC(hipStreamSynchronize(st));
+      if (!in) continue;
+      uint32_t r = root[i], c = 0, mf = 0;
+      int32_t mr = 0;
+      fetch1(cnt + r, 4, &c);
+      fetch1(minf + r, 4, &mf);
+      fetch1(maxrow + r, 4, &mr);
+      HC(hipStreamSynchronize(st));
+      if (c <= 1 || f == mf) continue;
+      // transform(sub(Signal f, Signal rh)) = {0: 0, rh: 1, f: -1}
+      EqCon e;
+      e.order = mr;
+      e.f = f;
+      uint64_t one[4] = {1, 0, 0, 0}, m1[4];
+      memcpy(m1, E->prime, 32);
+      m1[0] -= 1;
+      e.c.k[2] = {0};
+      e.c.v[2] = {0, 0, 0, 0};
+      if (mf < f) {
+        e.c.k[2].push_back(mf); e.c.v[2].insert(e.c.v[2].end(), one, one + 4);
+        e.c.k[2].push_back(f); e.c.v[2].insert(e.c.v[2].end(), m1, m1 + 4);
+      } else {
+        e.c.k[2].push_back(f); e.c.v[2].insert(e.c.v[2].end(), m1, m1 + 4);
+        e.c.k[2].push_back(mf); e.c.v[2].insert(e.c.v[2].end(), one, one + 4);
+      }
+      eqc.push_back(std::move(e));
+    }
+    if (nbf) {
+      bfv.resize(nbf);
+      HC(hipMemcpyAsync(bfv.data(), bf, 4 * nbf, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      for (uint32_t r : bfv) {
+        uint32_t kk[2];
+        uint64_t p0 = 0;
+        HC(hipMemcpyAsync(&p0, E->eq.ptr + r, 8, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        HC(hipMemcpyAsync(kk, E->eq.key + p0, 8, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        uint32_t rt = 0, c = 0;
+        // root of the row: the smaller signal's root (roots are compressed after k_eq_assign)
+        uint32_t x = kk[0];
+        for (;;) {
+          uint32_t px = 0;
+          HC(hipMemcpyAsync(&px, uf + x, 4, hipMemcpyDeviceToHost, st));
+          HC(hipStreamSynchronize(st));
+          if (px == x) break;
+          x = px;
+        }
+        rt = x;
+        HC(hipMemcpyAsync(&c, cnt + rt, 4, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        if (c != 1) continue;  // a single-constraint cluster with both ends forbidden: kept as is
+        EqCon e;
+        e.order = r;
+        e.f = 0;
+        uint64_t v[8];
+        HC(hipMemcpyAsync(v, E->eq.val + p0, 64, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        e.c.k[2] = {kk[0], kk[1]};
+        e.c.v[2].assign(v, v + 8);
+        eqc.push_back(std::move(e));
+      }
+    }
+    std::sort(eqc.begin(), eqc.end(), [](const EqCon &x, const EqCon &y) {
+      return x.order != y.order ? x.order < y.order : x.f < y.f;
+    });
+    for (auto &e : eqc) lconst.push_back(std::move(e.c));
+  }
+
+  // working copies (Montgomery): cons_eq (C), linear (C, one spare slot per row)
+  DRows ce{}, lin{};
+  ce.n = E->ce.n;
+  ce.off = A.get<uint64_t>("ce.off", ce.n);
+  ce.len = A.get<uint32_t>("ce.len", ce.n);
+  ce.key = A.get<uint32_t>("ce.key", E->ce.nnz);
+  ce.val = A.get<Fe>("ce.val", E->ce.nnz);
+  if (ce.n) launch(st, k_make_ragged, ce.n, E->F, (const uint64_t *)E->ce.ptr, (const uint32_t *)E->ce.key, (const Fe *)E->ce.val,
+                   ce.n, (uint64_t)0, ce.off, ce.len, ce.key, ce.val);
+  lin.n = E->lin.n;
+  lin.off = A.get<uint64_t>("lin.off", lin.n);
+  lin.len = A.get<uint32_t>("lin.len", lin.n);
+  lin.key = A.get<uint32_t>("lin.key", E->lin.nnz + lin.n);
+  lin.val = A.get<Fe>("lin.val", E->lin.nnz + lin.n);
+  if (lin.n) launch(st, k_make_ragged, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
+                    lin.n, (uint64_t)1, lin.off, lin.len, lin.key, lin.val);
+  if (ce.n) launch(st, k_rename_rows, ce.n, E->F, ce, (const int32_t *)eq_rep);
+
+  // ======================= constant_eq_simplification (:253-273)
+  int32_t *ce_last = A.get<int32_t>("ce.last", S);
+  uint8_t *ce_has = A.get<uint8_t>("ce.has", S);
+  Fe *ce_val = A.get<Fe>("ce.val_s", S);
+  HC(hipMemsetAsync(ce_last, 0xff, 4 * S, st));
+  HC(hipMemsetAsync(ce_has, 0, S, st));
+  {
+    uint32_t *cl = A.get<uint32_t>("ce.cons", ce.n);
+    uint32_t *cn = A.get<uint32_t>("ce.consn", 1);
+    HC(hipMemsetAsync(cn, 0, 4, st));
+    if (ce.n) {
+      launch(st, k_const_pick, ce.n, ce, (const uint8_t *)d_forb, ce_last, d_deleted, cl, cn, d_err);
+      launch(st, k_const_value, ce.n, E->F, ce, (const uint8_t *)d_forb, (const int32_t *)ce_last, ce_val, ce_has);
+    }
+    uint32_t ncons = 0;
+    HC(hipMemcpyAsync(&ncons, cn, 4, hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    if (ncons) {
+      std::vector<uint32_t> ids(ncons);
+      HC(hipMemcpyAsync(ids.data(), cl, 4 * ncons, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      std::sort(ids.begin(), ids.end());
+      std::vector<uint64_t> off(ncons), hoff(ce.n);
+      std::vector<uint32_t> len(ncons), hlen(ce.n);
+      HC(hipMemcpyAsync(hoff.data(), ce.off, 8 * ce.n, hipMemcpyDeviceToHost, st));
+      HC(hipMemcpyAsync(hlen.data(), ce.len, 4 * ce.n, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      for (uint32_t i = 0; i < ncons; ++i) { off[i] = hoff[ids[i]]; len[i] = hlen[ids[i]]; }
+      std::vector<uint32_t> keys;
+      std::vector<uint64_t> vals, optr;
+      fetch_pool_maps(E, off, len, ce.key, ce.val, keys, vals, optr);
+      for (uint32_t i = 0; i < ncons; ++i) {
+        HostCon c;
+        c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
+        c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
+        lconst.push_back(std::move(c));
+      }
+    }
+  }
+  if (lin.n) launch(st, k_linear_frames12, lin.n, E->F, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val);
+  HC(hipStreamSynchronize(st));
+  E->stats.eq_ms = now_ms() - T0;
+
+  // ======================= linear round 1 (:544-578)
+  ElimOut eo;
+  Pool P = get_pool(E, 1 << 20);
+  if (apply_linear) {
+    run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted);
+    collect_leftovers(E, eo, P, lconst);
+    E->stats.rounds++;
+  } else {
+    // --O1: the linear rows join lconst unchanged (:575-577)
+    HostRows H;
+    fetch_keys(E, lin, H);
+    std::vector<uint64_t> hoff(lin.n);
+    if (lin.n) {
+      HC(hipMemcpyAsync(hoff.data(), lin.off, 8 * lin.n, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+    }
+    std::vector<uint32_t> keys;
+    std::vector<uint64_t> vals, optr;
+    fetch_pool_maps(E, hoff, H.len, lin.key, lin.val, keys, vals, optr);
+    for (uint64_t i = 0; i < lin.n; ++i) {
+      HostCon c;
+      c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
+      c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
+      lconst.push_back(std::move(c));
+    }
+  }
+
+  // ======================= obtain_and_simplify_non_linear (non_linear_utils.rs:6-31)
+  double Ts = now_ms();
+  const uint64_t n_nl = E->na.n;
+  DRows ia{}, ib{}, ic{};
+  auto mk_in = [&](rs_engine::Blk &B, DRows &R, const char *nm) {
+    R.n = B.n;
+    R.off = A.get<uint64_t>(std::string(nm) + ".off", R.n);
+    R.len = A.get<uint32_t>(std::string(nm) + ".len", R.n);
+    R.key = A.get<uint32_t>(std::string(nm) + ".key", B.nnz);
+    R.val = A.get<Fe>(std::string(nm) + ".val", B.nnz);
+    if (R.n) launch(st, k_make_ragged, R.n, E->F, (const uint64_t *)B.ptr, (const uint32_t *)B.key, (const Fe *)B.val, R.n,
+                    (uint64_t)0, R.off, R.len, R.key, R.val);
+  };
+  mk_in(E->na, ia, "nla");
+  mk_in(E->nb, ib, "nlb");
+  mk_in(E->nc, ic, "nlc");
+  // storage rows live in one growable heap of (key, value) entries
+  DRows sa{}, sb{}, sc{};
+  uint64_t heap_top = 0, heap_cap = 0;
+  uint32_t *heap_k = nullptr;
+  Fe *heap_v = nullptr;
+  auto heap_reserve = [&](uint64_t need) {
+    if (heap_top + need <= heap_cap && heap_k) return;
+    uint64_t ncap = std::max<uint64_t>(heap_top + need, heap_cap * 2);
+    uint32_t *nk = nullptr;
+    Fe *nv = nullptr;
+    HC(hipMallocAsync((void **)&nk, 4 * std::max<uint64_t>(ncap, 1), st));
+    HC(hipMallocAsync((void **)&nv, 32 * std::max<uint64_t>(ncap, 1), st));
+    if (heap_top) {
+      HC(hipMemcpyAsync(nk, heap_k, 4 * heap_top, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(nv, heap_v, 32 * heap_top, hipMemcpyDeviceToDevice, st));
+    }
+    if (heap_k) { HC(hipFreeAsync(heap_k, st)); HC(hipFreeAsync(heap_v, st)); }
+    heap_k = nk;
+    heap_v = nv;
+    heap_cap = ncap;
+  };
+  struct HeapGuard {
+    hipStream_t st;
+    uint32_t **k;
+    Fe **v;
+    ~HeapGuard() {
+      if (*k) (void)hipFreeAsync(*k, st);
+      if (*v) (void)hipFreeAsync(*v, st);
+    }
+  } heap_guard{st, &heap_k, &heap_v};
+  unsigned long long *d_bytes = A.get<unsigned long long>("nl.bytes", 1);
+  HC(hipMemsetAsync(d_bytes, 0, 8, st));
+  FrameArgs fr;
+  fr.F = E->F;
+  fr.eq_rep = eq_rep;
+  fr.ce_has = ce_has;
+  fr.ce_val = ce_val;
+  fr.sub_of = sub_of;
+  fr.h_off = A.get<uint64_t>("el.h_off", 1);
+  fr.h_len = A.get<uint32_t>("el.h_len", 1);
+  fr.pk = P.pk;
+  fr.pv = P.pv;
+  for (DRows *R : {&sa, &sb, &sc}) {
+    R->n = n_nl;
+  }
+  sa.off = A.get<uint64_t>("st.a.off", n_nl);
+  sa.len = A.get<uint32_t>("st.a.len", n_nl);
+  sb.off = A.get<uint64_t>("st.b.off", n_nl);
+  sb.len = A.get<uint32_t>("st.b.len", n_nl);
+  sc.off = A.get<uint64_t>("st.c.off", n_nl);
+  sc.len = A.get<uint32_t>("st.c.len", n_nl);
+  if (n_nl) {
+    uint64_t *ca = A.get<uint64_t>("nl.capa", n_nl), *cb = A.get<uint64_t>("nl.capb", n_nl), *cc = A.get<uint64_t>("nl.capc", n_nl);
+    NLArgs a;
+    a.fr = fr;
+    a.a = ia; a.b = ib; a.c = ic;
+    a.cap_a = ca; a.cap_b = cb; a.cap_c = cc;
+    a.bytes = d_bytes;
+    launch(st, k_nl_count, n_nl, a);
+    uint64_t ta = excl_scan_u64(E, ca, A.get<uint64_t>("nl.sa", n_nl), n_nl, "a");
+    uint64_t tb = excl_scan_u64(E, cb, A.get<uint64_t>("nl.sb", n_nl), n_nl, "b");
+    uint64_t tc = excl_scan_u64(E, cc, A.get<uint64_t>("nl.sc", n_nl), n_nl, "c");
+    heap_reserve(ta + tb + tc);
+    launch(st, k_set_offsets, n_nl, (const uint64_t *)A.get<uint64_t>("nl.sa", 1), heap_top, sa.off, n_nl);
+    launch(st, k_set_offsets, n_nl, (const uint64_t *)A.get<uint64_t>("nl.sb", 1), heap_top + ta, sb.off, n_nl);
+    launch(st, k_set_offsets, n_nl, (const uint64_t *)A.get<uint64_t>("nl.sc", 1), heap_top + ta + tb, sc.off, n_nl);
+    heap_top += ta + tb + tc;
+    sa.key = sb.key = sc.key = heap_k;
+    sa.val = sb.val = sc.val = heap_v;
+    a.oa = sa; a.ob = sb; a.oc = sc;
+    HC(hipEventRecord(E->ev0, st));
+    launch(st, k_nl_fill, n_nl, a);
+    HC(hipEventRecord(E->ev1, st));
+    HC(hipEventSynchronize(E->ev1));
+    float ms = 0;
+    HC(hipEventElapsedTime(&ms, E->ev0, E->ev1));
+    E->stats.apply_kernel_ms += ms;
+    E->stats.apply_kernel_launches++;
+  }
+  unsigned long long bytes = 0;
+  HC(hipMemcpyAsync(&bytes, d_bytes, 8, hipMemcpyDeviceToHost, st));
+  // split: storage (still non-linear) vs with_linear, both in DFS order
+  uint64_t n_st = 0, n_wl = 0;
+  uint32_t *st_ids = A.get<uint32_t>("st.ids", n_nl), *wl_ids = A.get<uint32_t>("wl.ids", n_nl);
+  if (n_nl) {
+    uint64_t *fl_lin = A.get<uint64_t>("fl.lin", n_nl), *fl_nl = A.get<uint64_t>("fl.nl", n_nl);
+    uint64_t *p_lin = A.get<uint64_t>("fl.plin", n_nl), *p_nl = A.get<uint64_t>("fl.pnl", n_nl);
+    launch(st, k_flag_linear, n_nl, (const uint32_t *)sa.len, (const uint32_t *)sb.len, n_nl, fl_lin, fl_nl);
+    n_wl = excl_scan_u64(E, fl_lin, p_lin, n_nl, "fl");
+    n_st = excl_scan_u64(E, fl_nl, p_nl, n_nl, "fn");
+    launch(st, k_scatter_ids, n_nl, (const uint64_t *)fl_lin, (const uint64_t *)p_lin, n_nl, wl_ids);
+    launch(st, k_scatter_ids, n_nl, (const uint64_t *)fl_nl, (const uint64_t *)p_nl, n_nl, st_ids);
+  }
+  HC(hipStreamSynchronize(st));
+  E->stats.apply_bytes += bytes;
+  if (no_rounds > 0) no_rounds--;
+
+  // storage view (compacted) and the non-linear signal map bitmap (:599-612)
+  DRows ta_{}, tb_{}, tc_{};
+  for (DRows *R : {&ta_, &tb_, &tc_}) { R->n = n_st; R->key = heap_k; R->val = heap_v; }
+  ta_.off = A.get<uint64_t>("sv.a.off", n_st); ta_.len = A.get<uint32_t>("sv.a.len", n_st);
+  tb_.off = A.get<uint64_t>("sv.b.off", n_st); tb_.len = A.get<uint32_t>("sv.b.len", n_st);
+  tc_.off = A.get<uint64_t>("sv.c.off", n_st); tc_.len = A.get<uint32_t>("sv.c.len", n_st);
+  if (n_st) {
+    launch(st, k_view_rows, n_st, (const uint64_t *)sa.off, (const uint32_t *)sa.len, (const uint32_t *)st_ids, n_st, ta_.off, ta_.len);
+    launch(st, k_view_rows, n_st, (const uint64_t *)sb.off, (const uint32_t *)sb.len, (const uint32_t *)st_ids, n_st, tb_.off, tb_.len);
+    launch(st, k_view_rows, n_st, (const uint64_t *)sc.off, (const uint32_t *)sc.len, (const uint32_t *)st_ids, n_st, tc_.off, tc_.len);
+  }
+  uint8_t *nlmap = A.get<uint8_t>("nlmap", S);
+  HC(hipMemsetAsync(nlmap, 0, S, st));
+  if (n_st) {
+    launch(st, k_mark_keys, n_st, ta_, nlmap);
+    launch(st, k_mark_keys, n_st, tb_, nlmap);
+    launch(st, k_mark_keys, n_st, tc_, nlmap);
+  }
+  // the current linear list: a C-only view
+  DRows lv{};
+  lv.n = n_wl;
+  lv.key = heap_k;
+  lv.val = heap_v;
+  lv.off = A.get<uint64_t>("lv.off", n_wl);
+  lv.len = A.get<uint32_t>("lv.len", n_wl);
+  if (n_wl) launch(st, k_view_rows, n_wl, (const uint64_t *)sc.off, (const uint32_t *)sc.len, (const uint32_t *)wl_ids, n_wl, lv.off, lv.len);
+  HC(hipStreamSynchronize(st));
+  E->stats.subst_ms += now_ms() - Ts;
+
+  // ======================= rounds >= 2 (:613-646)
+  bool apply_round = apply_linear && no_rounds > 0 && n_wl > 0;
+  std::vector<uint32_t> extra_keys;  // keys appended to the signal map that no final row may hold
+  if (apply_round) {
+    // host copy of the non-linear signal map: initial lists (ascending ids) + appended entries
+    double Tm = now_ms();
+    HostRows hA, hB, hC;
+    fetch_keys(E, ta_, hA);
+    fetch_keys(E, tb_, hB);
+    fetch_keys(E, tc_, hC);
+    std::vector<uint64_t> mptr(S + 1, 0);
+    std::vector<uint32_t> sig;
+    auto row_sigs = [&](uint64_t r, std::vector<uint32_t> &out) {
+      out.clear();
+      for (const HostRows *H : {&hA, &hB, &hC})
+        for (uint32_t i = 0; i < H->len[r]; ++i)
+          if (H->key[H->off[r] + i]) out.push_back(H->key[H->off[r] + i]);
+      std::sort(out.begin(), out.end());
+      out.erase(std::unique(out.begin(), out.end()), out.end());
+    };
+    for (uint64_t r = 0; r < n_st; ++r) {
+      row_sigs(r, sig);
+      for (uint32_t s : sig) mptr[s + 1]++;
+    }
+    for (uint64_t s = 0; s < S; ++s) mptr[s + 1] += mptr[s];
+    std::vector<uint32_t> mlist(mptr[S]);
+    {
+      std::vector<uint64_t> fillp(mptr.begin(), mptr.end() - 1);
+      for (uint64_t r = 0; r < n_st; ++r) {
+        row_sigs(r, sig);
+        for (uint32_t s : sig) mlist[fillp[s]++] = (uint32_t)r;
+      }
+    }
+    std::unordered_map<uint32_t, std::vector<uint32_t>> mext;
+    std::vector<uint8_t> extra_mark;
+    E->stats.subst_ms += now_ms() - Tm;
+    int32_t *rank_of = A.get<int32_t>("rank_of", S);
+    HC(hipMemsetAsync(rank_of, 0xff, 4 * S, st));
+    int32_t *r_sub_of = A.get<int32_t>("r.sub_of", S);
+    HC(hipMemsetAsync(r_sub_of, 0xff, 4 * S, st));
+    while (apply_round) {
+      // linear_simplification over the current list
+      ElimOut er;
+      HC(hipMemsetAsync(r_sub_of, 0xff, 4 * S, st));
+      run_linear_simplification(E, lv, fl->use_old_heuristics, er, P, d_err, d_forb, r_sub_of, d_deleted);
+      E->stats.rounds++;
+      collect_leftovers(E, er, P, lconst);
+      double Tr = now_ms();
+      // ordered substitutions of the round: cluster order, ascending `from`
+      uint64_t n_slots = er.cl_off.back();
+      std::vector<uint32_t> hsig(n_slots);
+      std::vector<uint64_t> hoff(n_slots);
+      std::vector<uint32_t> hlen(n_slots);
+      if (n_slots) {
+        HC(hipMemcpyAsync(hsig.data(), A.get<uint32_t>("el.h_sig", 1), 4 * n_slots, hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(hoff.data(), A.get<uint64_t>("el.h_off", 1), 8 * n_slots, hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(hlen.data(), A.get<uint32_t>("el.h_len", 1), 4 * n_slots, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+      }
+      std::vector<uint32_t> U;      // slots in order
+      for (uint64_t c = 0; c < er.n_clusters; ++c) {
+        uint64_t b = er.cl_off[c];
+        std::vector<uint32_t> sl(er.n_sub[c]);
+        for (uint32_t i = 0; i < er.n_sub[c]; ++i) sl[i] = (uint32_t)(b + i);
+        std::sort(sl.begin(), sl.end(), [&](uint32_t x, uint32_t y) { return hsig[x] < hsig[y]; });
+        U.insert(U.end(), sl.begin(), sl.end());
+      }
+      uint64_t nU = U.size();
+      // RHS keys of the substitutions (for the map appends)
+      std::vector<uint64_t> uoff(nU);
+      std::vector<uint32_t> ulen(nU), ukeys;
+      std::vector<uint64_t> uvals, uptr;
+      for (uint64_t i = 0; i < nU; ++i) { uoff[i] = hoff[U[i]]; ulen[i] = hlen[U[i]]; }
+      fetch_pool_maps(E, uoff, ulen, P.pk, P.pv, ukeys, uvals, uptr);
+      std::vector<uint32_t> usig(nU);
+      std::vector<int32_t> urank(nU);
+      for (uint64_t i = 0; i < nU; ++i) { usig[i] = hsig[U[i]]; urank[i] = (int32_t)i; }
+      uint32_t *d_us = A.get<uint32_t>("r.us", nU);
+      int32_t *d_ur = A.get<int32_t>("r.ur", nU);
+      if (nU) {
+        HC(hipMemcpyAsync(d_us, usig.data(), 4 * nU, hipMemcpyHostToDevice, st));
+        HC(hipMemcpyAsync(d_ur, urank.data(), 4 * nU, hipMemcpyHostToDevice, st));
+        launch(st, k_set_rank, nU, (const uint32_t *)d_us, (const int32_t *)d_ur, nU, rank_of);
+      }
+      // apply to every storage row (apply_substitution_to_map, :345-396)
+      std::vector<std::pair<uint64_t, uint32_t>> turned;  // (order key, storage id)
+      if (n_st && nU) {
+        RoundArgs ra;
+        ra.F = E->F;
+        ra.a = ta_; ra.b = tb_; ra.c = tc_;
+        uint64_t *ca = A.get<uint64_t>("r.capa", n_st), *cb = A.get<uint64_t>("r.capb", n_st), *cc = A.get<uint64_t>("r.capc", n_st);
+        ra.cap_a = ca; ra.cap_b = cb; ra.cap_c = cc;
+        ra.sub_of = r_sub_of;
+        ra.rank_of = rank_of;
+        ra.h_off = A.get<uint64_t>("el.h_off", 1);
+        ra.h_len = A.get<uint32_t>("el.h_len", 1);
+        ra.pk = P.pk;
+        ra.pv = P.pv;
+        ra.turn = A.get<int32_t>("r.turn", n_st);
+        ra.touched = A.get<uint8_t>("r.touched", n_st);
+        launch(st, k_round_count, n_st, ra);
+        uint64_t qa = excl_scan_u64(E, ca, A.get<uint64_t>("r.sa", n_st), n_st, "ra");
+        uint64_t qb = excl_scan_u64(E, cb, A.get<uint64_t>("r.sb", n_st), n_st, "rb");
+        uint64_t qc = excl_scan_u64(E, cc, A.get<uint64_t>("r.sc", n_st), n_st, "rc");
+        heap_reserve(qa + qb + qc);
+        for (DRows *R : {&ta_, &tb_, &tc_, &lv}) { R->key = heap_k; R->val = heap_v; }
+        ra.a = ta_; ra.b = tb_; ra.c = tc_;
+        DRows oa = ta_, ob = tb_, oc = tc_;
+        oa.off = A.get<uint64_t>("r.oa.off", n_st); oa.len = A.get<uint32_t>("r.oa.len", n_st);
+        ob.off = A.get<uint64_t>("r.ob.off", n_st); ob.len = A.get<uint32_t>("r.ob.len", n_st);
+        oc.off = A.get<uint64_t>("r.oc.off", n_st); oc.len = A.get<uint32_t>("r.oc.len", n_st);
+        launch(st, k_set_offsets, n_st, (const uint64_t *)A.get<uint64_t>("r.sa", 1), heap_top, oa.off, n_st);
+        launch(st, k_set_offsets, n_st, (const uint64_t *)A.get<uint64_t>("r.sb", 1), heap_top + qa, ob.off, n_st);
+        launch(st, k_set_offsets, n_st, (const uint64_t *)A.get<uint64_t>("r.sc", 1), heap_top + qa + qb, oc.off, n_st);
+        heap_top += qa + qb + qc;
+        ra.oa = oa; ra.ob = ob; ra.oc = oc;
+        ra.tmpk = A.get<uint32_t>("r.tmpk", 2 * (qc + 1));
+        ra.tmpv = A.get<Fe>("r.tmpv", 2 * (qc + 1));
+        ra.c_base = heap_top - qc;  // row scratch = 2 * (its C offset - c_base)
+        launch(st, k_round_fill, n_st, ra);
+        launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
+        // turned rows
+        uint64_t *tf = A.get<uint64_t>("r.tf", n_st), *tp = A.get<uint64_t>("r.tp", n_st);
+        launch(st, k_turn_flags, n_st, (const int32_t *)ra.turn, n_st, tf);
+        uint64_t n_turn = excl_scan_u64(E, tf, tp, n_st, "tf");
+        uint32_t *tids = A.get<uint32_t>("r.tids", n_turn);
+        launch(st, k_scatter_ids, n_st, (const uint64_t *)tf, (const uint64_t *)tp, n_st, tids);
+        std::vector<uint32_t> htids(n_turn);
+        std::vector<int32_t> hturn(n_st);
+        if (n_turn) HC(hipMemcpyAsync(htids.data(), tids, 4 * n_turn, hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(hturn.data(), ra.turn, 4 * n_st, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        // order key: (rank of the turning substitution, first position in map[from])
+        for (uint32_t r : htids) {
+          int32_t q = hturn[r];
+          uint32_t from = usig[q];
+          uint64_t pos = UINT64_MAX;
+          for (uint64_t t = mptr[from]; t < mptr[from + 1]; ++t)
+            if (mlist[t] == r) { pos = t - mptr[from]; break; }
+          if (pos == UINT64_MAX) {
+            auto it = mext.find(from);
+            if (it != mext.end())
+              for (uint64_t t = 0; t < it->second.size(); ++t)
+                if (it->second[t] == r) { pos = (mptr[from + 1] - mptr[from]) + t; break; }
+          }
+          if (pos == UINT64_MAX) throw RsError(RS_E_INTERNAL, "substituted row missing from the signal map");
+          turned.push_back({((uint64_t)q << 32) | (pos & 0xffffffffu), r});
+        }
+        std::sort(turned.begin(), turned.end());
+      }
+      // map appends (:369-377): every key of sub.to gets every visited row
+      for (uint64_t i = 0; i < nU; ++i) {
+        uint32_t from = usig[i];
+        uint64_t n0 = mptr[from + 1] - mptr[from];
+        auto it = mext.find(from);
+        uint64_t n1 = it == mext.end() ? 0 : it->second.size();
+        if (n0 + n1 == 0) continue;
+        std::vector<uint32_t> visit(mlist.begin() + mptr[from], mlist.begin() + mptr[from + 1]);
+        if (n1) visit.insert(visit.end(), it->second.begin(), it->second.end());
+        for (uint64_t t = uptr[i]; t < uptr[i + 1]; ++t) {
+          uint32_t k = ukeys[t];
+          std::vector<uint32_t> &dst = mext[k];
+          dst.insert(dst.end(), visit.begin(), visit.end());
+          if (extra_mark.empty()) extra_mark.assign(S, 0);
+          if (!extra_mark[k]) { extra_mark[k] = 1; extra_keys.push_back(k); }
+        }
+      }
+      if (nU) {  // reset the dense rank index
+        std::vector<int32_t> neg(nU, -1);
+        HC(hipMemcpyAsync(d_ur, neg.data(), 4 * nU, hipMemcpyHostToDevice, st));
+        launch(st, k_set_rank, nU, (const uint32_t *)d_us, (const int32_t *)d_ur, nU, rank_of);
+      }
+      // next linear list: the turned rows, non-empty, in linear_id order
+      std::vector<uint32_t> next_ids;
+      {
+        std::vector<uint32_t> clen(n_st);
+        if (n_st) {
+          HC(hipMemcpyAsync(clen.data(), tc_.len, 4 * n_st, hipMemcpyDeviceToHost, st));
+          HC(hipStreamSynchronize(st));
+        }
+        for (auto &t : turned)
+          if (clen[t.second]) next_ids.push_back(t.second);
+      }
+      uint64_t nn = next_ids.size();
+      lv.n = nn;
+      lv.off = A.get<uint64_t>("lv.off", nn);
+      lv.len = A.get<uint32_t>("lv.len", nn);
+      lv.key = heap_k;
+      lv.val = heap_v;
+      if (nn) {
+        uint32_t *d_ids = A.get<uint32_t>("lv.ids", nn);
+        HC(hipMemcpyAsync(d_ids, next_ids.data(), 4 * nn, hipMemcpyHostToDevice, st));
+        launch(st, k_view_rows, nn, (const uint64_t *)tc_.off, (const uint32_t *)tc_.len, (const uint32_t *)d_ids, nn, lv.off, lv.len);
+      }
+      // emptied storage rows (storage.replace(c_id, C::empty()))
+      if (!turned.empty()) {
+        std::vector<uint32_t> all;
+        for (auto &t : turned) all.push_back(t.second);
+        uint32_t *d_all = A.get<uint32_t>("r.all", all.size());
+        HC(hipMemcpyAsync(d_all, all.data(), 4 * all.size(), hipMemcpyHostToDevice, st));
+        launch(st, k_zero_c, all.size(), (const uint32_t *)d_all, (uint64_t)all.size(), tc_.len);
+      }
+      HC(hipStreamSynchronize(st));
+      E->stats.subst_ms += now_ms() - Tr;
+      if (no_rounds > 0) no_rounds--;
+      apply_round = nn > 0 && no_rounds > 0;
+    }
+  }
+  // ======================= final assembly (:648-729)
+  double Tf = now_ms();
+  // leftover linear rows (rounds exhausted): appended after the storage rows
+  if (lv.n) launch(st, k_mark_keys, lv.n, lv, nlmap);
+  if (!extra_keys.empty()) {
+    uint32_t *d_x = A.get<uint32_t>("fin.extra", extra_keys.size());
+    HC(hipMemcpyAsync(d_x, extra_keys.data(), 4 * extra_keys.size(), hipMemcpyHostToDevice, st));
+    launch(st, k_mark_list, extra_keys.size(), (const uint32_t *)d_x, (uint64_t)extra_keys.size(), nlmap);
+  }
+  for (auto &c : lconst) host_fix(c);
+  {
+    std::vector<uint32_t> lk;
+    for (auto &c : lconst)
+      for (int q = 0; q < 3; ++q)
+        for (uint32_t k : c.k[q]) lk.push_back(k);
+    if (!lk.empty()) {
+      uint32_t *d_x = A.get<uint32_t>("fin.lk", lk.size());
+      HC(hipMemcpyAsync(d_x, lk.data(), 4 * lk.size(), hipMemcpyHostToDevice, st));
+      launch(st, k_mark_list, lk.size(), (const uint32_t *)d_x, (uint64_t)lk.size(), nlmap);
+    }
+  }
+  HC(hipMemsetAsync(nlmap, 0, 1, st));  // the constant key is not a signal
+  uint32_t *kept = A.get<uint32_t>("fin.kept", S);
+  uint64_t *kept64 = A.get<uint64_t>("fin.kept64", S);
+  uint64_t *rank = A.get<uint64_t>("fin.rank", S);
+  int64_t *l2w = A.get<int64_t>("fin.l2w", S);
+  launch(st, k_kept, S, (const uint8_t *)d_deleted, (const uint8_t *)d_forb, (const uint8_t *)nlmap, kept, S);
+  launch(st, k_u32_to_u64, S, (const uint32_t *)kept, kept64, S);
+  E->n_wires = excl_scan_u64(E, kept64, rank, S, "kept");
+  launch(st, k_l2w, S, (const uint32_t *)kept, (const uint64_t *)rank, l2w, S);
+  {
+    uint64_t lo = E->n_pub_out + 1, hi = E->n_pub_out + E->n_pub_in + E->n_priv_in;
+    uint64_t del_in = 0;
+    if (hi >= lo && lo < S) {
+      uint64_t cnt = std::min<uint64_t>(hi, S - 1) - lo + 1;
+      std::vector<uint32_t> k(cnt);
+      HC(hipMemcpyAsync(k.data(), kept + lo, 4 * cnt, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      for (uint32_t x : k) del_in += x ? 0 : 1;
+    }
+    E->npiw = E->n_priv_in - del_in;
+  }
+  // output rows: storage (non-empty) ++ leftover linear ++ lconst (host)
+  {
+    uint64_t *nef = A.get<uint64_t>("fin.nef", n_st), *nep = A.get<uint64_t>("fin.nep", n_st);
+    uint64_t n_keep = 0;
+    if (n_st) {
+      launch(st, k_nonempty_flags, n_st, (const uint32_t *)ta_.len, (const uint32_t *)tb_.len, (const uint32_t *)tc_.len, n_st, nef);
+      n_keep = excl_scan_u64(E, nef, nep, n_st, "ne");
+    }
+    uint32_t *keep_ids = A.get<uint32_t>("fin.keep", n_keep);
+    if (n_keep) launch(st, k_scatter_ids, n_st, (const uint64_t *)nef, (const uint64_t *)nep, n_st, keep_ids);
+    // leftover linear rows keep their list order (non-empty by construction)
+    uint64_t n_lv = lv.n;
+    uint64_t n_out = n_keep + n_lv;
+    E->out_n_dev = n_out;
+    uint32_t *lv_ids = A.get<uint32_t>("fin.lvids", n_lv);
+    if (n_lv) launch(st, k_iota_u32, n_lv, lv_ids, n_lv);
+    const DRows *parts[3] = {&ta_, &tb_, &tc_};
+    const char *nm[3] = {"out.a", "out.b", "out.c"};
+    DRows empty_lv = lv;
+    uint32_t *zero_len = A.get<uint32_t>("fin.zlen", n_lv);
+    if (n_lv) HC(hipMemsetAsync(zero_len, 0, 4 * n_lv, st));
+    for (int q = 0; q < 3; ++q) {
+      uint64_t *lens = A.get<uint64_t>(std::string(nm[q]) + ".lens", n_out + 1);
+      uint64_t *ptr = A.get<uint64_t>(std::string(nm[q]) + ".ptr", n_out + 1);
+      if (n_keep) launch(st, k_row_lens, n_keep, *parts[q], (const uint32_t *)keep_ids, n_keep, lens);
+      DRows lvq = empty_lv;
+      if (q < 2) lvq.len = zero_len;
+      if (n_lv) launch(st, k_row_lens, n_lv, lvq, (const uint32_t *)lv_ids, n_lv, lens + n_keep);
+      HC(hipMemsetAsync(lens + n_out, 0, 8, st));
+      uint64_t tot = excl_scan_u64(E, lens, ptr, n_out + 1, nm[q]);
+      E->out_nnz[q] = tot;
+      uint32_t *col = A.get<uint32_t>(std::string(nm[q]) + ".col", tot);
+      uint64_t *val = A.get<uint64_t>(std::string(nm[q]) + ".val", 4 * tot);
+      if (n_keep) launch(st, k_gather_rows, n_keep, E->F, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint64_t *)ptr, col, val);
+      if (n_lv) launch(st, k_gather_rows, n_lv, E->F, lvq, (const uint32_t *)lv_ids, n_lv, (const uint64_t *)(ptr + n_keep), col, val);
+    }
+    E->out_host_tail = std::move(lconst);
+  }
+  int err = 0;
+  HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  if (err) throw RsError(RS_E_INVALID, "input rejected by the device checks (code " + std::to_string(err) + ")");
+  E->stats.final_ms = now_ms() - Tf;
+  E->stats.total_ms = now_ms() - T0;
+  E->have_result = true;
+}
+
+}  // namespace rs
+
+// ==================================================================== C API
+extern "C" {
+
+const char *rs_last_error(void) { return g_err.c_str(); }
+int rs_abi_version(void) { return RS_ABI_VERSION; }
+
+int rs_engine_create(int device, rs_engine **eng) {
+  try {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+      set_error("no HIP device visible: librs_simplify runs only on a gfx950 GPU");
+      return RS_E_NODEVICE;
+    }
+    if (device < 0 || device >= n) { set_error("bad device ordinal"); return RS_E_INVALID; }
+    HC(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HC(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+      set_error(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only");
+      return RS_E_NODEVICE;
+    }
+    std::unique_ptr<rs_engine> E(new rs_engine());
+    E->device = device;
+    HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
+    HC(hipEventCreate(&E->ev0));
+    HC(hipEventCreate(&E->ev1));
+    *eng = E.release();
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+void rs_engine_destroy(rs_engine *E) {
+  if (!E) return;
+  (void)hipSetDevice(E->device);
+  if (E->st) (void)hipStreamSynchronize(E->st);
+  if (E->ev0) (void)hipEventDestroy(E->ev0);
+  if (E->ev1) (void)hipEventDestroy(E->ev1);
+  if (E->st) (void)hipStreamDestroy(E->st);
+  delete E;
+}
+
+int rs_engine_load(rs_engine *E, const rs_input *in) {
+  try {
+    HC(hipSetDevice(E->device));
+    uint64_t p[4];
+    if (!prime_of(in, p)) { set_error("unknown prime"); return RS_E_INVALID; }
+    if (in->max_signal == 0 || in->max_signal > 0xfffffff0ull) { set_error("bad max_signal"); return RS_E_INVALID; }
+    memcpy(E->prime, p, 32);
+    E->prime_id = in->prime_id;
+    E->F = make_field(p);
+    E->S = in->max_signal;
+    E->n_pub_out = in->n_pub_out;
+    E->n_pub_in = in->n_pub_in;
+    E->n_priv_in = in->n_priv_in;
+    E->forbidden.assign(in->forbidden, in->forbidden + in->n_forbidden);
+    bool has0 = false;
+    for (uint32_t f : E->forbidden) {
+      if (f >= E->S) { set_error("forbidden signal out of range"); return RS_E_INVALID; }
+      has0 |= f == 0;
+    }
+    if (!has0) { set_error("signal 0 must be forbidden"); return RS_E_INVALID; }
+    if (in->nl_a.n_rows != in->nl_b.n_rows || in->nl_a.n_rows != in->nl_c.n_rows) {
+      set_error("non-linear blocks differ in row count");
+      return RS_E_INVALID;
+    }
+    upload_block(E, in->cons_eq, E->ce, "in.ce");
+    upload_block(E, in->eq, E->eq, "in.eq");
+    upload_block(E, in->linear, E->lin, "in.lin");
+    upload_block(E, in->nl_a, E->na, "in.na");
+    upload_block(E, in->nl_b, E->nb, "in.nb");
+    upload_block(E, in->nl_c, E->nc, "in.nc");
+    int *d_err = E->A.get<int>("err", 1);
+    HC(hipMemsetAsync(d_err, 0, 4, E->st));
+    for (rs_engine::Blk *B : {&E->ce, &E->eq, &E->lin, &E->na, &E->nb, &E->nc})
+      if (B->n) launch(E->st, k_sort_validate, B->n, E->F, (const uint64_t *)B->ptr, B->key, B->val, B->n, E->S, d_err);
+    int err = 0;
+    HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
+    HC(hipStreamSynchronize(E->st));
+    if (err) { set_error("invalid input rows (duplicate key, zero or non-canonical value, signal >= max_signal)"); return RS_E_INVALID; }
+    E->loaded = true;
+    E->have_result = false;
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+int rs_engine_run(rs_engine *E, const rs_flags *fl) {
+  try {
+    if (!E->loaded) { set_error("engine has no input"); return RS_E_INVALID; }
+    HC(hipSetDevice(E->device));
+    engine_run(E, fl);
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+int rs_engine_stats(rs_engine *E, rs_stats *s) {
+  *s = E->stats;
+  return RS_OK;
+}
+
+int rs_engine_fetch(rs_engine *E, rs_output **out) {
+  try {
+    if (!E->have_result) { set_error("no result"); return RS_E_INVALID; }
+    HC(hipSetDevice(E->device));
+    rs_output *o = (rs_output *)calloc(1, sizeof(rs_output));
+    uint64_t nd = E->out_n_dev, nh = E->out_host_tail.size();
+    // count non-empty host rows (lconst after fix may be empty: extract_with removes them)
+    std::vector<const HostCon *> hrows;
+    for (auto &c : E->out_host_tail)
+      if (!(c.k[0].empty() && c.k[1].empty() && c.k[2].empty())) hrows.push_back(&c);
+    nh = hrows.size();
+    o->n_constraints = nd + nh;
+    const char *nm[3] = {"out.a", "out.b", "out.c"};
+    rs_lc *dst[3] = {&o->a, &o->b, &o->c};
+    for (int q = 0; q < 3; ++q) {
+      uint64_t hn = 0;
+      for (auto *c : hrows) hn += c->k[q].size();
+      uint64_t tot = E->out_nnz[q] + hn;
+      rs_lc &L = *dst[q];
+      L.n_rows = nd + nh;
+      L.nnz = tot;
+      L.ptr = (uint64_t *)malloc(8 * (nd + nh + 1));
+      L.col = (uint32_t *)malloc(4 * (tot ? tot : 1));
+      L.val = (uint64_t *)malloc(32 * (tot ? tot : 1));
+      if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
+      else L.ptr[0] = 0;
+      if (E->out_nnz[q]) {
+        HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(std::string(nm[q]) + ".col", 1), 4 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+        HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(std::string(nm[q]) + ".val", 1), 32 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+      }
+      HC(hipStreamSynchronize(E->st));
+      uint64_t e = E->out_nnz[q];
+      for (uint64_t i = 0; i < nh; ++i) {
+        const HostCon &c = *hrows[i];
+        for (size_t t = 0; t < c.k[q].size(); ++t) {
+          L.col[e] = c.k[q][t];
+          memcpy(L.val + 4 * e, &c.v[q][4 * t], 32);
+          ++e;
+        }
+        L.ptr[nd + i + 1] = e;
+      }
+    }
+    o->n_labels = E->S;
+    o->label_to_wire = (int64_t *)malloc(8 * E->S);
+    HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int64_t>("fin.l2w", 1), 8 * E->S, hipMemcpyDeviceToHost, E->st));
+    HC(hipStreamSynchronize(E->st));
+    o->n_wires = E->n_wires;
+    o->no_private_inputs_witness = E->npiw;
+    *out = o;
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+void rs_output_free(rs_output *o) {
+  if (!o) return;
+  free_lc(o->a);
+  free_lc(o->b);
+  free_lc(o->c);
+  free(o->label_to_wire);
+  free(o);
+}
+
+int rs_simplify(const rs_input *in, const rs_flags *fl, rs_output **out) {
+  rs_engine *E = nullptr;
+  int rc = rs_engine_create(fl->device, &E);
+  if (rc) return rc;
+  rc = rs_engine_load(E, in);
+  if (!rc) rc = rs_engine_run(E, fl);
+  if (!rc) rc = rs_engine_fetch(E, out);
+  rs_engine_destroy(E);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,147 @@
+// field.hpp -- F_p arithmetic for the device (and host helpers), p < 2^256 odd.
+//
+// Replaces circom_algebra/src/modular_arithmetic.rs:9-91 (num-bigint-dig BigInt + double
+// remainder per op) with fixed 4x64-bit limbs in Montgomery form (R = 2^256): one CIOS product
+// per field multiplication, carry-propagating add/sub with a single conditional correction.
+// Results are canonical residues, identical to the reference's ((a % p) + p) % p.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rs {
+
+typedef unsigned __int128 u128;
+
+struct __attribute__((aligned(16))) Fe {
+  uint64_t l[4];
+};
+
+struct FieldP {
+  uint64_t p[4];
+  uint64_t np;  // -p^-1 mod 2^64
+  Fe r2;        // R^2 mod p
+  Fe one;       // R mod p
+  Fe pm2;       // p - 2 (Fermat exponent)
+};
+
+__host__ __device__ __forceinline__ bool fe_is_zero(const Fe &a) {
+  return (a.l[0] | a.l[1] | a.l[2] | a.l[3]) == 0;
+}
+__host__ __device__ __forceinline__ Fe fe_zero() {
+  Fe z;
+  z.l[0] = z.l[1] = z.l[2] = z.l[3] = 0;
+  return z;
+}
+__host__ __device__ __forceinline__ bool fe_eq(const Fe &a, const Fe &b) {
+  return ((a.l[0] ^ b.l[0]) | (a.l[1] ^ b.l[1]) | (a.l[2] ^ b.l[2]) | (a.l[3] ^ b.l[3])) == 0;
+}
+__host__ __device__ __forceinline__ bool geq4(const uint64_t *a, const uint64_t *b) {
+  if (a[3] != b[3]) return a[3] > b[3];
+  if (a[2] != b[2]) return a[2] > b[2];
+  if (a[1] != b[1]) return a[1] > b[1];
+  return a[0] >= b[0];
+}
+__host__ __device__ __forceinline__ uint64_t sub4(uint64_t *r, const uint64_t *a, const uint64_t *b) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u128 d = (u128)a[i] - b[i] - br;
+    r[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  return br;
+}
+__host__ __device__ __forceinline__ uint64_t add4(uint64_t *r, const uint64_t *a, const uint64_t *b) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u128 s = (u128)a[i] + b[i] + c;
+    r[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  return c;
+}
+
+__host__ __device__ __forceinline__ Fe fadd(const FieldP &F, const Fe &a, const Fe &b) {
+  Fe r;
+  uint64_t c = add4(r.l, a.l, b.l);
+  if (c || geq4(r.l, F.p)) sub4(r.l, r.l, F.p);
+  return r;
+}
+__host__ __device__ __forceinline__ Fe fsub(const FieldP &F, const Fe &a, const Fe &b) {
+  Fe r;
+  if (sub4(r.l, a.l, b.l)) add4(r.l, r.l, F.p);
+  return r;
+}
+__host__ __device__ __forceinline__ Fe fneg(const FieldP &F, const Fe &a) {
+  if (fe_is_zero(a)) return a;
+  Fe r;
+  sub4(r.l, F.p, a.l);
+  return r;
+}
+// CIOS Montgomery product.
+__host__ __device__ __forceinline__ Fe fmul(const FieldP &F, const Fe &a, const Fe &b) {
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t bi = b.l[i];
+    u128 s;
+    s = (u128)a.l[0] * bi + t0; t0 = (uint64_t)s;
+    s = (u128)a.l[1] * bi + t1 + (uint64_t)(s >> 64); t1 = (uint64_t)s;
+    s = (u128)a.l[2] * bi + t2 + (uint64_t)(s >> 64); t2 = (uint64_t)s;
+    s = (u128)a.l[3] * bi + t3 + (uint64_t)(s >> 64); t3 = (uint64_t)s;
+    s = (u128)t4 + (uint64_t)(s >> 64); t4 = (uint64_t)s; t5 = (uint64_t)(s >> 64);
+    const uint64_t m = t0 * F.np;
+    s = (u128)m * F.p[0] + t0;
+    s = (u128)m * F.p[1] + t1 + (uint64_t)(s >> 64); t0 = (uint64_t)s;
+    s = (u128)m * F.p[2] + t2 + (uint64_t)(s >> 64); t1 = (uint64_t)s;
+    s = (u128)m * F.p[3] + t3 + (uint64_t)(s >> 64); t2 = (uint64_t)s;
+    s = (u128)t4 + (uint64_t)(s >> 64); t3 = (uint64_t)s;
+    t4 = t5 + (uint64_t)(s >> 64);
+  }
+  Fe r;
+  r.l[0] = t0; r.l[1] = t1; r.l[2] = t2; r.l[3] = t3;
+  if (t4 || geq4(r.l, F.p)) sub4(r.l, r.l, F.p);
+  return r;
+}
+__host__ __device__ __forceinline__ Fe fto_mont(const FieldP &F, const Fe &c) { return fmul(F, c, F.r2); }
+__host__ __device__ __forceinline__ Fe ffrom_mont(const FieldP &F, const Fe &a) {
+  Fe o = fe_zero();
+  o.l[0] = 1;
+  return fmul(F, a, o);
+}
+// a^(p-2) = a^-1 for a != 0 (the value num-bigint's mod_inverse returns).
+__host__ __device__ inline Fe finv(const FieldP &F, const Fe &a) {
+  Fe r = F.one, base = a;
+  for (int w = 0; w < 4; ++w) {
+    uint64_t e = F.pm2.l[w];
+    for (int i = 0; i < 64; ++i) {
+      if (e & 1) r = fmul(F, r, base);
+      base = fmul(F, base, base);
+      e >>= 1;
+    }
+  }
+  return r;
+}
+
+inline FieldP make_field(const uint64_t prime[4]) {
+  FieldP F;
+  for (int i = 0; i < 4; ++i) F.p[i] = prime[i];
+  uint64_t inv = 1;
+  for (int i = 0; i < 7; ++i) inv *= 2 - F.p[0] * inv;
+  F.np = (uint64_t)0 - inv;
+  uint64_t x[4] = {1, 0, 0, 0};
+  for (int i = 0; i < 512; ++i) {
+    uint64_t c = add4(x, x, x);
+    if (c || geq4(x, F.p)) sub4(x, x, F.p);
+    if (i == 255)
+      for (int j = 0; j < 4; ++j) F.one.l[j] = x[j];
+  }
+  for (int j = 0; j < 4; ++j) F.r2.l[j] = x[j];
+  uint64_t two[4] = {2, 0, 0, 0};
+  sub4(F.pm2.l, F.p, two);
+  return F;
+}
+
+}  // namespace rs

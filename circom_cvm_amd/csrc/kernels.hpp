@@ -1,0 +1,938 @@
+// kernels.hpp -- HIP kernels of the simplification path (gfx950).
+//
+// Rows live in HBM as ragged CSR: row r = entries [off[r], off[r] + len[r]) of (key u32, Fe
+// value 32 B, Montgomery form); keys sorted ascending, unique.  Substitution right-hand sides
+// (RHS) live in a bump-allocated pool with the same (key, value) SoA layout.
+//
+// Every kernel names the reference function it restates (file:line in /root/reference).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "field.hpp"
+
+namespace rs {
+
+#define RS_NONE 0xffffffffu
+
+struct DRows {
+  uint64_t *off;
+  uint32_t *len;
+  uint32_t *key;
+  Fe *val;
+  uint64_t n;
+};
+
+__device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
+
+// ---------------------------------------------------------------- small sequential helpers
+// insertion sort by key + combine duplicate keys (sum); zeros are kept (HashMap semantics).
+__device__ inline uint32_t d_sort_combine(const FieldP &F, uint32_t *k, Fe *v, uint32_t n) {
+  for (uint32_t i = 1; i < n; ++i) {
+    uint32_t kk = k[i];
+    Fe vv = v[i];
+    uint32_t j = i;
+    while (j > 0 && k[j - 1] > kk) {
+      k[j] = k[j - 1];
+      v[j] = v[j - 1];
+      --j;
+    }
+    k[j] = kk;
+    v[j] = vv;
+  }
+  uint32_t w = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (w > 0 && k[w - 1] == k[i]) v[w - 1] = fadd(F, v[w - 1], v[i]);
+    else { k[w] = k[i]; v[w] = v[i]; ++w; }
+  }
+  return w;
+}
+__device__ inline uint32_t d_drop_zeros(uint32_t *k, Fe *v, uint32_t n) {
+  uint32_t w = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!fe_is_zero(v[i])) { k[w] = k[i]; v[w] = v[i]; ++w; }
+  return w;
+}
+// out = c - s*b over sorted maps, zeros dropped (constant_linear_linear_reduction, algebra.rs:1326-1344)
+__device__ inline uint32_t d_axpy_merge(const FieldP &F, const uint32_t *ck, const Fe *cv, uint32_t cn,
+                                        const uint32_t *bk, const Fe *bv, uint32_t bn, const Fe &s,
+                                        uint32_t *ok, Fe *ov) {
+  uint32_t i = 0, j = 0, w = 0;
+  while (i < cn || j < bn) {
+    uint32_t kk;
+    Fe x;
+    if (j >= bn || (i < cn && ck[i] < bk[j])) { kk = ck[i]; x = cv[i]; ++i; }
+    else if (i >= cn || bk[j] < ck[i]) { kk = bk[j]; x = fneg(F, fmul(F, s, bv[j])); ++j; }
+    else { kk = ck[i]; x = fsub(F, cv[i], fmul(F, s, bv[j])); ++i; ++j; }
+    if (!fe_is_zero(x)) { ok[w] = kk; ov[w] = x; ++w; }
+  }
+  return w;
+}
+
+// fix_raw_constraint (algebra.rs:1309-1324) on zero-free sorted maps a, b, c (in place).
+// c must have room for |c| + max(|a|, |b|) entries plus scratch of the same size after it.
+__device__ inline void d_fix(const FieldP &F, uint32_t *ak, Fe *av, uint32_t &an, uint32_t *bk, Fe *bv,
+                             uint32_t &bn, uint32_t *ck, Fe *cv, uint32_t &cn, uint32_t *tk, Fe *tv) {
+  if (an == 0 || bn == 0) { an = 0; bn = 0; return; }
+  const uint32_t *ok_;
+  const Fe *ov_;
+  uint32_t on;
+  Fe s;
+  if (an == 1 && ak[0] == 0) { s = av[0]; ok_ = bk; ov_ = bv; on = bn; }
+  else if (bn == 1 && bk[0] == 0) { s = bv[0]; ok_ = ak; ov_ = av; on = an; }
+  else return;
+  uint32_t w = d_axpy_merge(F, ck, cv, cn, ok_, ov_, on, s, tk, tv);
+  for (uint32_t i = 0; i < w; ++i) { ck[i] = tk[i]; cv[i] = tv[i]; }
+  cn = w;
+  an = 0;
+  bn = 0;
+}
+
+// ---------------------------------------------------------------- load / convert / validate
+// Sorts every row by key and validates it (distinct keys < S, canonical nonzero values).
+__global__ void k_sort_validate(FieldP F, const uint64_t *ptr, uint32_t *key, Fe *val, uint64_t n,
+                                uint64_t S, int *err) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    uint64_t b = ptr[r], e = ptr[r + 1];
+    uint32_t *k = key + b;
+    Fe *v = val + b;
+    uint32_t m = (uint32_t)(e - b);
+    for (uint32_t i = 1; i < m; ++i) {
+      uint32_t kk = k[i];
+      Fe vv = v[i];
+      uint32_t j = i;
+      while (j > 0 && k[j - 1] > kk) { k[j] = k[j - 1]; v[j] = v[j - 1]; --j; }
+      k[j] = kk;
+      v[j] = vv;
+    }
+    for (uint32_t i = 0; i < m; ++i) {
+      if (k[i] >= S || (i > 0 && k[i] == k[i - 1]) || fe_is_zero(v[i]) || geq4(v[i].l, F.p)) atomicOr(err, 1);
+    }
+  }
+}
+// canonical -> Montgomery copy (working buffers), plus len/off for ragged rows.
+__global__ void k_to_mont(FieldP F, const Fe *src, Fe *dst, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) dst[i] = fto_mont(F, src[i]);
+}
+__global__ void k_ptr_to_ragged(const uint64_t *ptr, uint64_t *off, uint32_t *len, uint64_t n, uint64_t extra) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    off[r] = ptr[r] + extra * r;
+    len[r] = (uint32_t)(ptr[r + 1] - ptr[r]);
+  }
+}
+__global__ void k_fill_i32(int32_t *p, int32_t v, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) p[i] = v;
+}
+
+// ---------------------------------------------------------------- eq_simplification (:126-251)
+__device__ __forceinline__ uint32_t uf_load(uint32_t *uf, uint32_t x) {
+  return __hip_atomic_load(&uf[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint32_t uf_find(uint32_t *uf, uint32_t x) {
+  uint32_t p = uf_load(uf, x);
+  while (p != x) {
+    uint32_t gp = uf_load(uf, p);
+    if (gp != p) __hip_atomic_store(&uf[x], gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = p;
+    p = gp;
+  }
+  return x;
+}
+// build_clusters over the equalities: connected components of the 2-signal rows.
+__global__ void k_eq_union(const uint64_t *ptr, const uint32_t *key, uint64_t n, uint32_t *uf, int *err) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    if (ptr[r + 1] - ptr[r] != 2 || key[ptr[r]] == 0) { atomicOr(err, 2); continue; }
+    uint32_t a = key[ptr[r]], b = key[ptr[r] + 1];
+    for (;;) {
+      a = uf_find(uf, a);
+      b = uf_find(uf, b);
+      if (a == b) break;
+      if (a > b) { uint32_t t = a; a = b; b = t; }
+      uint32_t old = atomicCAS(&uf[b], b, a);
+      if (old == b) break;
+      b = old;
+    }
+  }
+}
+// per-component statistics: #rows, max row index (= arena index, i.e. cluster order),
+// min forbidden and min removable signal (eq_cluster_simplification :158-179).
+__global__ void k_eq_stats(const uint64_t *ptr, const uint32_t *key, uint64_t n, uint32_t *uf,
+                           const uint8_t *forb, uint32_t *cnt, int32_t *maxrow, uint32_t *minf,
+                           uint32_t *minr, uint8_t *in_eq) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    uint32_t a = key[ptr[r]], b = key[ptr[r] + 1];
+    uint32_t root = uf_find(uf, a);
+    atomicAdd(&cnt[root], 1u);
+    atomicMax(&maxrow[root], (int32_t)r);
+    for (int t = 0; t < 2; ++t) {
+      uint32_t s = t ? b : a;
+      in_eq[s] = 1;
+      if (forb[s]) atomicMin(&minf[root], s);
+      else atomicMin(&minr[root], s);
+    }
+  }
+}
+// every removable signal := representative (min forbidden, else min removable).
+__global__ void k_eq_assign(const uint64_t *ptr, const uint32_t *key, uint64_t n, uint32_t *uf,
+                            const uint8_t *forb, const uint32_t *minf, const uint32_t *minr,
+                            int32_t *eq_rep, uint8_t *deleted, uint32_t *bf_list, uint32_t *bf_n) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    uint32_t a = key[ptr[r]], b = key[ptr[r] + 1];
+    uint32_t root = uf_find(uf, a);
+    uint32_t rh = minf[root] != RS_NONE ? minf[root] : minr[root];
+    for (int t = 0; t < 2; ++t) {
+      uint32_t s = t ? b : a;
+      if (!forb[s] && s != rh) { eq_rep[s] = (int32_t)rh; deleted[s] = 1; }
+    }
+    if (forb[a] && forb[b]) bf_list[atomicAdd(bf_n, 1u)] = (uint32_t)r;
+  }
+}
+__global__ void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t *dst, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) dst[i] = src[idx[i]];
+}
+
+// ---------------------------------------------------------------- constant equalities (:253-273)
+// Applies the eq frame (fast_encoded_constraint_substitution + fix) to a C-only row in place;
+// renaming never grows a row.
+__device__ inline uint32_t d_rename_row(const FieldP &F, uint32_t *k, Fe *v, uint32_t n, const int32_t *eq_rep) {
+  bool any = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    int32_t t = eq_rep[k[i]];
+    if (t >= 0) { k[i] = (uint32_t)t; any = true; }
+  }
+  if (!any) return n;
+  n = d_sort_combine(F, k, v, n);
+  return d_drop_zeros(k, v, n);
+}
+__global__ void k_rename_rows(FieldP F, DRows R, const int32_t *eq_rep) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride())
+    R.len[r] = d_rename_row(F, R.key + R.off[r], R.val + R.off[r], R.len[r], eq_rep);
+}
+// picks, per signal, the last constant equality (HashMap insert: last wins) and lists the
+// forbidden ones, which stay as constraints.
+__global__ void k_const_pick(DRows R, const uint8_t *forb, int32_t *ce_last, uint8_t *deleted,
+                             uint32_t *cons_list, uint32_t *cons_n, int *err) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride()) {
+    const uint32_t *k = R.key + R.off[r];
+    uint32_t n = R.len[r];
+    uint32_t s = n ? k[n - 1] : 0;
+    if (s == 0) { atomicOr(err, 4); continue; }
+    if (forb[s]) { cons_list[atomicAdd(cons_n, 1u)] = (uint32_t)r; continue; }
+    atomicMax(&ce_last[s], (int32_t)r);
+    deleted[s] = 1;
+  }
+}
+// clear_signal (algebra.rs:1108-1124): s := c / (-k)   (an empty map when c == 0 -> value 0)
+__global__ void k_const_value(FieldP F, DRows R, const uint8_t *forb, const int32_t *ce_last, Fe *ce_val,
+                              uint8_t *ce_has) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride()) {
+    const uint32_t *k = R.key + R.off[r];
+    const Fe *v = R.val + R.off[r];
+    uint32_t n = R.len[r];
+    if (n == 0) continue;
+    uint32_t s = k[n - 1];
+    if (forb[s] || ce_last[s] != (int32_t)r) continue;
+    Fe c = (n == 2 && k[0] == 0) ? v[0] : fe_zero();
+    Fe inv = finv(F, fneg(F, v[n - 1]));
+    ce_val[s] = fmul(F, c, inv);
+    ce_has[s] = 1;
+  }
+}
+// eq frame then constant frame on the linear rows (each frame + fix, :493-527); capacity len+1.
+__global__ void k_linear_frames12(FieldP F, DRows R, const int32_t *eq_rep, const uint8_t *ce_has, const Fe *ce_val) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride()) {
+    uint32_t *k = R.key + R.off[r];
+    Fe *v = R.val + R.off[r];
+    uint32_t n = d_rename_row(F, k, v, R.len[r], eq_rep);
+    bool any = false;
+    for (uint32_t i = 0; i < n; ++i)
+      if (ce_has[k[i]]) any = true;
+    if (any) {
+      Fe c0 = fe_zero();
+      uint32_t w = 0;
+      for (uint32_t i = 0; i < n; ++i) {
+        if (ce_has[k[i]]) c0 = fadd(F, c0, fmul(F, v[i], ce_val[k[i]]));
+        else if (k[i] == 0) c0 = fadd(F, c0, v[i]);
+        else { k[w] = k[i]; v[w] = v[i]; ++w; }
+      }
+      // key 0 goes first (smallest key)
+      for (uint32_t i = w; i > 0; --i) { k[i] = k[i - 1]; v[i] = v[i - 1]; }
+      k[0] = 0;
+      v[0] = c0;
+      n = d_drop_zeros(k, v, w + 1);
+    }
+    R.len[r] = n;
+  }
+}
+
+// ---------------------------------------------------------------- per-cluster elimination
+// full_simplification (simplification_utils.rs:543-581): one thread per cluster.
+struct ElimArgs {
+  FieldP F;
+  DRows rows;               // linear rows of this round
+  const uint32_t *perm;     // rows in cluster order (clusters concatenated)
+  const uint64_t *cl_off;   // cluster c = perm[cl_off[c] .. cl_off[c+1])
+  uint64_t n_clusters;
+  const uint8_t *forb;
+  int old_heur;
+  // dense per-signal scratch (clusters are signal-disjoint); reset by the kernel
+  int32_t *holder_idx, *occ, *rep_pos, *noov;
+  uint8_t *del;
+  // per-slot arrays (slot = position in perm)
+  uint32_t *h_sig;
+  Fe *h_coef;
+  uint64_t *h_off;
+  uint32_t *h_len;
+  uint32_t *tmp;            // scratch u32 per slot
+  Fe *ftmp;                 // scratch Fe per slot
+  uint8_t *dead;            // p4 rows emptied by the uniques phase
+  uint32_t *order;          // p4 deletion order
+  uint64_t *l_off;          // leftovers
+  uint32_t *l_len;
+  uint32_t *n_sub, *n_left; // per cluster
+  // outputs
+  int32_t *sub_of;          // dense: signal -> slot of its substitution
+  uint8_t *deleted;
+  // pool
+  uint32_t *pk;
+  Fe *pv;
+  unsigned long long *pool_top;
+  uint64_t pool_cap;
+  int *err;
+};
+
+__device__ __forceinline__ uint64_t pool_alloc(const ElimArgs &A, uint64_t n) {
+  unsigned long long o = atomicAdd(A.pool_top, (unsigned long long)n);
+  if (o + n > A.pool_cap) { atomicOr(A.err, 8); return RS_NONE; }
+  return (uint64_t)o;
+}
+
+// clear_signal_not_normalized (algebra.rs:1126-1136): to = row minus key, {0: 0} ensured.
+__device__ inline bool d_clear_nn(const ElimArgs &A, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
+                                  Fe &coef, uint64_t &to_off, uint32_t &to_len) {
+  coef = fneg(A.F, v[oi]);
+  bool has0 = n > 0 && k[0] == 0 && oi != 0;
+  uint32_t m = n - 1 + (has0 ? 0 : 1);
+  uint64_t o = pool_alloc(A, m);
+  if (o == RS_NONE) return false;
+  uint32_t w = 0;
+  if (!has0) { A.pk[o] = 0; A.pv[o] = fe_zero(); w = 1; }
+  for (uint32_t i = 0; i < n; ++i)
+    if (i != oi) { A.pk[o + w] = k[i]; A.pv[o + w] = v[i]; ++w; }
+  to_off = o;
+  to_len = m;
+  return true;
+}
+// treat_constraint_3/4 conflict: work = coef*R - c2*L, zeros dropped; L = row minus key (+{0:0}).
+__device__ inline bool d_merge(const ElimArgs &A, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
+                               const Fe &coef, const Fe &c2, uint64_t r_off, uint32_t r_len,
+                               uint64_t &w_off, uint32_t &w_len) {
+  const FieldP &F = A.F;
+  uint64_t o = pool_alloc(A, (uint64_t)n + r_len + 1);
+  if (o == RS_NONE) return false;
+  const uint32_t *rk = A.pk + r_off;
+  const Fe *rv = A.pv + r_off;
+  uint32_t i = 0, j = 0, w = 0;
+  while (i < n || j < r_len) {
+    if (i == oi) { ++i; continue; }
+    uint32_t kk;
+    Fe x;
+    if (j >= r_len || (i < n && k[i] < rk[j])) { kk = k[i]; x = fneg(F, fmul(F, c2, v[i])); ++i; }
+    else if (i >= n || rk[j] < k[i]) { kk = rk[j]; x = fmul(F, coef, rv[j]); ++j; }
+    else { kk = k[i]; x = fsub(F, fmul(F, coef, rv[j]), fmul(F, c2, v[i])); ++i; ++j; }
+    if (!fe_is_zero(x)) { A.pk[o + w] = kk; A.pv[o + w] = x; ++w; }
+  }
+  w_off = o;
+  w_len = w;
+  return true;
+}
+// Substitution::apply_substitution with a single change (raw_substitution, algebra.rs:1279-1294):
+// out = src[from := val*rhs]; every rhs key is inserted, zeros kept; both maps hold key 0.
+__device__ inline bool d_raw_sub(const ElimArgs &A, uint64_t s_off, uint32_t s_len, uint32_t from, uint64_t r_off,
+                                 uint32_t r_len, uint64_t &o_off, uint32_t &o_len) {
+  const FieldP &F = A.F;
+  const uint32_t *sk = A.pk + s_off;
+  const Fe *sv = A.pv + s_off;
+  const uint32_t *rk = A.pk + r_off;
+  const Fe *rv = A.pv + r_off;
+  Fe val = fe_zero();
+  uint32_t fi = RS_NONE;
+  for (uint32_t i = 0; i < s_len; ++i)
+    if (sk[i] == from) { val = sv[i]; fi = i; break; }
+  if (fi == RS_NONE) { o_off = s_off; o_len = s_len; return true; }
+  uint64_t o = pool_alloc(A, (uint64_t)s_len + r_len);
+  if (o == RS_NONE) return false;
+  uint32_t i = 0, j = 0, w = 0;
+  while (i < s_len || j < r_len) {
+    if (i == fi) { ++i; continue; }
+    if (j >= r_len || (i < s_len && sk[i] < rk[j])) { A.pk[o + w] = sk[i]; A.pv[o + w] = sv[i]; ++i; }
+    else if (i >= s_len || rk[j] < sk[i]) { A.pk[o + w] = rk[j]; A.pv[o + w] = fmul(F, val, rv[j]); ++j; }
+    else { A.pk[o + w] = sk[i]; A.pv[o + w] = fadd(F, sv[i], fmul(F, val, rv[j])); ++i; ++j; }
+    ++w;
+  }
+  o_off = o;
+  o_len = w;
+  return true;
+}
+
+__device__ inline void d_heap_sort_u32(uint32_t *a, uint32_t n) {
+  if (n < 2) return;
+  for (uint32_t start = n / 2; start-- > 0;) {
+    uint32_t root = start;
+    for (;;) {
+      uint32_t child = 2 * root + 1;
+      if (child >= n) break;
+      if (child + 1 < n && a[child] < a[child + 1]) ++child;
+      if (a[root] < a[child]) { uint32_t t = a[root]; a[root] = a[child]; a[child] = t; root = child; }
+      else break;
+    }
+  }
+  for (uint32_t end = n - 1; end > 0; --end) {
+    uint32_t t = a[0]; a[0] = a[end]; a[end] = t;
+    uint32_t root = 0;
+    for (;;) {
+      uint32_t child = 2 * root + 1;
+      if (child >= end) break;
+      if (child + 1 < end && a[child] < a[child + 1]) ++child;
+      if (a[root] < a[child]) { uint32_t tt = a[root]; a[root] = a[child]; a[child] = tt; root = child; }
+      else break;
+    }
+  }
+}
+
+// normalize_substitutions (:414-437) + create_nonoverlapping_substitutions(_4) (:451-479).
+// Slots [b, b+m) hold the holder; `seq` lists the signals in composition order.
+__device__ inline bool d_normalize_compose(const ElimArgs &A, uint64_t b, uint32_t m, const uint32_t *seq) {
+  const FieldP &F = A.F;
+  if (m == 0) return true;
+  // batch inversion (Montgomery's trick; exact inverses, so order-free)
+  Fe acc = A.h_coef[b];
+  A.ftmp[b] = acc;
+  for (uint32_t i = 1; i < m; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
+  Fe inv = finv(F, acc);
+  for (uint32_t i = m; i-- > 0;) {
+    Fe inv_i = i ? fmul(F, A.ftmp[b + i - 1], inv) : inv;
+    inv = fmul(F, inv, A.h_coef[b + i]);
+    Fe *v = A.pv + A.h_off[b + i];
+    for (uint32_t t = 0; t < A.h_len[b + i]; ++t) v[t] = fmul(F, v[t], inv_i);
+  }
+  for (uint32_t q = 0; q < m; ++q) {
+    uint32_t s = seq[q];
+    int32_t slot = A.holder_idx[s];
+    uint64_t off = A.h_off[slot];
+    uint32_t len = A.h_len[slot];
+    // collect the keys to apply first (take_substitutions_to_be_applied, :439-448)
+    const uint32_t *kk = A.pk + off;
+    uint32_t n_app = 0;
+    for (uint32_t t = 0; t < len; ++t)
+      if (A.noov[kk[t]] >= 0) ++n_app;
+    if (n_app) {
+      // keys of the original map, in ascending order; applying one never removes another
+      uint64_t orig_off = off;
+      uint32_t orig_len = len;
+      for (uint32_t t = 0; t < orig_len; ++t) {
+        uint32_t key = A.pk[orig_off + t];
+        int32_t ns = A.noov[key];
+        if (ns < 0) continue;
+        uint64_t no;
+        uint32_t nl;
+        if (!d_raw_sub(A, off, len, key, A.h_off[ns], A.h_len[ns], no, nl)) return false;
+        off = no;
+        len = nl;
+      }
+      A.h_off[slot] = off;
+      A.h_len[slot] = len;
+    }
+    A.noov[s] = slot;
+  }
+  return true;
+}
+
+__global__ void k_eliminate(ElimArgs A) {
+  const FieldP &F = A.F;
+  for (uint64_t c = gtid(); c < A.n_clusters; c += gstride()) {
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b);
+    const bool use4 = n >= 350 && n < 1000000 && !A.old_heur;
+    uint32_t m = 0, nl = 0, nd = 0;
+    bool ok = true;
+    if (!use4) {
+      // ---- substitution_process_3 + treat_constraint_3 + take_signal_3 (:143-154, :259-294, :368-377)
+      for (uint64_t idx = e; idx-- > b && ok;) {
+        uint32_t r = A.perm[idx];
+        const uint32_t *k = A.rows.key + A.rows.off[r];
+        const Fe *v = A.rows.val + A.rows.off[r];
+        uint32_t len = A.rows.len[r];
+        for (;;) {
+          if (len == 0) break;
+          uint32_t oi = RS_NONE;
+          for (uint32_t i = len; i-- > 0;)
+            if (!A.forb[k[i]]) { oi = i; break; }
+          if (oi == RS_NONE) {  // no takeable signal: leftover
+            uint64_t o = pool_alloc(A, len);
+            if (o == RS_NONE) { ok = false; break; }
+            for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
+            A.l_off[b + nl] = o;
+            A.l_len[b + nl] = len;
+            ++nl;
+            break;
+          }
+          uint32_t out = k[oi];
+          int32_t hi = A.holder_idx[out];
+          if (hi < 0) {
+            Fe coef;
+            uint64_t to_off;
+            uint32_t to_len;
+            if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+            A.holder_idx[out] = (int32_t)(b + m);
+            A.h_sig[b + m] = out;
+            A.h_coef[b + m] = coef;
+            A.h_off[b + m] = to_off;
+            A.h_len[b + m] = to_len;
+            ++m;
+            break;
+          }
+          uint64_t w_off;
+          uint32_t w_len;
+          if (!d_merge(A, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
+            ok = false;
+            break;
+          }
+          k = A.pk + w_off;
+          v = A.pv + w_off;
+          len = w_len;
+        }
+      }
+      // BTreeMap order: ascending signal
+      for (uint32_t i = 0; i < m; ++i) A.tmp[b + i] = A.h_sig[b + i];
+      d_heap_sort_u32(A.tmp + b, m);
+      if (ok) ok = d_normalize_compose(A, b, m, A.tmp + b);
+    } else {
+      // ---- substitution_process_4 (:156-185), SignalsInformation (:60-113)
+      uint32_t n_touch = 0;
+      uint64_t touch_off = 0;
+      {
+        uint64_t tot = 0;
+        for (uint64_t idx = b; idx < e; ++idx) tot += A.rows.len[A.perm[idx]];
+        touch_off = pool_alloc(A, tot + 1);
+        if (touch_off == RS_NONE) ok = false;
+      }
+      uint32_t *touch = A.pk + touch_off;
+      for (uint64_t idx = b; idx < e && ok; ++idx) {
+        uint32_t r = A.perm[idx];
+        const uint32_t *k = A.rows.key + A.rows.off[r];
+        uint32_t len = A.rows.len[r];
+        A.dead[idx] = 0;
+        for (uint32_t i = 0; i < len; ++i) {
+          uint32_t s = k[i];
+          if (A.forb[s]) continue;
+          if (A.occ[s] < 0) { A.occ[s] = 1; A.rep_pos[s] = (int32_t)(idx - b); touch[n_touch++] = s; }
+          else A.occ[s]++;
+        }
+      }
+      // uniques in ascending signal order (scratch after the touched list; can exceed n)
+      uint32_t n_u = 0;
+      uint64_t uniq_off = ok ? pool_alloc(A, (uint64_t)n_touch + 1) : RS_NONE;
+      if (uniq_off == RS_NONE) ok = false;
+      uint32_t *uniq = A.pk + (ok ? uniq_off : 0);
+      if (ok) {
+        for (uint32_t t = 0; t < n_touch; ++t)
+          if (A.occ[touch[t]] == 1) uniq[n_u++] = touch[t];
+        d_heap_sort_u32(uniq, n_u);
+      }
+      auto remove_constraint = [&](const uint32_t *k, uint32_t len) {
+        for (uint32_t i = 0; i < len; ++i)
+          if (!A.forb[k[i]] && A.occ[k[i]] >= 0) A.occ[k[i]]--;
+      };
+      for (uint32_t u = 0; u < n_u && ok; ++u) {
+        uint32_t s = uniq[u];
+        uint64_t idx = b + (uint64_t)A.rep_pos[s];
+        if (A.dead[idx]) continue;
+        A.dead[idx] = 1;
+        uint32_t r = A.perm[idx];
+        const uint32_t *k = A.rows.key + A.rows.off[r];
+        const Fe *v = A.rows.val + A.rows.off[r];
+        uint32_t len = A.rows.len[r];
+        remove_constraint(k, len);
+        uint32_t oi = 0;
+        while (k[oi] != s) ++oi;
+        Fe coef;
+        uint64_t to_off;
+        uint32_t to_len;
+        if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+        A.holder_idx[s] = (int32_t)(b + m);
+        A.h_sig[b + m] = s;
+        A.h_coef[b + m] = coef;
+        A.h_off[b + m] = to_off;
+        A.h_len[b + m] = to_len;
+        ++m;
+        A.occ[s] = -1;
+        A.del[s] = 1;
+        A.order[b + nd++] = s;
+      }
+      for (uint64_t idx = e; idx-- > b && ok;) {
+        if (A.dead[idx]) continue;
+        uint32_t r = A.perm[idx];
+        const uint32_t *k = A.rows.key + A.rows.off[r];
+        const Fe *v = A.rows.val + A.rows.off[r];
+        uint32_t len = A.rows.len[r];
+        remove_constraint(k, len);
+        for (;;) {
+          if (len == 0) break;
+          // take_signal_4 (:379-411), HashMap order := ascending
+          uint32_t oi = RS_NONE;
+          int32_t occ_ret = -1;
+          for (uint32_t i = 0; i < len; ++i) {
+            uint32_t s = k[i];
+            if (A.forb[s]) continue;
+            if (A.del[s]) { oi = i; break; }
+            int32_t c2 = A.occ[s];
+            if (c2 < 0) { atomicOr(A.err, 16); c2 = 0; }
+            if (occ_ret < 0 || c2 < occ_ret) { oi = i; occ_ret = c2; }
+            else if (c2 == occ_ret && k[oi] < s) oi = i;
+          }
+          if (oi == RS_NONE) {
+            uint64_t o = pool_alloc(A, len);
+            if (o == RS_NONE) { ok = false; break; }
+            for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
+            A.l_off[b + nl] = o;
+            A.l_len[b + nl] = len;
+            ++nl;
+            break;
+          }
+          uint32_t out = k[oi];
+          int32_t hi = A.holder_idx[out];
+          if (hi < 0) {
+            Fe coef;
+            uint64_t to_off;
+            uint32_t to_len;
+            if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+            A.holder_idx[out] = (int32_t)(b + m);
+            A.h_sig[b + m] = out;
+            A.h_coef[b + m] = coef;
+            A.h_off[b + m] = to_off;
+            A.h_len[b + m] = to_len;
+            ++m;
+            A.occ[out] = -1;
+            A.del[out] = 1;
+            A.order[b + nd++] = out;
+            break;
+          }
+          uint64_t w_off;
+          uint32_t w_len;
+          if (!d_merge(A, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
+            ok = false;
+            break;
+          }
+          k = A.pk + w_off;
+          v = A.pv + w_off;
+          len = w_len;
+        }
+      }
+      for (uint32_t t = 0; t < n_touch; ++t) A.occ[touch[t]] = -1;
+      for (uint32_t t = 0; t < nd; ++t) A.del[A.order[b + t]] = 0;
+      // composition order: deletion order, newest first
+      uint32_t *seq = A.tmp + b;
+      for (uint32_t t = 0; t < nd; ++t) seq[t] = A.order[b + nd - 1 - t];
+      if (ok) ok = d_normalize_compose(A, b, m, seq);
+    }
+    for (uint32_t i = 0; i < m; ++i) {
+      uint32_t s = A.h_sig[b + i];
+      A.holder_idx[s] = -1;
+      A.noov[s] = -1;
+      A.sub_of[s] = (int32_t)(b + i);
+      A.deleted[s] = 1;
+    }
+    A.n_sub[c] = m;
+    A.n_left[c] = nl;
+    if (!ok) atomicOr(A.err, 8);
+  }
+}
+
+// ---------------------------------------------------------------- substitution frames
+// obtain_and_simplify_non_linear (non_linear_utils.rs:6-31): frames [eq, const, linear], then fix.
+struct FrameArgs {
+  FieldP F;
+  const int32_t *eq_rep;   // frame 1: signal -> representative (Signal substitution)
+  const uint8_t *ce_has;   // frame 2: signal -> constant
+  const Fe *ce_val;
+  const int32_t *sub_of;   // frame 3: signal -> slot of its RHS in the pool
+  const uint64_t *h_off;
+  const uint32_t *h_len;
+  const uint32_t *pk;
+  const Fe *pv;
+};
+
+__device__ __forceinline__ uint32_t d_frame_weight(const FrameArgs &A, uint32_t k) {
+  int32_t t = A.eq_rep ? A.eq_rep[k] : -1;
+  uint32_t k1 = t >= 0 ? (uint32_t)t : k;
+  if (A.ce_has && A.ce_has[k1]) return 1;
+  int32_t s = A.sub_of[k1];
+  return s >= 0 ? A.h_len[s] : 1;
+}
+
+// Expands one linear combination through the frames into [k, v) (capacity from d_frame_weight + 1)
+__device__ inline uint32_t d_apply_frames(const FrameArgs &A, const uint32_t *ik, const Fe *iv, uint32_t n,
+                                          uint32_t *k, Fe *v, uint32_t cap) {
+  const FieldP &F = A.F;
+  // place the input at the tail of the region, frames 1-2 in place there
+  uint32_t base = cap - n;
+  for (uint32_t i = 0; i < n; ++i) { k[base + i] = ik[i]; v[base + i] = iv[i]; }
+  uint32_t *tk = k + base;
+  Fe *tv = v + base;
+  bool any = false;
+  if (A.eq_rep)
+    for (uint32_t i = 0; i < n; ++i) {
+      int32_t t = A.eq_rep[tk[i]];
+      if (t >= 0) { tk[i] = (uint32_t)t; any = true; }
+    }
+  if (any) n = d_sort_combine(F, tk, tv, n);
+  if (A.ce_has) {
+    any = false;
+    for (uint32_t i = 0; i < n; ++i)
+      if (A.ce_has[tk[i]]) { tv[i] = fmul(F, tv[i], A.ce_val[tk[i]]); tk[i] = 0; any = true; }
+    if (any) n = d_sort_combine(F, tk, tv, n);
+  }
+  // frame 3 expands: write from the front, reading from the (shrunk) tail copy
+  uint32_t rb = cap - n;
+  if (rb != base)
+    for (uint32_t i = n; i-- > 0;) { k[rb + i] = tk[i]; v[rb + i] = tv[i]; }  // overlapping: copy backwards
+  uint32_t w = 0;
+  any = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t kk = k[rb + i];
+    Fe vv = v[rb + i];
+    int32_t s = A.sub_of[kk];
+    if (s >= 0) {
+      any = true;
+      const uint32_t *rk = A.pk + A.h_off[s];
+      const Fe *rv = A.pv + A.h_off[s];
+      uint32_t rl = A.h_len[s];
+      for (uint32_t j = 0; j < rl; ++j) { k[w] = rk[j]; v[w] = fmul(F, vv, rv[j]); ++w; }
+    } else {
+      k[w] = kk;
+      v[w] = vv;
+      ++w;
+    }
+  }
+  if (any) w = d_sort_combine(F, k, v, w);
+  return d_drop_zeros(k, v, w);
+}
+
+struct NLArgs {
+  FrameArgs fr;
+  DRows a, b, c;       // input rows
+  DRows oa, ob, oc;    // output rows (off/cap computed by the count pass)
+  uint64_t *cap_a, *cap_b, *cap_c;
+  unsigned long long *bytes;  // algorithmic bytes counter
+};
+
+__global__ void k_nl_count(NLArgs A) {
+  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
+    uint64_t ca = 1, cb = 1, cc = 1;
+    for (uint32_t i = 0; i < A.a.len[r]; ++i) ca += d_frame_weight(A.fr, A.a.key[A.a.off[r] + i]);
+    for (uint32_t i = 0; i < A.b.len[r]; ++i) cb += d_frame_weight(A.fr, A.b.key[A.b.off[r] + i]);
+    for (uint32_t i = 0; i < A.c.len[r]; ++i) cc += d_frame_weight(A.fr, A.c.key[A.c.off[r] + i]);
+    A.cap_a[r] = ca;
+    A.cap_b[r] = cb;
+    A.cap_c[r] = 2 * cc + (ca > cb ? ca : cb);  // expansion + scratch for c - a0*b
+  }
+}
+
+__global__ void k_nl_fill(NLArgs A) {
+  unsigned long long bytes = 0;
+  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
+    uint64_t oa = A.oa.off[r], ob = A.ob.off[r], oc = A.oc.off[r];
+    uint32_t capa = (uint32_t)A.cap_a[r], capb = (uint32_t)A.cap_b[r];
+    uint32_t capc = (uint32_t)A.cap_c[r];
+    uint32_t mx = capa > capb ? capa : capb;
+    uint32_t cc = (capc - mx) / 2;
+    uint32_t na = d_apply_frames(A.fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
+    uint32_t nb = d_apply_frames(A.fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
+    uint32_t nc = d_apply_frames(A.fr, A.c.key + A.c.off[r], A.c.val + A.c.off[r], A.c.len[r], A.oc.key + oc, A.oc.val + oc, cc);
+    d_fix(A.fr.F, A.oa.key + oa, A.oa.val + oa, na, A.ob.key + ob, A.ob.val + ob, nb, A.oc.key + oc, A.oc.val + oc,
+          nc, A.oc.key + oc + cc, A.oc.val + oc + cc);
+    A.oa.len[r] = na;
+    A.ob.len[r] = nb;
+    A.oc.len[r] = nc;
+    bytes += 36ull * (A.a.len[r] + A.b.len[r] + A.c.len[r] + na + nb + nc) + 24;
+  }
+  atomicAdd(A.bytes, bytes);
+}
+
+// ---------------------------------------------------------------- rounds >= 2 on the storage
+// apply_substitution_to_map (:345-396) restated per row: the final content is
+// fix(all of this round's substitutions applied) and `turn` is the rank (in the round's
+// substitution order) of the first substitution after which the row is linear.
+struct RoundArgs {
+  FieldP F;
+  DRows a, b, c;        // storage rows (updated in place into oa/ob/oc)
+  DRows oa, ob, oc;
+  uint64_t *cap_a, *cap_b, *cap_c;
+  const int32_t *sub_of;   // signal -> slot (this round)
+  const int32_t *rank_of;  // signal -> position in this round's ordered list
+  const uint64_t *h_off;
+  const uint32_t *h_len;
+  const uint32_t *pk;
+  const Fe *pv;
+  int32_t *turn;           // out: rank or -1
+  uint8_t *touched;        // out: row contained a substituted signal
+  uint32_t *tmpk;          // per-row scratch: 2 * cap_c entries at 2 * (C offset - c_base)
+  Fe *tmpv;
+  uint64_t c_base;
+};
+
+__global__ void k_round_count(RoundArgs A) {
+  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
+    uint64_t ca = 1, cb = 1, cc = 1;
+    bool hit = false;
+    for (uint32_t i = 0; i < A.a.len[r]; ++i) { int32_t s = A.sub_of[A.a.key[A.a.off[r] + i]]; ca += s >= 0 ? A.h_len[s] : 1; hit |= s >= 0; }
+    for (uint32_t i = 0; i < A.b.len[r]; ++i) { int32_t s = A.sub_of[A.b.key[A.b.off[r] + i]]; cb += s >= 0 ? A.h_len[s] : 1; hit |= s >= 0; }
+    for (uint32_t i = 0; i < A.c.len[r]; ++i) { int32_t s = A.sub_of[A.c.key[A.c.off[r] + i]]; cc += s >= 0 ? A.h_len[s] : 1; hit |= s >= 0; }
+    if (!hit) ca = cb = cc = 0;
+    A.cap_a[r] = ca;
+    A.cap_b[r] = cb;
+    A.cap_c[r] = hit ? 2 * cc + (ca > cb ? ca : cb) : 0;
+  }
+}
+
+// is the (zero-free, sorted) map empty or constant-only?
+__device__ __forceinline__ bool d_const_or_empty(const uint32_t *k, uint32_t n) { return n == 0 || (n == 1 && k[0] == 0); }
+
+__global__ void k_round_fill(RoundArgs A) {
+  const FieldP &F = A.F;
+  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
+    A.turn[r] = -1;
+    A.touched[r] = 0;
+    if (A.cap_c[r] == 0) continue;
+    A.touched[r] = 1;
+    FrameArgs fr;
+    fr.F = F;
+    fr.eq_rep = nullptr;
+    fr.ce_has = nullptr;
+    fr.ce_val = nullptr;
+    fr.sub_of = A.sub_of;
+    fr.h_off = A.h_off;
+    fr.h_len = A.h_len;
+    fr.pk = A.pk;
+    fr.pv = A.pv;
+    uint64_t oa = A.oa.off[r], ob = A.ob.off[r], oc = A.oc.off[r];
+    uint32_t capa = (uint32_t)A.cap_a[r], capb = (uint32_t)A.cap_b[r], capc = (uint32_t)A.cap_c[r];
+    uint32_t mx = capa > capb ? capa : capb;
+    uint32_t cc = (capc - mx) / 2;
+    // ---- first substitution (in round order) after which A or B is constant/empty
+    {
+      // applicable ranks from A u B, ascending; per-row scratch = [2*oc, 2*oc + 2*capc)
+      uint32_t *rk_ = A.tmpk + 2 * (oc - A.c_base);
+      uint32_t nr = 0;
+      for (int part = 0; part < 2; ++part) {
+        const DRows &P = part ? A.b : A.a;
+        for (uint32_t i = 0; i < P.len[r]; ++i) {
+          int32_t q = A.rank_of[P.key[P.off[r] + i]];
+          if (q >= 0) rk_[nr++] = (uint32_t)q;
+        }
+      }
+      d_heap_sort_u32(rk_, nr);
+      // incremental application on copies of A and B held in the output regions
+      uint32_t na = A.a.len[r], nb = A.b.len[r];
+      uint32_t *ak = A.oa.key + oa, *bk = A.ob.key + ob;
+      Fe *av = A.oa.val + oa, *bv = A.ob.val + ob;
+      for (uint32_t i = 0; i < na; ++i) { ak[i] = A.a.key[A.a.off[r] + i]; av[i] = A.a.val[A.a.off[r] + i]; }
+      for (uint32_t i = 0; i < nb; ++i) { bk[i] = A.b.key[A.b.off[r] + i]; bv[i] = A.b.val[A.b.off[r] + i]; }
+      if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = -2;  // already linear
+      for (uint32_t q = 0; q < nr && A.turn[r] == -1; ++q) {
+        if (q > 0 && rk_[q] == rk_[q - 1]) continue;
+        for (int part = 0; part < 2; ++part) {
+          uint32_t *pk_ = part ? bk : ak;
+          Fe *pv_ = part ? bv : av;
+          uint32_t &pn = part ? nb : na;
+          uint32_t pcap = part ? capb : capa;
+          // find the signal with this rank in the part
+          uint32_t fi = RS_NONE;
+          for (uint32_t i = 0; i < pn; ++i)
+            if (A.rank_of[pk_[i]] == (int32_t)rk_[q]) { fi = i; break; }
+          if (fi == RS_NONE) continue;
+          int32_t s = A.sub_of[pk_[fi]];
+          Fe val = pv_[fi];
+          const uint32_t *hk = A.pk + A.h_off[s];
+          const Fe *hv = A.pv + A.h_off[s];
+          uint32_t hl = A.h_len[s];
+          // merge (pn - 1 + hl <= pcap) via scratch tmp region after rk_
+          uint32_t *mk = A.tmpk + 2 * (oc - A.c_base) + capc;
+          Fe *mv = A.tmpv + 2 * (oc - A.c_base) + capc;
+          uint32_t i = 0, j = 0, w = 0;
+          while (i < pn || j < hl) {
+            if (i == fi) { ++i; continue; }
+            if (j >= hl || (i < pn && pk_[i] < hk[j])) { mk[w] = pk_[i]; mv[w] = pv_[i]; ++i; }
+            else if (i >= pn || hk[j] < pk_[i]) { mk[w] = hk[j]; mv[w] = fmul(F, val, hv[j]); ++j; }
+            else { mk[w] = pk_[i]; mv[w] = fadd(F, pv_[i], fmul(F, val, hv[j])); ++i; ++j; }
+            ++w;
+          }
+          w = d_drop_zeros(mk, mv, w);
+          (void)pcap;
+          for (uint32_t t = 0; t < w; ++t) { pk_[t] = mk[t]; pv_[t] = mv[t]; }
+          pn = w;
+        }
+        if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = (int32_t)rk_[q];
+      }
+    }
+    // ---- final content: fix(all substitutions applied)
+    uint32_t na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
+    uint32_t nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
+    uint32_t nc = d_apply_frames(fr, A.c.key + A.c.off[r], A.c.val + A.c.off[r], A.c.len[r], A.oc.key + oc, A.oc.val + oc, cc);
+    d_fix(F, A.oa.key + oa, A.oa.val + oa, na, A.ob.key + ob, A.ob.val + ob, nb, A.oc.key + oc, A.oc.val + oc, nc,
+          A.oc.key + oc + cc, A.oc.val + oc + cc);
+    A.oa.len[r] = na;
+    A.ob.len[r] = nb;
+    A.oc.len[r] = nc;
+  }
+}
+
+// ---------------------------------------------------------------- final assembly
+__global__ void k_mark_keys(DRows R, uint8_t *bits) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride())
+    for (uint32_t i = 0; i < R.len[r]; ++i) bits[R.key[R.off[r] + i]] = 1;
+}
+__global__ void k_mark_list(const uint32_t *sig, uint64_t n, uint8_t *bits) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) bits[sig[i]] = 1;
+}
+// rebuild_witness (:101-124): kept = !deleted && (forbidden || key of non_linear_map)
+__global__ void k_kept(const uint8_t *deleted, const uint8_t *forb, const uint8_t *nlmap, uint32_t *kept, uint64_t S) {
+  for (uint64_t s = gtid(); s < S; s += gstride()) kept[s] = (!deleted[s] && (forb[s] || nlmap[s])) ? 1u : 0u;
+}
+__global__ void k_l2w(const uint32_t *kept, const uint64_t *rank, int64_t *l2w, uint64_t S) {
+  for (uint64_t s = gtid(); s < S; s += gstride()) l2w[s] = kept[s] ? (int64_t)rank[s] : -1;
+}
+// gathers ragged rows (selected ids) into a compact CSR with canonical values
+__global__ void k_gather_rows(FieldP F, DRows R, const uint32_t *ids, uint64_t n, const uint64_t *optr,
+                              uint32_t *ocol, uint64_t *oval) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    uint32_t r = ids[i];
+    uint64_t o = optr[i];
+    for (uint32_t t = 0; t < R.len[r]; ++t) {
+      ocol[o + t] = R.key[R.off[r] + t];
+      Fe c = ffrom_mont(F, R.val[R.off[r] + t]);
+      oval[4 * (o + t) + 0] = c.l[0];
+      oval[4 * (o + t) + 1] = c.l[1];
+      oval[4 * (o + t) + 2] = c.l[2];
+      oval[4 * (o + t) + 3] = c.l[3];
+    }
+  }
+}
+__global__ void k_row_lens(DRows R, const uint32_t *ids, uint64_t n, uint64_t *lens) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) lens[i] = R.len[ids[i]];
+}
+// pool RHS / leftover copy-out (canonical) for the host bookkeeping of rounds >= 2
+__global__ void k_pool_to_canon(FieldP F, const uint64_t *off, const uint32_t *len, const uint64_t *optr, uint64_t n,
+                                const uint32_t *pk, const Fe *pv, uint32_t *ok, uint64_t *ov) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    uint64_t o = optr[i];
+    for (uint32_t t = 0; t < len[i]; ++t) {
+      ok[o + t] = pk[off[i] + t];
+      Fe c = ffrom_mont(F, pv[off[i] + t]);
+      for (int q = 0; q < 4; ++q) ov[4 * (o + t) + q] = c.l[q];
+    }
+  }
+}
+
+}  // namespace rs

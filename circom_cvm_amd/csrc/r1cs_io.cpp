@@ -1,0 +1,282 @@
+// r1cs_io.cpp -- the file formats around the path (host side of the drop-in boundary).
+//
+//   rs_read_r1cs_o0 : an --O0 .r1cs (dag/src/r1cs_porting.rs:5-135, which writes the rows in the
+//                     DFS order map_tree classifies them) -> rs_input, classified exactly like
+//                     dag/src/map_to_constraint_list.rs:12-44 with algebra.rs:1346-1372.
+//   rs_write_r1cs   : constraint_list/src/r1cs_porting.rs:4-124 + constraint_writers/src/
+//                     r1cs_writer.rs:16-353 (constraints section first, header, wire->label;
+//                     keys written in lexicographic order of their minimal little-endian bytes).
+//   rs_write_sym    : constraint_list/src/sym_porting.rs:5-37 -- the --O0 .sym lines with the
+//                     witness column remapped (-1 when the label is not a wire).
+#include <algorithm>
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+
+#include "host_common.hpp"
+
+namespace rs {
+
+static bool read_file(const char *path, std::vector<uint8_t> &buf) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  buf.resize(n > 0 ? n : 0);
+  bool ok = n <= 0 || fread(buf.data(), 1, n, f) == (size_t)n;
+  fclose(f);
+  return ok;
+}
+
+template <class T>
+static T rd(const uint8_t *p) {
+  T v;
+  memcpy(&v, p, sizeof(T));
+  return v;
+}
+
+// p - a == b  for canonical nonzero a, b  (signal_equals_signal: c1 * -1 == c0)
+static bool neg_equal(const uint64_t p[4], const uint64_t *a, const uint64_t *b) {
+  unsigned __int128 borrow = 0;
+  for (int i = 0; i < 4; ++i) {
+    unsigned __int128 d = (unsigned __int128)p[i] - a[i] - (uint64_t)borrow;
+    if ((uint64_t)d != b[i]) return false;
+    borrow = (d >> 64) & 1;
+  }
+  return true;
+}
+
+// LE-byte-string order key of a signal id (r1cs_writer.rs:49-72, sort of Vec<u8> keys).
+static inline uint64_t le_order_key(uint32_t k) {
+  int len = k == 0 ? 1 : (32 - __builtin_clz(k) + 7) / 8;
+  uint64_t key = 0;
+  for (int i = 0; i < 4; ++i) {
+    uint64_t b = i < len ? ((k >> (8 * i)) & 0xff) + 1 : 0;
+    key = (key << 9) | b;
+  }
+  return key;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_read_r1cs_o0(const char *path, rs_input **out) {
+  std::vector<uint8_t> buf;
+  if (!read_file(path, buf) || buf.size() < 12 || memcmp(buf.data(), "r1cs", 4) != 0) {
+    set_error(std::string("cannot read r1cs file ") + path);
+    return RS_E_INVALID;
+  }
+  uint32_t nsec = rd<uint32_t>(&buf[8]);
+  size_t off = 12;
+  size_t hdr_off = 0, cons_off = 0;
+  bool have_hdr = false, have_cons = false;
+  for (uint32_t s = 0; s < nsec; ++s) {
+    if (off + 12 > buf.size()) { set_error("truncated r1cs"); return RS_E_INVALID; }
+    uint32_t t = rd<uint32_t>(&buf[off]);
+    uint64_t sz = rd<uint64_t>(&buf[off + 4]);
+    off += 12;
+    if (t == 1 && !have_hdr) { hdr_off = off; have_hdr = true; }
+    if (t == 2 && !have_cons) { cons_off = off; have_cons = true; }
+    if (t == 4 || t == 5) {
+      set_error("custom-gate sections are out of scope for this back end");
+      return RS_E_INVALID;
+    }
+    off += sz;
+  }
+  if (!have_hdr || !have_cons) { set_error("r1cs without header/constraints"); return RS_E_INVALID; }
+  uint32_t fs = rd<uint32_t>(&buf[hdr_off]);
+  if (fs == 0 || fs > 32 || fs % 8) { set_error("unsupported field size"); return RS_E_INVALID; }
+  uint64_t p[4] = {0, 0, 0, 0};
+  memcpy(p, &buf[hdr_off + 4], fs);
+  size_t h = hdr_off + 4 + fs;
+  uint32_t n_out = rd<uint32_t>(&buf[h + 4]);
+  uint32_t n_pub = rd<uint32_t>(&buf[h + 8]);
+  uint32_t n_prv = rd<uint32_t>(&buf[h + 12]);
+  uint64_t n_labels = rd<uint64_t>(&buf[h + 16]);
+  uint32_t n_cons = rd<uint32_t>(&buf[h + 24]);
+
+  rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
+  in->prime_id = RS_PRIME_CUSTOM;
+  for (int i = 0; i < 8; ++i)
+    if (memcmp(kPrimes[i], p, 32) == 0) in->prime_id = i;
+  memcpy(in->prime, p, 32);
+  in->max_signal = n_labels;
+  in->n_pub_out = n_out;
+  in->n_pub_in = n_pub;
+  in->n_priv_in = n_prv;
+  // forbidden_if_main = {0} u outputs u public inputs (dag/src/lib.rs:174, 179-204)
+  in->n_forbidden = 1 + (uint64_t)n_out + n_pub;
+  in->forbidden = (uint32_t *)malloc(sizeof(uint32_t) * in->n_forbidden);
+  for (uint64_t i = 0; i < in->n_forbidden; ++i) in->forbidden[i] = (uint32_t)i;
+
+  Block ce, eq, lin, na, nb, nc;
+  size_t o = cons_off;
+  std::vector<uint32_t> ks[3];
+  std::vector<uint64_t> vs[3];
+  for (uint32_t r = 0; r < n_cons; ++r) {
+    for (int part = 0; part < 3; ++part) {
+      ks[part].clear();
+      vs[part].clear();
+      uint32_t n = rd<uint32_t>(&buf[o]);
+      o += 4;
+      for (uint32_t e = 0; e < n; ++e) {
+        ks[part].push_back(rd<uint32_t>(&buf[o]));
+        uint64_t v[4] = {0, 0, 0, 0};
+        memcpy(v, &buf[o + 4], fs);
+        vs[part].insert(vs[part].end(), v, v + 4);
+        o += 4 + fs;
+      }
+    }
+    bool lin_row = ks[0].empty() && ks[1].empty();
+    auto push = [&](Block &b, int part) {
+      for (size_t e = 0; e < ks[part].size(); ++e) b.push(ks[part][e], &vs[part][4 * e]);
+      b.end_row();
+    };
+    if (lin_row) {
+      const auto &k = ks[2];
+      bool has0 = std::find(k.begin(), k.end(), 0u) != k.end();
+      if ((has0 && k.size() == 2) || (!has0 && k.size() == 1)) {
+        push(ce, 2);  // signal_equals_constant
+      } else if (!has0 && k.size() == 2 && neg_equal(p, &vs[2][4], &vs[2][0])) {
+        push(eq, 2);  // signal_equals_signal
+      } else {
+        push(lin, 2);
+      }
+    } else {
+      push(na, 0);
+      push(nb, 1);
+      push(nc, 2);
+    }
+  }
+  to_lc(ce, in->cons_eq);
+  to_lc(eq, in->eq);
+  to_lc(lin, in->linear);
+  to_lc(na, in->nl_a);
+  to_lc(nb, in->nl_b);
+  to_lc(nc, in->nl_c);
+  *out = in;
+  return RS_OK;
+}
+
+void rs_input_free(rs_input *in) {
+  if (!in) return;
+  for (rs_lc *b : {&in->cons_eq, &in->eq, &in->linear, &in->nl_a, &in->nl_b, &in->nl_c}) free_lc(*b);
+  free(in->forbidden);
+  free(in);
+}
+
+int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out) {
+  uint64_t p[4];
+  if (!prime_of(in, p)) { set_error("unknown prime"); return RS_E_INVALID; }
+  int fs = field_size_bytes(p);
+  FILE *f = fopen(path, "wb");
+  if (!f) { set_error(std::string("cannot write ") + path); return RS_E_INVALID; }
+  std::vector<uint8_t> body;
+  body.reserve(1 << 20);
+  auto put32 = [&](std::vector<uint8_t> &b, uint32_t v) {
+    uint8_t t[4];
+    memcpy(t, &v, 4);
+    b.insert(b.end(), t, t + 4);
+  };
+  auto put64 = [&](std::vector<uint8_t> &b, uint64_t v) {
+    uint8_t t[8];
+    memcpy(t, &v, 8);
+    b.insert(b.end(), t, t + 8);
+  };
+  std::vector<std::pair<uint64_t, uint64_t>> ord;  // (order key, entry)
+  const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
+  fwrite("r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
+  // constraints section (r1cs_porting.rs:20-35) -- written first, size back-patched
+  std::vector<uint8_t> hdr;
+  put32(hdr, 2);
+  put64(hdr, 0);
+  long sec_pos = 12;
+  fwrite(hdr.data(), 1, hdr.size(), f);
+  uint64_t sec_size = 0;
+  for (uint64_t r = 0; r < out->n_constraints; ++r) {
+    body.clear();
+    for (int q = 0; q < 3; ++q) {
+      const rs_lc &b = *parts[q];
+      ord.clear();
+      for (uint64_t e = b.ptr[r]; e < b.ptr[r + 1]; ++e) {
+        uint32_t k = b.col[e];
+        uint32_t w;
+        if (k == 0) w = 0;
+        else {
+          int64_t ww = k < out->n_labels ? out->label_to_wire[k] : -1;
+          if (ww < 0) {
+            fclose(f);
+            set_error("constraint mentions a removed signal (apply_raw_correspondence panics)");
+            return RS_E_INTERNAL;
+          }
+          w = (uint32_t)ww;
+        }
+        ord.push_back({le_order_key(w), ((uint64_t)w << 32) | (e - b.ptr[r])});
+      }
+      std::sort(ord.begin(), ord.end());
+      put32(body, (uint32_t)ord.size());
+      for (auto &x : ord) {
+        put32(body, (uint32_t)(x.second >> 32));
+        uint64_t e = b.ptr[r] + (x.second & 0xffffffffu);
+        const uint8_t *v = (const uint8_t *)(b.val + 4 * e);
+        body.insert(body.end(), v, v + fs);
+      }
+    }
+    fwrite(body.data(), 1, body.size(), f);
+    sec_size += body.size();
+  }
+  long end_pos = ftell(f);
+  fseek(f, sec_pos + 4, SEEK_SET);
+  fwrite(&sec_size, 8, 1, f);
+  fseek(f, end_pos, SEEK_SET);
+  // header section (r1cs_writer.rs:246-269)
+  hdr.clear();
+  put32(hdr, 1);
+  put64(hdr, 4 + fs + 4 * 4 + 8 + 4);
+  put32(hdr, (uint32_t)fs);
+  hdr.insert(hdr.end(), (const uint8_t *)p, (const uint8_t *)p + fs);
+  put32(hdr, (uint32_t)out->n_wires);
+  put32(hdr, (uint32_t)in->n_pub_out);
+  put32(hdr, (uint32_t)in->n_pub_in);
+  put32(hdr, (uint32_t)in->n_priv_in);
+  put64(hdr, out->n_labels);
+  put32(hdr, (uint32_t)out->n_constraints);
+  fwrite(hdr.data(), 1, hdr.size(), f);
+  // wire -> label section (r1cs_porting.rs:48-53, get_witness_as_vec lib.rs:187-193)
+  std::vector<uint64_t> w2l(out->n_wires, 0);
+  for (uint64_t s = 0; s < out->n_labels; ++s)
+    if (out->label_to_wire[s] >= 0) w2l[out->label_to_wire[s]] = s;
+  hdr.clear();
+  put32(hdr, 3);
+  put64(hdr, 8 * out->n_wires);
+  fwrite(hdr.data(), 1, hdr.size(), f);
+  fwrite(w2l.data(), 8, w2l.size(), f);
+  bool ok = !ferror(f);
+  fclose(f);
+  if (!ok) { set_error("write error"); return RS_E_INVALID; }
+  return RS_OK;
+}
+
+int rs_write_sym(const char *o0_sym, const char *path, const rs_output *out) {
+  std::ifstream src(o0_sym);
+  if (!src) { set_error(std::string("cannot read ") + o0_sym); return RS_E_INVALID; }
+  FILE *f = fopen(path, "wb");
+  if (!f) { set_error(std::string("cannot write ") + path); return RS_E_INVALID; }
+  std::string line;
+  while (std::getline(src, line)) {
+    if (line.empty()) continue;
+    size_t c1 = line.find(','), c2 = line.find(',', c1 + 1);
+    if (c1 == std::string::npos || c2 == std::string::npos) { fclose(f); set_error("bad sym line"); return RS_E_INVALID; }
+    uint64_t orig = strtoull(line.c_str(), nullptr, 10);
+    int64_t w = orig < out->n_labels ? out->label_to_wire[orig] : -1;
+    fprintf(f, "%llu,%lld%s\n", (unsigned long long)orig, (long long)w, line.c_str() + c2);
+  }
+  fclose(f);
+  return RS_OK;
+}
+
+}  // extern "C"

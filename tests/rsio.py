@@ -14,55 +14,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import pyref as R  # noqa: E402
 
-U64_MAX = (1 << 64) - 1
-PRIME_IDS = {"bn128": 0, "bls12381": 1, "goldilocks": 2, "grumpkin": 3, "pallas": 4,
-             "vesta": 5, "secq256r1": 6, "bls12377": 7}
-
-
-class RsLc(C.Structure):
-    _fields_ = [("n_rows", C.c_uint64), ("nnz", C.c_uint64), ("ptr", C.POINTER(C.c_uint64)),
-                ("col", C.POINTER(C.c_uint32)), ("val", C.POINTER(C.c_uint64))]
-
-
-class RsInput(C.Structure):
-    _fields_ = [("prime_id", C.c_uint32), ("prime", C.c_uint64 * 4), ("max_signal", C.c_uint64),
-                ("n_pub_out", C.c_uint64), ("n_pub_in", C.c_uint64), ("n_priv_in", C.c_uint64),
-                ("n_forbidden", C.c_uint64), ("forbidden", C.POINTER(C.c_uint32)),
-                ("cons_eq", RsLc), ("eq", RsLc), ("linear", RsLc),
-                ("nl_a", RsLc), ("nl_b", RsLc), ("nl_c", RsLc)]
-
-
-class RsFlags(C.Structure):
-    _fields_ = [("flag_s", C.c_uint32), ("use_old_heuristics", C.c_uint32),
-                ("no_rounds", C.c_uint64), ("emit_substitution_log", C.c_uint32),
-                ("device", C.c_int32)]
-
-
-class RsOutput(C.Structure):
-    _fields_ = [("n_constraints", C.c_uint64), ("a", RsLc), ("b", RsLc), ("c", RsLc),
-                ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int64)),
-                ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64)]
-
-
-class RsStats(C.Structure):
-    _fields_ = [("total_ms", C.c_double), ("eq_ms", C.c_double), ("cluster_ms", C.c_double),
-                ("elim_ms", C.c_double), ("subst_ms", C.c_double), ("final_ms", C.c_double),
-                ("apply_kernel_ms", C.c_double), ("apply_kernel_launches", C.c_uint64),
-                ("apply_bytes", C.c_uint64), ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
-                ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
+sys.path.insert(0, ROOT)
+from circom_cvm_amd.abi import (PRIME_IDS, U64_MAX, RsFlags, RsInput, RsLc, RsOutput,  # noqa: E402
+                                RsStats, make_flags)
 
 
 def flags(level="O2", rounds=None, old=False, device=0) -> RsFlags:
-    f = RsFlags()
-    if level == "O1":
-        f.flag_s, f.no_rounds = 1, 0
-    elif level == "O2":
-        f.flag_s, f.no_rounds = 0, U64_MAX if rounds is None else rounds
-    else:
-        raise ValueError(level)
-    f.use_old_heuristics = 1 if old else 0
-    f.device = device
-    return f
+    return make_flags(level, rounds, old, device)
 
 
 # --------------------------------------------------------------------------- pyref <-> C ABI
