@@ -130,6 +130,9 @@ struct rs_engine {
   rs_stats stats{};
   std::vector<int32_t> sig2cl;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
+  Fe *heap_v = nullptr;
+  uint64_t heap_cap = 0;
 };
 
 namespace rs {
@@ -147,6 +150,13 @@ static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, co
     HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, E->st));
     HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, E->st));
   }
+}
+
+// H2D copy whose host buffer may be released right after the call: wait for it.
+static void h2d(rs_engine *E, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return;
+  HC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, E->st));
+  HC(hipStreamSynchronize(E->st));
 }
 
 // ---------------------------------------------------------------- scans
@@ -312,7 +322,7 @@ static void fetch_keys(rs_engine *E, const DRows &V, HostRows &H) {
   if (tot == 0) { for (uint64_t r = 0; r < V.n; ++r) H.off[r] = doff[r]; return; }
   uint64_t *d_doff = E->A.get<uint64_t>("fk.doff", V.n);
   uint32_t *d_key = E->A.get<uint32_t>("fk.key", tot);
-  HC(hipMemcpyAsync(d_doff, doff.data(), 8 * V.n, hipMemcpyHostToDevice, E->st));
+  h2d(E, d_doff, doff.data(), 8 * V.n);
   launch(E->st, k_compact_keys, V.n, V, (const uint64_t *)d_doff, d_key);
   HC(hipMemcpyAsync(H.key.data(), d_key, 4 * tot, hipMemcpyDeviceToHost, E->st));
   HC(hipStreamSynchronize(E->st));
@@ -335,9 +345,9 @@ static void fetch_pool_maps(rs_engine *E, const std::vector<uint64_t> &off, cons
   uint64_t *d_optr = E->A.get<uint64_t>("fp.optr", n + 1);
   uint32_t *d_k = E->A.get<uint32_t>("fp.k", tot);
   uint64_t *d_v = E->A.get<uint64_t>("fp.v", 4 * tot);
-  HC(hipMemcpyAsync(d_off, off.data(), 8 * n, hipMemcpyHostToDevice, E->st));
-  HC(hipMemcpyAsync(d_len, len.data(), 4 * n, hipMemcpyHostToDevice, E->st));
-  HC(hipMemcpyAsync(d_optr, optr.data(), 8 * (n + 1), hipMemcpyHostToDevice, E->st));
+  h2d(E, d_off, off.data(), 8 * n);
+  h2d(E, d_len, len.data(), 4 * n);
+  h2d(E, d_optr, optr.data(), 8 * (n + 1));
   launch(E->st, k_pool_to_canon, n, E->F, (const uint64_t *)d_off, (const uint32_t *)d_len, (const uint64_t *)d_optr, n,
          pk, pv, d_k, d_v);
   HC(hipMemcpyAsync(keys.data(), d_k, 4 * tot, hipMemcpyDeviceToHost, E->st));
@@ -407,12 +417,12 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   uint64_t n_slots = perm.size();
   uint32_t *d_perm = E->A.get<uint32_t>("el.perm", n_slots);
   uint64_t *d_cl = E->A.get<uint64_t>("el.cl", eo.n_clusters + 1);
-  if (n_slots) HC(hipMemcpyAsync(d_perm, perm.data(), 4 * n_slots, hipMemcpyHostToDevice, E->st));
-  HC(hipMemcpyAsync(d_cl, eo.cl_off.data(), 8 * (eo.n_clusters + 1), hipMemcpyHostToDevice, E->st));
+  if (n_slots) h2d(E, d_perm, perm.data(), 4 * n_slots);
+  h2d(E, d_cl, eo.cl_off.data(), 8 * (eo.n_clusters + 1));
   uint64_t tot_nnz = 0;
   for (uint64_t i = 0; i < n_slots; ++i) tot_nnz += H.len[perm[i]];
   uint64_t want = std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots));
-  for (int attempt = 0; attempt < 4; ++attempt) {
+  for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
     HC(hipMemsetAsync(P.top, 0, 8, E->st));
     HC(hipMemsetAsync(d_err, 0, 4, E->st));
@@ -456,7 +466,12 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     int err = 0;
     HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
     HC(hipStreamSynchronize(E->st));
-    if (err & 8) { want *= 2; continue; }
+    if (err & 8) {
+      size_t fr_ = 0, tot_ = 0;
+      (void)hipMemGetInfo(&fr_, &tot_);
+      want = std::min<uint64_t>(want * 4, (uint64_t)(fr_ * 0.8) / 36 + want / 2);
+      continue;
+    }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
     eo.n_sub.resize(eo.n_clusters);
     eo.n_left.resize(eo.n_clusters);
@@ -498,6 +513,89 @@ static void collect_leftovers(rs_engine *E, const ElimOut &eo, const Pool &P, st
   }
 }
 
+// ---------------------------------------------------------------- debug: host re-check of a round
+static void d2h_row(rs_engine *E, const DRows &R, uint64_t r, std::vector<uint32_t> &k, std::vector<Fe> &v) {
+  uint64_t off = 0;
+  uint32_t len = 0;
+  HC(hipMemcpy(&off, R.off + r, 8, hipMemcpyDeviceToHost));
+  HC(hipMemcpy(&len, R.len + r, 4, hipMemcpyDeviceToHost));
+  k.resize(len);
+  v.resize(len);
+  if (len) {
+    HC(hipMemcpy(k.data(), R.key + off, 4 * len, hipMemcpyDeviceToHost));
+    HC(hipMemcpy(v.data(), R.val + off, 32 * len, hipMemcpyDeviceToHost));
+  }
+}
+static void debug_check_round(rs_engine *E, const RoundArgs &ra, uint64_t n, uint64_t) {
+  HC(hipStreamSynchronize(E->st));
+  const FieldP &F = E->F;
+  std::vector<uint8_t> touched(n);
+  HC(hipMemcpy(touched.data(), ra.touched, n, hipMemcpyDeviceToHost));
+  int shown = 0;
+  for (uint64_t r = 0; r < n && shown < 3; ++r) {
+    if (!touched[r]) continue;
+    std::vector<uint32_t> ik[3], ok[3];
+    std::vector<Fe> iv[3], ov[3];
+    const DRows *in[3] = {&ra.a, &ra.b, &ra.c}, *out[3] = {&ra.oa, &ra.ob, &ra.oc};
+    std::map<uint32_t, Fe> exp[3];
+    for (int q = 0; q < 3; ++q) {
+      d2h_row(E, *in[q], r, ik[q], iv[q]);
+      d2h_row(E, *out[q], r, ok[q], ov[q]);
+      for (size_t i = 0; i < ik[q].size(); ++i) {
+        int32_t s = -1;
+        HC(hipMemcpy(&s, ra.sub_of + ik[q][i], 4, hipMemcpyDeviceToHost));
+        if (s < 0) {
+          Fe &x = exp[q][ik[q][i]];
+          if (!exp[q].count(ik[q][i])) x = fe_zero();
+          x = fadd(F, x, iv[q][i]);
+          continue;
+        }
+        uint64_t ho = 0;
+        uint32_t hl = 0;
+        HC(hipMemcpy(&ho, ra.h_off + s, 8, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(&hl, ra.h_len + s, 4, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> hk(hl);
+        std::vector<Fe> hv(hl);
+        HC(hipMemcpy(hk.data(), ra.pk + ho, 4 * hl, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(hv.data(), ra.pv + ho, 32 * hl, hipMemcpyDeviceToHost));
+        for (uint32_t j = 0; j < hl; ++j) {
+          auto it = exp[q].find(hk[j]);
+          Fe add = fmul(F, iv[q][i], hv[j]);
+          if (it == exp[q].end()) exp[q][hk[j]] = add;
+          else it->second = fadd(F, it->second, add);
+        }
+      }
+    }
+    // drop zeros (no fix re-check: report A/B/C expansions)
+    bool bad = false;
+    for (int q = 0; q < 3; ++q) {
+      std::vector<std::pair<uint32_t, Fe>> e;
+      for (auto &kv : exp[q])
+        if (!fe_is_zero(kv.second)) e.push_back(kv);
+      bool same = e.size() == ok[q].size();
+      for (size_t i = 0; same && i < e.size(); ++i) same = e[i].first == ok[q][i] && fe_eq(e[i].second, ov[q][i]);
+      if (!same) {
+        bad = true;
+        fprintf(stderr, "[rs-debug] row %llu part %d: in=%zu out=%zu expected=%zu\n", (unsigned long long)r, q,
+                ik[q].size(), ok[q].size(), e.size());
+        for (size_t i = 0; i < ik[q].size(); ++i) {
+          Fe c = ffrom_mont(F, iv[q][i]);
+          fprintf(stderr, "   in  %u:%llu\n", ik[q][i], (unsigned long long)c.l[0]);
+        }
+        for (size_t i = 0; i < ok[q].size(); ++i) {
+          Fe c = ffrom_mont(F, ov[q][i]);
+          fprintf(stderr, "   out %u:%llu\n", ok[q][i], (unsigned long long)c.l[0]);
+        }
+        for (auto &kv : e) {
+          Fe c = ffrom_mont(F, kv.second);
+          fprintf(stderr, "   exp %u:%llu\n", kv.first, (unsigned long long)c.l[0]);
+        }
+      }
+    }
+    if (bad) ++shown;
+  }
+}
+
 // ---------------------------------------------------------------- the run
 static void engine_run(rs_engine *E, const rs_flags *fl) {
   const uint64_t S = E->S;
@@ -517,7 +615,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   HC(hipMemsetAsync(d_deleted, 0, S, st));
   {
     uint32_t *d_fl = A.get<uint32_t>("forb.list", E->forbidden.size());
-    HC(hipMemcpyAsync(d_fl, E->forbidden.data(), 4 * E->forbidden.size(), hipMemcpyHostToDevice, st));
+    h2d(E, d_fl, E->forbidden.data(), 4 * E->forbidden.size());
     launch(st, k_mark_list, E->forbidden.size(), (const uint32_t *)d_fl, (uint64_t)E->forbidden.size(), d_forb);
   }
   for (const char *nm : {"el.holder_idx", "el.occ", "el.noov", "el.rep_pos"})
@@ -751,36 +849,30 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   mk_in(E->na, ia, "nla");
   mk_in(E->nb, ib, "nlb");
   mk_in(E->nc, ic, "nlc");
-  // storage rows live in one growable heap of (key, value) entries
+  // storage rows live in one growable heap of (key, value) entries, owned by the engine
   DRows sa{}, sb{}, sc{};
-  uint64_t heap_top = 0, heap_cap = 0;
-  uint32_t *heap_k = nullptr;
-  Fe *heap_v = nullptr;
+  uint64_t heap_top = 0;
+  uint32_t *heap_k = E->heap_k;
+  Fe *heap_v = E->heap_v;
   auto heap_reserve = [&](uint64_t need) {
-    if (heap_top + need <= heap_cap && heap_k) return;
-    uint64_t ncap = std::max<uint64_t>(heap_top + need, heap_cap * 2);
+    if (heap_top + need <= E->heap_cap && E->heap_k) return;
+    uint64_t ncap = std::max<uint64_t>(heap_top + need, E->heap_cap * 2);
+    ncap = std::max<uint64_t>(ncap, 1 << 16);
     uint32_t *nk = nullptr;
     Fe *nv = nullptr;
-    HC(hipMallocAsync((void **)&nk, 4 * std::max<uint64_t>(ncap, 1), st));
-    HC(hipMallocAsync((void **)&nv, 32 * std::max<uint64_t>(ncap, 1), st));
+    HC(hipStreamSynchronize(st));
+    HC(hipMalloc((void **)&nk, 4 * ncap));
+    HC(hipMalloc((void **)&nv, 32 * ncap));
     if (heap_top) {
-      HC(hipMemcpyAsync(nk, heap_k, 4 * heap_top, hipMemcpyDeviceToDevice, st));
-      HC(hipMemcpyAsync(nv, heap_v, 32 * heap_top, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(nk, E->heap_k, 4 * heap_top, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(nv, E->heap_v, 32 * heap_top, hipMemcpyDeviceToDevice, st));
+      HC(hipStreamSynchronize(st));
     }
-    if (heap_k) { HC(hipFreeAsync(heap_k, st)); HC(hipFreeAsync(heap_v, st)); }
-    heap_k = nk;
-    heap_v = nv;
-    heap_cap = ncap;
+    if (E->heap_k) { HC(hipFree(E->heap_k)); HC(hipFree(E->heap_v)); }
+    E->heap_k = heap_k = nk;
+    E->heap_v = heap_v = nv;
+    E->heap_cap = ncap;
   };
-  struct HeapGuard {
-    hipStream_t st;
-    uint32_t **k;
-    Fe **v;
-    ~HeapGuard() {
-      if (*k) (void)hipFreeAsync(*k, st);
-      if (*v) (void)hipFreeAsync(*v, st);
-    }
-  } heap_guard{st, &heap_k, &heap_v};
   unsigned long long *d_bytes = A.get<unsigned long long>("nl.bytes", 1);
   HC(hipMemsetAsync(d_bytes, 0, 8, st));
   FrameArgs fr;
@@ -880,6 +972,21 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   // ======================= rounds >= 2 (:613-646)
   bool apply_round = apply_linear && no_rounds > 0 && n_wl > 0;
   std::vector<uint32_t> extra_keys;  // keys appended to the signal map that no final row may hold
+  if (getenv("RS_DEBUG")) {
+    HC(hipStreamSynchronize(st));
+    fprintf(stderr, "[rs-debug] heap %p cap %llu top %llu n_st %llu n_wl %llu\n", (void *)heap_k,
+            (unsigned long long)E->heap_cap, (unsigned long long)heap_top, (unsigned long long)n_st, (unsigned long long)n_wl);
+    for (uint64_t r = 0; r < std::min<uint64_t>(n_st, 3); ++r) {
+      uint64_t o = 0; uint32_t l = 0;
+      HC(hipMemcpy(&o, tc_.off + r, 8, hipMemcpyDeviceToHost));
+      HC(hipMemcpy(&l, tc_.len + r, 4, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> kk; std::vector<Fe> vv;
+      d2h_row(E, tc_, r, kk, vv);
+      fprintf(stderr, "[rs-debug]  st %llu C off %llu len %u:", (unsigned long long)r, (unsigned long long)o, l);
+      for (size_t i = 0; i < kk.size(); ++i) fprintf(stderr, " %u:%llu", kk[i], (unsigned long long)ffrom_mont(E->F, vv[i]).l[0]);
+      fprintf(stderr, "\n");
+    }
+  }
   if (apply_round) {
     // host copy of the non-linear signal map: initial lists (ascending ids) + appended entries
     double Tm = now_ms();
@@ -957,8 +1064,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint32_t *d_us = A.get<uint32_t>("r.us", nU);
       int32_t *d_ur = A.get<int32_t>("r.ur", nU);
       if (nU) {
-        HC(hipMemcpyAsync(d_us, usig.data(), 4 * nU, hipMemcpyHostToDevice, st));
-        HC(hipMemcpyAsync(d_ur, urank.data(), 4 * nU, hipMemcpyHostToDevice, st));
+        h2d(E, d_us, usig.data(), 4 * nU);
+        h2d(E, d_ur, urank.data(), 4 * nU);
         launch(st, k_set_rank, nU, (const uint32_t *)d_us, (const int32_t *)d_ur, nU, rank_of);
       }
       // apply to every storage row (apply_substitution_to_map, :345-396)
@@ -997,6 +1104,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         ra.tmpv = A.get<Fe>("r.tmpv", 2 * (qc + 1));
         ra.c_base = heap_top - qc;  // row scratch = 2 * (its C offset - c_base)
         launch(st, k_round_fill, n_st, ra);
+        if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qa + qb + qc);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
         // turned rows
         uint64_t *tf = A.get<uint64_t>("r.tf", n_st), *tp = A.get<uint64_t>("r.tp", n_st);
@@ -1026,6 +1134,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           turned.push_back({((uint64_t)q << 32) | (pos & 0xffffffffu), r});
         }
         std::sort(turned.begin(), turned.end());
+        if (getenv("RS_DEBUG")) {
+          std::vector<uint8_t> tch(n_st);
+          HC(hipMemcpy(tch.data(), ra.touched, n_st, hipMemcpyDeviceToHost));
+          uint64_t nt = 0;
+          for (auto x : tch) nt += x;
+          fprintf(stderr, "[rs-debug] round: nU=%llu touched=%llu turned=%llu:", (unsigned long long)nU,
+                  (unsigned long long)nt, (unsigned long long)n_turn);
+          for (auto &t : turned) fprintf(stderr, " %u(q%llu)", t.second, (unsigned long long)(t.first >> 32));
+          fprintf(stderr, "\n");
+        }
       }
       // map appends (:369-377): every key of sub.to gets every visited row
       for (uint64_t i = 0; i < nU; ++i) {
@@ -1046,7 +1164,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       }
       if (nU) {  // reset the dense rank index
         std::vector<int32_t> neg(nU, -1);
-        HC(hipMemcpyAsync(d_ur, neg.data(), 4 * nU, hipMemcpyHostToDevice, st));
+        h2d(E, d_ur, neg.data(), 4 * nU);
         launch(st, k_set_rank, nU, (const uint32_t *)d_us, (const int32_t *)d_ur, nU, rank_of);
       }
       // next linear list: the turned rows, non-empty, in linear_id order
@@ -1068,7 +1186,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       lv.val = heap_v;
       if (nn) {
         uint32_t *d_ids = A.get<uint32_t>("lv.ids", nn);
-        HC(hipMemcpyAsync(d_ids, next_ids.data(), 4 * nn, hipMemcpyHostToDevice, st));
+        h2d(E, d_ids, next_ids.data(), 4 * nn);
         launch(st, k_view_rows, nn, (const uint64_t *)tc_.off, (const uint32_t *)tc_.len, (const uint32_t *)d_ids, nn, lv.off, lv.len);
       }
       // emptied storage rows (storage.replace(c_id, C::empty()))
@@ -1076,10 +1194,24 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         std::vector<uint32_t> all;
         for (auto &t : turned) all.push_back(t.second);
         uint32_t *d_all = A.get<uint32_t>("r.all", all.size());
-        HC(hipMemcpyAsync(d_all, all.data(), 4 * all.size(), hipMemcpyHostToDevice, st));
+        h2d(E, d_all, all.data(), 4 * all.size());
         launch(st, k_zero_c, all.size(), (const uint32_t *)d_all, (uint64_t)all.size(), tc_.len);
       }
       HC(hipStreamSynchronize(st));
+      if (getenv("RS_DEBUG")) {
+        for (uint64_t r = 0; r < std::min<uint64_t>(n_st, 24); ++r) {
+          uint32_t la = 0, lb = 0, lc = 0;
+          HC(hipMemcpy(&la, ta_.len + r, 4, hipMemcpyDeviceToHost));
+          HC(hipMemcpy(&lb, tb_.len + r, 4, hipMemcpyDeviceToHost));
+          HC(hipMemcpy(&lc, tc_.len + r, 4, hipMemcpyDeviceToHost));
+          std::vector<uint32_t> kk;
+          std::vector<Fe> vv;
+          d2h_row(E, tc_, r, kk, vv);
+          fprintf(stderr, "[rs-debug] storage %llu lens %u %u %u C:", (unsigned long long)r, la, lb, lc);
+          for (size_t i = 0; i < kk.size(); ++i) fprintf(stderr, " %u:%llu", kk[i], (unsigned long long)ffrom_mont(E->F, vv[i]).l[0]);
+          fprintf(stderr, "\n");
+        }
+      }
       E->stats.subst_ms += now_ms() - Tr;
       if (no_rounds > 0) no_rounds--;
       apply_round = nn > 0 && no_rounds > 0;
@@ -1091,7 +1223,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   if (lv.n) launch(st, k_mark_keys, lv.n, lv, nlmap);
   if (!extra_keys.empty()) {
     uint32_t *d_x = A.get<uint32_t>("fin.extra", extra_keys.size());
-    HC(hipMemcpyAsync(d_x, extra_keys.data(), 4 * extra_keys.size(), hipMemcpyHostToDevice, st));
+    h2d(E, d_x, extra_keys.data(), 4 * extra_keys.size());
     launch(st, k_mark_list, extra_keys.size(), (const uint32_t *)d_x, (uint64_t)extra_keys.size(), nlmap);
   }
   for (auto &c : lconst) host_fix(c);
@@ -1102,7 +1234,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         for (uint32_t k : c.k[q]) lk.push_back(k);
     if (!lk.empty()) {
       uint32_t *d_x = A.get<uint32_t>("fin.lk", lk.size());
-      HC(hipMemcpyAsync(d_x, lk.data(), 4 * lk.size(), hipMemcpyHostToDevice, st));
+      h2d(E, d_x, lk.data(), 4 * lk.size());
       launch(st, k_mark_list, lk.size(), (const uint32_t *)d_x, (uint64_t)lk.size(), nlmap);
     }
   }
@@ -1137,17 +1269,22 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
     uint32_t *keep_ids = A.get<uint32_t>("fin.keep", n_keep);
     if (n_keep) launch(st, k_scatter_ids, n_st, (const uint64_t *)nef, (const uint64_t *)nep, n_st, keep_ids);
-    // leftover linear rows keep their list order (non-empty by construction)
-    uint64_t n_lv = lv.n;
+    // leftover linear rows keep their list order; empty ones are dropped (extract_with(is_empty))
+    uint64_t n_lv = 0;
+    uint32_t *lv_ids = A.get<uint32_t>("fin.lvids", lv.n);
+    uint32_t *zero_len = A.get<uint32_t>("fin.zlen", lv.n);
+    if (lv.n) {
+      HC(hipMemsetAsync(zero_len, 0, 4 * lv.n, st));
+      uint64_t *lf = A.get<uint64_t>("fin.lvf", lv.n), *lp = A.get<uint64_t>("fin.lvp", lv.n);
+      launch(st, k_nonempty_flags, lv.n, (const uint32_t *)zero_len, (const uint32_t *)zero_len, (const uint32_t *)lv.len, lv.n, lf);
+      n_lv = excl_scan_u64(E, lf, lp, lv.n, "lvf");
+      launch(st, k_scatter_ids, lv.n, (const uint64_t *)lf, (const uint64_t *)lp, lv.n, lv_ids);
+    }
     uint64_t n_out = n_keep + n_lv;
     E->out_n_dev = n_out;
-    uint32_t *lv_ids = A.get<uint32_t>("fin.lvids", n_lv);
-    if (n_lv) launch(st, k_iota_u32, n_lv, lv_ids, n_lv);
     const DRows *parts[3] = {&ta_, &tb_, &tc_};
     const char *nm[3] = {"out.a", "out.b", "out.c"};
     DRows empty_lv = lv;
-    uint32_t *zero_len = A.get<uint32_t>("fin.zlen", n_lv);
-    if (n_lv) HC(hipMemsetAsync(zero_len, 0, 4 * n_lv, st));
     for (int q = 0; q < 3; ++q) {
       uint64_t *lens = A.get<uint64_t>(std::string(nm[q]) + ".lens", n_out + 1);
       uint64_t *ptr = A.get<uint64_t>(std::string(nm[q]) + ".ptr", n_out + 1);
@@ -1219,6 +1356,8 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->st) (void)hipStreamSynchronize(E->st);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
+  if (E->heap_k) (void)hipFree(E->heap_k);
+  if (E->heap_v) (void)hipFree(E->heap_v);
   if (E->st) (void)hipStreamDestroy(E->st);
   delete E;
 }

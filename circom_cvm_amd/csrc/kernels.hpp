@@ -375,6 +375,34 @@ __device__ inline bool d_raw_sub(const ElimArgs &A, uint64_t s_off, uint32_t s_l
   return true;
 }
 
+// raw_substitution into a caller-provided buffer (no allocation)
+__device__ inline void d_raw_sub_into(const ElimArgs &A, uint64_t s_off, uint32_t s_len, uint32_t from, uint64_t r_off,
+                                      uint32_t r_len, uint64_t o, uint32_t &o_len) {
+  const FieldP &F = A.F;
+  const uint32_t *sk = A.pk + s_off;
+  const Fe *sv = A.pv + s_off;
+  const uint32_t *rk = A.pk + r_off;
+  const Fe *rv = A.pv + r_off;
+  Fe val = fe_zero();
+  uint32_t fi = RS_NONE;
+  for (uint32_t i = 0; i < s_len; ++i)
+    if (sk[i] == from) { val = sv[i]; fi = i; break; }
+  uint32_t i = 0, j = 0, w = 0;
+  if (fi == RS_NONE) {
+    for (; i < s_len; ++i) { A.pk[o + i] = sk[i]; A.pv[o + i] = sv[i]; }
+    o_len = s_len;
+    return;
+  }
+  while (i < s_len || j < r_len) {
+    if (i == fi) { ++i; continue; }
+    if (j >= r_len || (i < s_len && sk[i] < rk[j])) { A.pk[o + w] = sk[i]; A.pv[o + w] = sv[i]; ++i; }
+    else if (i >= s_len || rk[j] < sk[i]) { A.pk[o + w] = rk[j]; A.pv[o + w] = fmul(F, val, rv[j]); ++j; }
+    else { A.pk[o + w] = sk[i]; A.pv[o + w] = fadd(F, sv[i], fmul(F, val, rv[j])); ++i; ++j; }
+    ++w;
+  }
+  o_len = w;
+}
+
 __device__ inline void d_heap_sort_u32(uint32_t *a, uint32_t n) {
   if (n < 2) return;
   for (uint32_t start = n / 2; start-- > 0;) {
@@ -427,18 +455,27 @@ __device__ inline bool d_normalize_compose(const ElimArgs &A, uint64_t b, uint32
     for (uint32_t t = 0; t < len; ++t)
       if (A.noov[kk[t]] >= 0) ++n_app;
     if (n_app) {
-      // keys of the original map, in ascending order; applying one never removes another
+      // one output bound for all applications, two ping-pong buffers (raw_substitution applied
+      // key by key in ascending order; applying one never removes another applicable key)
+      uint64_t bound = len;
+      for (uint32_t t = 0; t < len; ++t) {
+        int32_t ns = A.noov[kk[t]];
+        if (ns >= 0) bound += A.h_len[ns];
+      }
+      uint64_t buf0 = pool_alloc(A, bound), buf1 = pool_alloc(A, bound);
+      if (buf0 == RS_NONE || buf1 == RS_NONE) return false;
       uint64_t orig_off = off;
       uint32_t orig_len = len;
+      uint64_t dst = buf0;
       for (uint32_t t = 0; t < orig_len; ++t) {
         uint32_t key = A.pk[orig_off + t];
         int32_t ns = A.noov[key];
         if (ns < 0) continue;
-        uint64_t no;
         uint32_t nl;
-        if (!d_raw_sub(A, off, len, key, A.h_off[ns], A.h_len[ns], no, nl)) return false;
-        off = no;
+        d_raw_sub_into(A, off, len, key, A.h_off[ns], A.h_len[ns], dst, nl);
+        off = dst;
         len = nl;
+        dst = dst == buf0 ? buf1 : buf0;
       }
       A.h_off[slot] = off;
       A.h_len[slot] = len;
