@@ -1,0 +1,149 @@
+"""bench.py -- constraints simplified/sec (--O2) on the 10M-constraint synthetic circuit.
+
+One step = one full --O2 simplification (rs_engine_run): the Simplifier bundle already resident in
+HBM -> simplified constraints + label->wire map resident in HBM.  N ranks (one process per GPU,
+torch.distributed over RCCL) each own an independent shard of template instances (weak scaling;
+the shards share no signal, so no exchange step is needed -- see DESIGN.md "Multi-GPU").
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events around it on
+the library's own stream) and the CPU baseline (the canonical CPU oracle, oracle/refcpu.cpp, on a
+bounded sample of the same workload, rank 0 only)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "constraints simplified/sec (--O2) on 10M-constraint circuit; bit-exact .r1cs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(rows: int, seed: int, threads: int):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rsio
+    import circom_cvm_amd as M
+    inp = M.Input.synth(0, rows, seed)
+    t0 = time.time()
+    _, ms, _ = rsio.oracle_run(inp.c, rsio.flags("O2"), threads=threads)
+    wall = time.time() - t0
+    return {"value": round(inp.rows() / (ms / 1000.0), 1), "unit": "constraints/s", "cores": threads,
+            "kind": "port",
+            "sample": f"synth_mixed rows={inp.rows()} seed={seed} bn128 --O2, oracle/refcpu.cpp "
+                      f"simplification() only, {ms / 1000.0:.1f} s ({wall:.1f} s incl. load)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--prime", default="bn128")
+    ap.add_argument("--cpu-rows", type=int, default=3_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_
+        torch.cuda.set_device(local)
+        dist_.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = dist_
+
+    import circom_cvm_amd as M
+
+    # each rank: its own shard of instances (seed + rank), staged in HBM once
+    inp = M.Input.synth(0, args.rows, args.seed + rank, args.prime)
+    n_rows = inp.rows()
+    eng = M.Engine(local)
+    eng.load(inp.c)
+    fl = M.make_flags("O2", device=local)
+    for _ in range(args.warmup):
+        eng.run(fl)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    elim_ms = elim_bytes = apply_ms = apply_bytes = 0.0
+    elim_launches = apply_launches = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run(fl)  # synchronous: returns after its stream has drained
+        st = eng.stats()
+        elim_ms += st.elim_kernel_ms
+        elim_bytes += st.elim_bytes
+        elim_launches += st.elim_kernel_launches
+        apply_ms += st.apply_kernel_ms
+        apply_bytes += st.apply_bytes
+        apply_launches += st.apply_kernel_launches
+    barrier()
+    dt = time.perf_counter() - t0
+    total_rows = n_rows
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt, float(n_rows)], device="cuda", dtype=torch.float64)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        dt = float(mx[0])
+        total_rows = int(sm[1])
+    last = eng.stats()
+    if rank == 0:
+        ms_step = dt * 1000.0 / args.steps
+        value = total_rows * args.steps / dt
+        # dominant kernel: the one with the larger device time over the timed region
+        if elim_ms >= apply_ms:
+            k_name, k_ms, k_bytes, k_launch = "k_eliminate", elim_ms, elim_bytes, elim_launches
+        else:
+            k_name, k_ms, k_bytes, k_launch = "k_nl_fill", apply_ms, apply_bytes, apply_launches
+        per_launch_s = (k_ms / 1000.0) / max(k_launch, 1)
+        per_launch_bytes = k_bytes / max(k_launch, 1)
+        achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+        traffic = None
+        tf = os.environ.get("RS_PMC_TRAFFIC_BYTES")  # from profiles/ PMC pass, per launch
+        if tf:
+            traffic = float(tf)
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "constraints/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64x4 (F_p, 256-bit Montgomery)", "data": "synthetic",
+            "config": {"workload": f"synth_mixed rows={args.rows}/rank prime={args.prime} "
+                                   f"seed={args.seed}+rank --O2 (metric circuit, SURVEY 8(d))",
+                       "constraints_per_rank": n_rows, "parallelism": f"shards{world}"},
+            "roofline": {"bound": "hbm", "kernel": k_name, "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic, "launches_per_step": k_launch / args.steps,
+                         "avg_launch_ms": round(per_launch_s * 1000.0, 4),
+                         "alg_bytes_per_launch": int(per_launch_bytes)},
+            "phases_ms": {k: round(getattr(last, k), 2) for k in
+                          ("total_ms", "eq_ms", "cluster_ms", "elim_ms", "subst_ms", "final_ms")},
+        }
+        if not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed, args.cpu_threads)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

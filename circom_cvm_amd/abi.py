@@ -48,7 +48,9 @@ class RsStats(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("eq_ms", C.c_double), ("cluster_ms", C.c_double),
                 ("elim_ms", C.c_double), ("subst_ms", C.c_double), ("final_ms", C.c_double),
                 ("apply_kernel_ms", C.c_double), ("apply_kernel_launches", C.c_uint64),
-                ("apply_bytes", C.c_uint64), ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
+                ("apply_bytes", C.c_uint64), ("elim_kernel_ms", C.c_double),
+                ("elim_kernel_launches", C.c_uint64), ("elim_bytes", C.c_uint64),
+                ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
                 ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
 
     def as_dict(self):

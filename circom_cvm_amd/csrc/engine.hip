@@ -129,7 +129,7 @@ struct rs_engine {
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
   std::vector<int32_t> sig2cl;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
@@ -458,10 +458,14 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.pool_top = P.top;
     a.pool_cap = P.cap;
     a.err = d_err;
+    a.bytes = E->A.get<unsigned long long>("el.bytes", 1);
+    HC(hipMemsetAsync(a.bytes, 0, 8, E->st));
     if (eo.n_clusters) {
       uint64_t blocks = (eo.n_clusters + 63) / 64;
+      HC(hipEventRecord(E->ev2, E->st));
       hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a);
       HC(hipGetLastError());
+      HC(hipEventRecord(E->ev3, E->st));
     }
     int err = 0;
     HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
@@ -473,6 +477,15 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       continue;
     }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
+    if (eo.n_clusters) {
+      float ms = 0;
+      unsigned long long by = 0;
+      HC(hipEventElapsedTime(&ms, E->ev2, E->ev3));
+      HC(hipMemcpy(&by, a.bytes, 8, hipMemcpyDeviceToHost));
+      E->stats.elim_kernel_ms += ms;
+      E->stats.elim_kernel_launches++;
+      E->stats.elim_bytes += by;
+    }
     eo.n_sub.resize(eo.n_clusters);
     eo.n_left.resize(eo.n_clusters);
     if (eo.n_clusters) {
@@ -1339,6 +1352,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
     HC(hipEventCreate(&E->ev0));
     HC(hipEventCreate(&E->ev1));
+    HC(hipEventCreate(&E->ev2));
+    HC(hipEventCreate(&E->ev3));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {
@@ -1356,6 +1371,8 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->st) (void)hipStreamSynchronize(E->st);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
+  if (E->ev2) (void)hipEventDestroy(E->ev2);
+  if (E->ev3) (void)hipEventDestroy(E->ev3);
   if (E->heap_k) (void)hipFree(E->heap_k);
   if (E->heap_v) (void)hipFree(E->heap_v);
   if (E->st) (void)hipStreamDestroy(E->st);

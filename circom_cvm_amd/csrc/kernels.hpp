@@ -299,6 +299,7 @@ struct ElimArgs {
   unsigned long long *pool_top;
   uint64_t pool_cap;
   int *err;
+  unsigned long long *bytes;  // algorithmic bytes (SURVEY 8(d) B_alg terms of this kernel)
 };
 
 __device__ __forceinline__ uint64_t pool_alloc(const ElimArgs &A, uint64_t n) {
@@ -683,6 +684,12 @@ __global__ void k_eliminate(ElimArgs A) {
     A.n_sub[c] = m;
     A.n_left[c] = nl;
     if (!ok) atomicOr(A.err, 8);
+    // B_alg of the cluster: its rows read once (36 B per entry + 8 B row pointer), every
+    // substitution read and written by normalisation and written once more by composition
+    uint64_t rows_e = 0, subs_e = 0;
+    for (uint64_t idx = b; idx < e; ++idx) rows_e += A.rows.len[A.perm[idx]];
+    for (uint32_t i = 0; i < m; ++i) subs_e += A.h_len[b + i];
+    atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * n));
   }
 }
 

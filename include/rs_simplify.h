@@ -125,9 +125,12 @@ typedef struct rs_stats {
   double elim_ms;              /* per-cluster elimination + normalisation + composition      */
   double subst_ms;             /* substitution application (non-linear rows, rounds >= 2)    */
   double final_ms;             /* compaction, rebuild_witness, output assembly               */
-  double apply_kernel_ms;      /* device time of the dominant substitution kernel            */
+  double apply_kernel_ms;      /* device time of the non-linear substitution kernel (k_nl_fill) */
   uint64_t apply_kernel_launches;
-  uint64_t apply_bytes;        /* algorithmic bytes moved by that kernel (sum over launches) */
+  uint64_t apply_bytes;        /* its algorithmic bytes (sum over launches)                  */
+  double elim_kernel_ms;       /* device time of the per-cluster elimination (k_eliminate)   */
+  uint64_t elim_kernel_launches;
+  uint64_t elim_bytes;         /* its algorithmic bytes (sum over launches)                  */
   uint64_t rounds;             /* linear-elimination rounds executed                         */
   uint64_t n_clusters;
   uint64_t n_substitutions;
