@@ -421,6 +421,23 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   h2d(E, d_cl, eo.cl_off.data(), 8 * (eo.n_clusters + 1));
   uint64_t tot_nnz = 0;
   for (uint64_t i = 0; i < n_slots; ++i) tot_nnz += H.len[perm[i]];
+  // process_4 clusters go to the workgroup kernel; the rest, largest first, one lane each
+  std::vector<uint32_t> big, small;
+  for (uint64_t c = 0; c < eo.n_clusters; ++c) {
+    uint64_t n = eo.cl_off[c + 1] - eo.cl_off[c];
+    if (n >= 350 && n < 1000000 && !old_heur) big.push_back((uint32_t)c);
+    else small.push_back((uint32_t)c);
+  }
+  std::stable_sort(small.begin(), small.end(), [&](uint32_t x, uint32_t y) {
+    return eo.cl_off[x + 1] - eo.cl_off[x] > eo.cl_off[y + 1] - eo.cl_off[y];
+  });
+  std::stable_sort(big.begin(), big.end(), [&](uint32_t x, uint32_t y) {
+    return eo.cl_off[x + 1] - eo.cl_off[x] > eo.cl_off[y + 1] - eo.cl_off[y];
+  });
+  uint64_t n_big = big.size(), n_small = small.size();
+  uint32_t *d_big = E->A.get<uint32_t>("el.big", n_big), *d_small = E->A.get<uint32_t>("el.small", n_small);
+  h2d(E, d_big, big.data(), 4 * n_big);
+  h2d(E, d_small, small.data(), 4 * n_small);
   uint64_t want = std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots));
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
@@ -461,10 +478,18 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.bytes = E->A.get<unsigned long long>("el.bytes", 1);
     HC(hipMemsetAsync(a.bytes, 0, 8, E->st));
     if (eo.n_clusters) {
-      uint64_t blocks = (eo.n_clusters + 63) / 64;
       HC(hipEventRecord(E->ev2, E->st));
-      hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a);
-      HC(hipGetLastError());
+      if (n_big) {
+        hipLaunchKernelGGL(k_eliminate_big, dim3((unsigned)std::min<uint64_t>(n_big, 4096)), dim3(256), 0, E->st, a,
+                           (const uint32_t *)d_big, (uint64_t)n_big);
+        HC(hipGetLastError());
+      }
+      if (n_small) {
+        uint64_t blocks = (n_small + 63) / 64;
+        hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a,
+                           (const uint32_t *)d_small, (uint64_t)n_small);
+        HC(hipGetLastError());
+      }
       HC(hipEventRecord(E->ev3, E->st));
     }
     int err = 0;

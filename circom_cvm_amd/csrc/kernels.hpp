@@ -486,9 +486,10 @@ __device__ inline bool d_normalize_compose(const ElimArgs &A, uint64_t b, uint32
   return true;
 }
 
-__global__ void k_eliminate(ElimArgs A) {
+__global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
-  for (uint64_t c = gtid(); c < A.n_clusters; c += gstride()) {
+  for (uint64_t ci = gtid(); ci < n_ids; ci += gstride()) {
+    const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     const uint32_t n = (uint32_t)(e - b);
     const bool use4 = n >= 350 && n < 1000000 && !A.old_heur;
@@ -690,6 +691,271 @@ __global__ void k_eliminate(ElimArgs A) {
     for (uint64_t idx = b; idx < e; ++idx) rows_e += A.rows.len[A.perm[idx]];
     for (uint32_t i = 0; i < m; ++i) subs_e += A.h_len[b + i];
     atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * n));
+  }
+}
+
+
+// ---------------------------------------------------------------- large clusters (process_4)
+// One workgroup per cluster of 350 <= n < 1e6 rows (simplification_utils.rs:548-553, 156-185).
+// Exactness of the parallel phases:
+//  * SignalsInformation::new counts are order-free (atomics);
+//  * the uniques loop (:170-176) consumes every row by the SMALLEST unique signal it holds, rows
+//    are independent (a unique occurs in one row) and remove_constraint decrements commute;
+//  * the main loop (:178-183, treat_constraint_4) stays sequential (one lane);
+//  * normalisation is per substitution (exact inverses);
+//  * create_nonoverlapping_substitutions_4 (:465-479) only ever applies substitutions of NEWER
+//    deletions, all fully resolved, so resolving the dependency DAG level by level yields the
+//    same values and the same key sets as the newest-first sequential loop.
+__global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const FieldP &F = A.F;
+  __shared__ uint32_t s_m, s_touch, s_nl, s_left_todo, s_ok, s_progress;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b);
+    uint64_t tot = 0;
+    if (tid == 0) { s_m = 0; s_touch = 0; s_nl = 0; s_ok = 1; }
+    // scratch: touched signals (<= total entries)
+    for (uint32_t pos = tid; pos < n; pos += nt) tot += A.rows.len[A.perm[b + pos]];
+    __syncthreads();
+    __shared__ unsigned long long s_tot;
+    __shared__ uint64_t s_touch_off;
+    if (tid == 0) s_tot = 0;
+    __syncthreads();
+    atomicAdd(&s_tot, (unsigned long long)tot);
+    __syncthreads();
+    if (tid == 0) {
+      s_touch_off = pool_alloc(A, s_tot + 1);
+      if (s_touch_off == RS_NONE) s_ok = 0;
+    }
+    __syncthreads();
+    if (!s_ok) { if (tid == 0) { A.n_sub[c] = 0; A.n_left[c] = 0; atomicOr(A.err, 8); } continue; }
+    uint32_t *touch = A.pk + s_touch_off;
+    // ---- SignalsInformation::new: occ (init -1 = absent), first position
+    for (uint32_t pos = tid; pos < n; pos += nt) {
+      uint32_t r = A.perm[b + pos];
+      const uint32_t *k = A.rows.key + A.rows.off[r];
+      uint32_t len = A.rows.len[r];
+      A.dead[b + pos] = 0;
+      for (uint32_t i = 0; i < len; ++i) {
+        uint32_t s = k[i];
+        if (A.forb[s]) continue;
+        int32_t old = atomicAdd(&A.occ[s], 1);
+        atomicMin((uint32_t *)&A.rep_pos[s], pos);
+        if (old == -1) touch[atomicAdd(&s_touch, 1u)] = s;
+      }
+    }
+    __syncthreads();
+    const uint32_t n_touch = s_touch;
+    for (uint32_t t = tid; t < n_touch; t += nt) A.occ[touch[t]] += 1;  // -1 based -> count
+    __syncthreads();
+    // ---- uniques: each row is consumed by its smallest unique signal
+    for (uint32_t pos = tid; pos < n; pos += nt) {
+      uint32_t r = A.perm[b + pos];
+      const uint32_t *k = A.rows.key + A.rows.off[r];
+      uint32_t len = A.rows.len[r];
+      for (uint32_t i = 0; i < len; ++i)
+        if (!A.forb[k[i]] && A.occ[k[i]] == 1) { A.dead[b + pos] = 1; A.order[b + pos] = i; break; }
+    }
+    __syncthreads();
+    for (uint32_t pos = tid; pos < n; pos += nt) {
+      if (!A.dead[b + pos]) continue;
+      uint32_t r = A.perm[b + pos];
+      const uint32_t *k = A.rows.key + A.rows.off[r];
+      for (uint32_t i = 0; i < A.rows.len[r]; ++i)
+        if (!A.forb[k[i]]) atomicSub(&A.occ[k[i]], 1);  // remove_constraint
+    }
+    __syncthreads();
+    for (uint32_t pos = tid; pos < n; pos += nt) {
+      if (!A.dead[b + pos]) continue;
+      uint32_t r = A.perm[b + pos];
+      const uint32_t *k = A.rows.key + A.rows.off[r];
+      const Fe *v = A.rows.val + A.rows.off[r];
+      uint32_t len = A.rows.len[r];
+      uint32_t oi = A.order[b + pos];  // the row's smallest unique signal (chosen above)
+      Fe coef;
+      uint64_t to_off;
+      uint32_t to_len;
+      if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { s_ok = 0; continue; }
+      uint32_t slot = atomicAdd(&s_m, 1u);
+      uint32_t s = k[oi];
+      A.holder_idx[s] = (int32_t)(b + slot);
+      A.h_sig[b + slot] = s;
+      A.h_coef[b + slot] = coef;
+      A.h_off[b + slot] = to_off;
+      A.h_len[b + slot] = to_len;
+      A.del[s] = 1;
+    }
+    __syncthreads();
+    // remove_signal for the consumed uniques
+    for (uint32_t i = tid; i < s_m; i += nt) A.occ[A.h_sig[b + i]] = -1;
+    __syncthreads();
+    // ---- main loop (treat_constraint_4 + take_signal_4), one lane
+    if (tid == 0 && s_ok) {
+      uint32_t m = s_m, nl = 0;
+      bool ok = true;
+      for (uint64_t idx = e; idx-- > b && ok;) {
+        if (A.dead[idx]) continue;
+        uint32_t r = A.perm[idx];
+        const uint32_t *k = A.rows.key + A.rows.off[r];
+        const Fe *v = A.rows.val + A.rows.off[r];
+        uint32_t len = A.rows.len[r];
+        for (uint32_t i = 0; i < len; ++i)
+          if (!A.forb[k[i]] && A.occ[k[i]] >= 0) A.occ[k[i]]--;
+        for (;;) {
+          if (len == 0) break;
+          uint32_t oi = RS_NONE;
+          int32_t occ_ret = -1;
+          for (uint32_t i = 0; i < len; ++i) {
+            uint32_t s = k[i];
+            if (A.forb[s]) continue;
+            if (A.del[s]) { oi = i; break; }
+            int32_t c2 = A.occ[s];
+            if (c2 < 0) { atomicOr(A.err, 16); c2 = 0; }
+            if (occ_ret < 0 || c2 < occ_ret) { oi = i; occ_ret = c2; }
+            else if (c2 == occ_ret && k[oi] < s) oi = i;
+          }
+          if (oi == RS_NONE) {
+            uint64_t o = pool_alloc(A, len);
+            if (o == RS_NONE) { ok = false; break; }
+            for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
+            A.l_off[b + nl] = o;
+            A.l_len[b + nl] = len;
+            ++nl;
+            break;
+          }
+          uint32_t out = k[oi];
+          int32_t hi = A.holder_idx[out];
+          if (hi < 0) {
+            Fe coef;
+            uint64_t to_off;
+            uint32_t to_len;
+            if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+            A.holder_idx[out] = (int32_t)(b + m);
+            A.h_sig[b + m] = out;
+            A.h_coef[b + m] = coef;
+            A.h_off[b + m] = to_off;
+            A.h_len[b + m] = to_len;
+            ++m;
+            A.occ[out] = -1;
+            A.del[out] = 1;
+            break;
+          }
+          uint64_t w_off;
+          uint32_t w_len;
+          if (!d_merge(A, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
+            ok = false;
+            break;
+          }
+          k = A.pk + w_off;
+          v = A.pv + w_off;
+          len = w_len;
+        }
+      }
+      s_m = m;
+      s_nl = nl;
+      if (!ok) s_ok = 0;
+    }
+    __syncthreads();
+    const uint32_t m = s_m;
+    // ---- normalize_substitutions: per-thread chunks with Montgomery's batch inversion
+    if (s_ok) {
+      uint32_t per = (m + nt - 1) / nt;
+      uint32_t lo = tid * per, hi = min(m, lo + per);
+      if (lo < hi) {
+        Fe acc = A.h_coef[b + lo];
+        A.ftmp[b + lo] = acc;
+        for (uint32_t i = lo + 1; i < hi; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
+        Fe inv = finv(F, acc);
+        for (uint32_t i = hi; i-- > lo;) {
+          Fe inv_i = i > lo ? fmul(F, A.ftmp[b + i - 1], inv) : inv;
+          inv = fmul(F, inv, A.h_coef[b + i]);
+          Fe *vv = A.pv + A.h_off[b + i];
+          for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- composition, level by level over the dependency DAG
+    for (uint32_t i = tid; i < m; i += nt) A.tmp[b + i] = 0;  // resolved flags
+    __syncthreads();
+    for (uint32_t iter = 0; s_ok && iter <= m; ++iter) {
+      if (tid == 0) { s_progress = 0; s_left_todo = 0; }
+      __syncthreads();
+      // readiness (read-only pass): 1 = ready, 2 = already resolved
+      for (uint32_t i = tid; i < m; i += nt) {
+        if (A.tmp[b + i] == 1) continue;  // resolved
+        const uint32_t *kk = A.pk + A.h_off[b + i];
+        uint32_t len = A.h_len[b + i];
+        bool ready = true;
+        for (uint32_t t = 0; t < len && ready; ++t) {
+          int32_t hs = A.holder_idx[kk[t]];
+          if (hs >= 0 && A.tmp[hs] != 1) ready = false;
+        }
+        A.order[b + i] = ready ? 1u : 0u;
+        atomicAdd(&s_left_todo, 1u);
+      }
+      __syncthreads();
+      if (s_left_todo == 0) break;
+      for (uint32_t i = tid; i < m; i += nt) {
+        if (A.tmp[b + i] == 1 || A.order[b + i] != 1) continue;
+        uint64_t off = A.h_off[b + i];
+        uint32_t len = A.h_len[b + i];
+        const uint32_t *kk = A.pk + off;
+        uint64_t bound = len;
+        uint32_t n_app = 0;
+        for (uint32_t t = 0; t < len; ++t) {
+          int32_t hs = A.holder_idx[kk[t]];
+          if (hs >= 0) { bound += A.h_len[hs]; ++n_app; }
+        }
+        if (n_app) {
+          uint64_t buf0 = pool_alloc(A, bound), buf1 = pool_alloc(A, bound);
+          if (buf0 == RS_NONE || buf1 == RS_NONE) { s_ok = 0; continue; }
+          uint64_t orig_off = off;
+          uint32_t orig_len = len;
+          uint64_t dst = buf0;
+          for (uint32_t t = 0; t < orig_len; ++t) {
+            int32_t hs = A.holder_idx[A.pk[orig_off + t]];
+            if (hs < 0) continue;
+            uint32_t nl2;
+            d_raw_sub_into(A, off, len, A.pk[orig_off + t], A.h_off[hs], A.h_len[hs], dst, nl2);
+            off = dst;
+            len = nl2;
+            dst = dst == buf0 ? buf1 : buf0;
+          }
+          A.h_off[b + i] = off;
+          A.h_len[b + i] = len;
+        }
+        A.order[b + i] = 2;  // resolved at the end of this level
+        s_progress = 1;
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < m; i += nt)
+        if (A.order[b + i] == 2) A.tmp[b + i] = 1;
+      __syncthreads();
+      if (!s_progress) { if (tid == 0) { s_ok = 0; atomicOr(A.err, 32); } break; }
+    }
+    __syncthreads();
+    // ---- emit, reset the dense scratch
+    for (uint32_t i = tid; i < m; i += nt) {
+      uint32_t s = A.h_sig[b + i];
+      A.holder_idx[s] = -1;
+      A.del[s] = 0;
+      A.sub_of[s] = (int32_t)(b + i);
+      A.deleted[s] = 1;
+    }
+    for (uint32_t t = tid; t < n_touch; t += nt) { A.occ[touch[t]] = -1; A.rep_pos[touch[t]] = -1; }
+    uint64_t rows_e = 0, subs_e = 0;
+    for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
+    for (uint32_t i = tid; i < m; i += nt) subs_e += A.h_len[b + i];
+    atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0)));
+    if (tid == 0) {
+      A.n_sub[c] = m;
+      A.n_left[c] = s_nl;
+      if (!s_ok) atomicOr(A.err, 8);
+    }
+    __syncthreads();
   }
 }
 
