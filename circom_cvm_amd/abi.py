@@ -50,6 +50,8 @@ class RsStats(C.Structure):
                 ("apply_kernel_ms", C.c_double), ("apply_kernel_launches", C.c_uint64),
                 ("apply_bytes", C.c_uint64), ("elim_kernel_ms", C.c_double),
                 ("elim_kernel_launches", C.c_uint64), ("elim_bytes", C.c_uint64),
+                ("elim_big_ms", C.c_double), ("elim_small_ms", C.c_double), ("nl_ms", C.c_double),
+                ("map_ms", C.c_double), ("rounds_ms", C.c_double),
                 ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
                 ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
 

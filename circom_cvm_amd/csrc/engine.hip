@@ -129,7 +129,7 @@ struct rs_engine {
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
   std::vector<int32_t> sig2cl;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
@@ -237,6 +237,9 @@ __global__ void k_commit_round(const uint8_t *touched, const int32_t *turn, uint
     c.off[r] = oc.off[r]; c.len[r] = oc.len[r];
   }
 }
+__global__ void k_unmark_list(const uint32_t *sig, uint64_t n, uint8_t *bits) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) bits[sig[i]] = 0;
+}
 __global__ void k_zero_c(const uint32_t *ids, uint64_t n, uint32_t *clen) {
   for (uint64_t i = gtid(); i < n; i += gstride()) clen[ids[i]] = 0;
 }
@@ -247,6 +250,36 @@ __global__ void k_nonempty_flags(const uint32_t *la, const uint32_t *lb, const u
 __global__ void k_compact_keys(DRows V, const uint64_t *doff, uint32_t *out) {
   for (uint64_t r = gtid(); r < V.n; r += gstride())
     for (uint32_t i = 0; i < V.len[r]; ++i) out[doff[r] + i] = V.key[V.off[r] + i];
+}
+
+// (signal, row) pairs of the round-1 storage rows for the flagged signals: the initial lists of
+// build_non_linear_signal_map (:327-343) restricted to the signals a later round asks for.
+__device__ inline bool d_has_key(const uint32_t *k, uint32_t n, uint32_t s) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (k[mid] < s) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && k[lo] == s;
+}
+__global__ void k_emit_pairs(DRows a, DRows b, DRows c, const uint8_t *flag, uint64_t *pairs, unsigned long long *cnt,
+                             uint64_t cap) {
+  for (uint64_t r = gtid(); r < a.n; r += gstride()) {
+    const uint32_t *ka = a.key + a.off[r], *kb = b.key + b.off[r], *kc = c.key + c.off[r];
+    uint32_t na = a.len[r], nb = b.len[r], nc = c.len[r];
+    for (int part = 0; part < 3; ++part) {
+      const uint32_t *k = part == 0 ? ka : part == 1 ? kb : kc;
+      uint32_t n = part == 0 ? na : part == 1 ? nb : nc;
+      for (uint32_t i = 0; i < n; ++i) {
+        uint32_t s = k[i];
+        if (!flag[s]) continue;
+        if (part >= 1 && d_has_key(ka, na, s)) continue;
+        if (part == 2 && d_has_key(kb, nb, s)) continue;
+        unsigned long long o = atomicAdd(cnt, 1ull);
+        if (o < cap) pairs[o] = ((uint64_t)s << 32) | (uint32_t)r;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- host clustering
@@ -476,14 +509,22 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.pool_cap = P.cap;
     a.err = d_err;
     a.bytes = E->A.get<unsigned long long>("el.bytes", 1);
+    a.big_touch_off = E->A.get<uint64_t>("el.bt_off", std::max<uint64_t>(n_big, 1));
+    a.big_touch_n = E->A.get<uint32_t>("el.bt_n", std::max<uint64_t>(n_big, 1));
+    a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", 16 * n_big) : nullptr;
     HC(hipMemsetAsync(a.bytes, 0, 8, E->st));
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_big) {
-        hipLaunchKernelGGL(k_eliminate_big, dim3((unsigned)std::min<uint64_t>(n_big, 4096)), dim3(256), 0, E->st, a,
-                           (const uint32_t *)d_big, (uint64_t)n_big);
+        const unsigned gb = (unsigned)std::min<uint64_t>(n_big, 8192);
+        hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        HC(hipGetLastError());
+        hipLaunchKernelGGL(k_big_main, dim3(gb), dim3(64), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        HC(hipGetLastError());
+        hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
       }
+      HC(hipEventRecord(E->ev4, E->st));
       if (n_small) {
         uint64_t blocks = (n_small + 63) / 64;
         hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a,
@@ -506,10 +547,40 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       float ms = 0;
       unsigned long long by = 0;
       HC(hipEventElapsedTime(&ms, E->ev2, E->ev3));
+      float mb = 0;
+      HC(hipEventElapsedTime(&mb, E->ev2, E->ev4));
+      E->stats.elim_big_ms += mb;
+      E->stats.elim_small_ms += ms - mb;
       HC(hipMemcpy(&by, a.bytes, 8, hipMemcpyDeviceToHost));
       E->stats.elim_kernel_ms += ms;
       E->stats.elim_kernel_launches++;
       E->stats.elim_bytes += by;
+    }
+    if (a.prof) {
+      std::vector<unsigned long long> pf(16 * n_big);
+      HC(hipMemcpy(pf.data(), a.prof, 8 * pf.size(), hipMemcpyDeviceToHost));
+      std::vector<uint64_t> ix(n_big);
+      for (uint64_t i = 0; i < n_big; ++i) ix[i] = i;
+      std::sort(ix.begin(), ix.end(), [&](uint64_t x, uint64_t y) {
+        return pf[16 * x + 4] + pf[16 * x + 5] + pf[16 * x + 6] + pf[16 * x + 7] > pf[16 * y + 4] + pf[16 * y + 5] + pf[16 * y + 6] + pf[16 * y + 7];
+      });
+      double sum[4] = {0, 0, 0, 0};
+      unsigned long long rows_all = 0, rows_main = 0, subs_all = 0, it_max = 0;
+      for (uint64_t q = 0; q < n_big; ++q) {
+        for (int j = 0; j < 4; ++j) sum[j] += pf[16 * q + 4 + j] / 100.0;
+        rows_all += pf[16 * q]; subs_all += pf[16 * q + 1]; rows_main += pf[16 * q + 2];
+        it_max = std::max(it_max, pf[16 * q + 3]);
+      }
+      fprintf(stderr, "[rs-debug] big clusters: %llu rows %llu subs %llu sequential rows %llu max iters %llu; "
+              "summed us: %.0f / %.0f / %.0f / %.0f\n", (unsigned long long)n_big, rows_all, subs_all, rows_main, it_max,
+              sum[0], sum[1], sum[2], sum[3]);
+      fprintf(stderr, "[rs-debug] big clusters: %llu (times in us: count+uniques / main / normalize / compose)\n", (unsigned long long)n_big);
+      for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 8); ++q) {
+        unsigned long long *p = &pf[16 * ix[q]];
+        fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu iters=%llu  %.1f / %.1f / %.1f / %.1f  merges=%llu mwork=%llu "
+                "rhs_sum=%llu rhs_max=%llu touched=%llu\n", p[0], p[1], p[2], p[3],
+                p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0, p[8], p[9], p[10], p[11], p[12]);
+      }
     }
     eo.n_sub.resize(eo.n_clusters);
     eo.n_left.resize(eo.n_clusters);
@@ -1006,6 +1077,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   if (n_wl) launch(st, k_view_rows, n_wl, (const uint64_t *)sc.off, (const uint32_t *)sc.len, (const uint32_t *)wl_ids, n_wl, lv.off, lv.len);
   HC(hipStreamSynchronize(st));
   E->stats.subst_ms += now_ms() - Ts;
+  E->stats.nl_ms += now_ms() - Ts;
 
   // ======================= rounds >= 2 (:613-646)
   bool apply_round = apply_linear && no_rounds > 0 && n_wl > 0;
@@ -1026,38 +1098,58 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
   }
   if (apply_round) {
-    // host copy of the non-linear signal map: initial lists (ascending ids) + appended entries
+    // the non-linear signal map, kept on the host only for the signals a round substitutes:
+    // initial lists (round-1 storage rows, ascending ids; built on the GPU on demand) + appends
     double Tm = now_ms();
-    HostRows hA, hB, hC;
-    fetch_keys(E, ta_, hA);
-    fetch_keys(E, tb_, hB);
-    fetch_keys(E, tc_, hC);
-    std::vector<uint64_t> mptr(S + 1, 0);
-    std::vector<uint32_t> sig;
-    auto row_sigs = [&](uint64_t r, std::vector<uint32_t> &out) {
-      out.clear();
-      for (const HostRows *H : {&hA, &hB, &hC})
-        for (uint32_t i = 0; i < H->len[r]; ++i)
-          if (H->key[H->off[r] + i]) out.push_back(H->key[H->off[r] + i]);
-      std::sort(out.begin(), out.end());
-      out.erase(std::unique(out.begin(), out.end()), out.end());
-    };
-    for (uint64_t r = 0; r < n_st; ++r) {
-      row_sigs(r, sig);
-      for (uint32_t s : sig) mptr[s + 1]++;
+    DRows ia0 = ta_, ib0 = tb_, ic0 = tc_;  // snapshot of the round-1 storage rows
+    ia0.off = A.get<uint64_t>("m0.a.off", n_st); ia0.len = A.get<uint32_t>("m0.a.len", n_st);
+    ib0.off = A.get<uint64_t>("m0.b.off", n_st); ib0.len = A.get<uint32_t>("m0.b.len", n_st);
+    ic0.off = A.get<uint64_t>("m0.c.off", n_st); ic0.len = A.get<uint32_t>("m0.c.len", n_st);
+    if (n_st) {
+      HC(hipMemcpyAsync(ia0.off, ta_.off, 8 * n_st, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(ia0.len, ta_.len, 4 * n_st, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(ib0.off, tb_.off, 8 * n_st, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(ib0.len, tb_.len, 4 * n_st, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(ic0.off, tc_.off, 8 * n_st, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(ic0.len, tc_.len, 4 * n_st, hipMemcpyDeviceToDevice, st));
     }
-    for (uint64_t s = 0; s < S; ++s) mptr[s + 1] += mptr[s];
-    std::vector<uint32_t> mlist(mptr[S]);
-    {
-      std::vector<uint64_t> fillp(mptr.begin(), mptr.end() - 1);
-      for (uint64_t r = 0; r < n_st; ++r) {
-        row_sigs(r, sig);
-        for (uint32_t s : sig) mlist[fillp[s]++] = (uint32_t)r;
-      }
-    }
+    std::unordered_map<uint32_t, std::vector<uint32_t>> minit;  // queried signals only
     std::unordered_map<uint32_t, std::vector<uint32_t>> mext;
+    uint8_t *qflag = A.get<uint8_t>("m.qflag", S);
+    HC(hipMemsetAsync(qflag, 0, S, st));
+    auto query_initial = [&](const std::vector<uint32_t> &sigs) {
+      std::vector<uint32_t> q;
+      for (uint32_t s : sigs)
+        if (!minit.count(s)) { minit[s]; q.push_back(s); }
+      if (q.empty() || n_st == 0) return;
+      uint32_t *d_q = A.get<uint32_t>("m.q", q.size());
+      h2d(E, d_q, q.data(), 4 * q.size());
+      launch(st, k_mark_list, q.size(), (const uint32_t *)d_q, (uint64_t)q.size(), qflag);
+      unsigned long long *d_cnt = A.get<unsigned long long>("m.cnt", 1);
+      uint64_t cap = std::max<uint64_t>(4 * q.size(), 1 << 16);
+      for (;;) {
+        uint64_t *d_pairs = A.get<uint64_t>("m.pairs", cap);
+        HC(hipMemsetAsync(d_cnt, 0, 8, st));
+        for (DRows *R : {&ia0, &ib0, &ic0}) { R->key = heap_k; R->val = heap_v; }
+        launch(st, k_emit_pairs, n_st, ia0, ib0, ic0, (const uint8_t *)qflag, d_pairs, d_cnt, cap);
+        unsigned long long cnt = 0;
+        HC(hipMemcpyAsync(&cnt, d_cnt, 8, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        if (cnt > cap) { cap = cnt; continue; }
+        std::vector<uint64_t> pairs(cnt);
+        if (cnt) {
+          HC(hipMemcpyAsync(pairs.data(), d_pairs, 8 * cnt, hipMemcpyDeviceToHost, st));
+          HC(hipStreamSynchronize(st));
+        }
+        std::sort(pairs.begin(), pairs.end());
+        for (uint64_t x : pairs) minit[(uint32_t)(x >> 32)].push_back((uint32_t)x);
+        break;
+      }
+      launch(st, k_unmark_list, q.size(), (const uint32_t *)d_q, (uint64_t)q.size(), qflag);
+    };
     std::vector<uint8_t> extra_mark;
     E->stats.subst_ms += now_ms() - Tm;
+    E->stats.map_ms += now_ms() - Tm;
     int32_t *rank_of = A.get<int32_t>("rank_of", S);
     HC(hipMemsetAsync(rank_of, 0xff, 4 * S, st));
     int32_t *r_sub_of = A.get<int32_t>("r.sub_of", S);
@@ -1099,6 +1191,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       std::vector<uint32_t> usig(nU);
       std::vector<int32_t> urank(nU);
       for (uint64_t i = 0; i < nU; ++i) { usig[i] = hsig[U[i]]; urank[i] = (int32_t)i; }
+      {
+        double Tq = now_ms();
+        query_initial(usig);
+        E->stats.map_ms += now_ms() - Tq;
+      }
       uint32_t *d_us = A.get<uint32_t>("r.us", nU);
       int32_t *d_ur = A.get<int32_t>("r.ur", nU);
       if (nU) {
@@ -1160,13 +1257,14 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           int32_t q = hturn[r];
           uint32_t from = usig[q];
           uint64_t pos = UINT64_MAX;
-          for (uint64_t t = mptr[from]; t < mptr[from + 1]; ++t)
-            if (mlist[t] == r) { pos = t - mptr[from]; break; }
+          const std::vector<uint32_t> &L0 = minit[from];
+          auto lb = std::lower_bound(L0.begin(), L0.end(), r);  // initial lists are ascending
+          if (lb != L0.end() && *lb == r) pos = lb - L0.begin();
           if (pos == UINT64_MAX) {
             auto it = mext.find(from);
             if (it != mext.end())
               for (uint64_t t = 0; t < it->second.size(); ++t)
-                if (it->second[t] == r) { pos = (mptr[from + 1] - mptr[from]) + t; break; }
+                if (it->second[t] == r) { pos = L0.size() + t; break; }
           }
           if (pos == UINT64_MAX) throw RsError(RS_E_INTERNAL, "substituted row missing from the signal map");
           turned.push_back({((uint64_t)q << 32) | (pos & 0xffffffffu), r});
@@ -1186,11 +1284,12 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       // map appends (:369-377): every key of sub.to gets every visited row
       for (uint64_t i = 0; i < nU; ++i) {
         uint32_t from = usig[i];
-        uint64_t n0 = mptr[from + 1] - mptr[from];
+        const std::vector<uint32_t> &L0 = minit[from];
+        uint64_t n0 = L0.size();
         auto it = mext.find(from);
         uint64_t n1 = it == mext.end() ? 0 : it->second.size();
         if (n0 + n1 == 0) continue;
-        std::vector<uint32_t> visit(mlist.begin() + mptr[from], mlist.begin() + mptr[from + 1]);
+        std::vector<uint32_t> visit(L0.begin(), L0.end());
         if (n1) visit.insert(visit.end(), it->second.begin(), it->second.end());
         for (uint64_t t = uptr[i]; t < uptr[i + 1]; ++t) {
           uint32_t k = ukeys[t];
@@ -1251,6 +1350,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         }
       }
       E->stats.subst_ms += now_ms() - Tr;
+      E->stats.rounds_ms += now_ms() - Tr;
       if (no_rounds > 0) no_rounds--;
       apply_round = nn > 0 && no_rounds > 0;
     }
@@ -1379,6 +1479,7 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipEventCreate(&E->ev1));
     HC(hipEventCreate(&E->ev2));
     HC(hipEventCreate(&E->ev3));
+    HC(hipEventCreate(&E->ev4));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {
@@ -1398,6 +1499,7 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->ev1) (void)hipEventDestroy(E->ev1);
   if (E->ev2) (void)hipEventDestroy(E->ev2);
   if (E->ev3) (void)hipEventDestroy(E->ev3);
+  if (E->ev4) (void)hipEventDestroy(E->ev4);
   if (E->heap_k) (void)hipFree(E->heap_k);
   if (E->heap_v) (void)hipFree(E->heap_v);
   if (E->st) (void)hipStreamDestroy(E->st);

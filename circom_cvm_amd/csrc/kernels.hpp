@@ -300,21 +300,39 @@ struct ElimArgs {
   uint64_t pool_cap;
   int *err;
   unsigned long long *bytes;  // algorithmic bytes (SURVEY 8(d) B_alg terms of this kernel)
+  unsigned long long *prof;   // debug: 16 words per big cluster (see run_linear_simplification), or null
+  uint64_t *big_touch_off;    // per big cluster: touched-signal list in the pool (k_big_prep)
+  uint32_t *big_touch_n;
 };
 
-__device__ __forceinline__ uint64_t pool_alloc(const ElimArgs &A, uint64_t n) {
+__device__ __forceinline__ uint64_t pool_alloc_global(const ElimArgs &A, uint64_t n) {
   unsigned long long o = atomicAdd(A.pool_top, (unsigned long long)n);
   if (o + n > A.pool_cap) { atomicOr(A.err, 8); return RS_NONE; }
   return (uint64_t)o;
 }
+// Per-thread bump allocator over chunks of the pool: one global atomic per chunk instead of one per
+// allocation (the global counter is shared by every lane of every cluster).
+struct Alloc {
+  uint64_t cur = 0, end = 0;
+  uint32_t chunk = 512;
+};
+__device__ __forceinline__ uint64_t pool_alloc(const ElimArgs &A, Alloc &al, uint64_t n) {
+  if (al.cur + n <= al.end) { uint64_t o = al.cur; al.cur += n; return o; }
+  if (n >= al.chunk / 4) return pool_alloc_global(A, n);
+  uint64_t c = pool_alloc_global(A, al.chunk);
+  if (c == RS_NONE) return RS_NONE;
+  al.cur = c + n;
+  al.end = c + al.chunk;
+  return c;
+}
 
 // clear_signal_not_normalized (algebra.rs:1126-1136): to = row minus key, {0: 0} ensured.
-__device__ inline bool d_clear_nn(const ElimArgs &A, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
+__device__ inline bool d_clear_nn(const ElimArgs &A, Alloc &al, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
                                   Fe &coef, uint64_t &to_off, uint32_t &to_len) {
   coef = fneg(A.F, v[oi]);
   bool has0 = n > 0 && k[0] == 0 && oi != 0;
   uint32_t m = n - 1 + (has0 ? 0 : 1);
-  uint64_t o = pool_alloc(A, m);
+  uint64_t o = pool_alloc(A, al, m);
   if (o == RS_NONE) return false;
   uint32_t w = 0;
   if (!has0) { A.pk[o] = 0; A.pv[o] = fe_zero(); w = 1; }
@@ -325,11 +343,11 @@ __device__ inline bool d_clear_nn(const ElimArgs &A, const uint32_t *k, const Fe
   return true;
 }
 // treat_constraint_3/4 conflict: work = coef*R - c2*L, zeros dropped; L = row minus key (+{0:0}).
-__device__ inline bool d_merge(const ElimArgs &A, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
+__device__ inline bool d_merge(const ElimArgs &A, Alloc &al, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
                                const Fe &coef, const Fe &c2, uint64_t r_off, uint32_t r_len,
                                uint64_t &w_off, uint32_t &w_len) {
   const FieldP &F = A.F;
-  uint64_t o = pool_alloc(A, (uint64_t)n + r_len + 1);
+  uint64_t o = pool_alloc(A, al, (uint64_t)n + r_len + 1);
   if (o == RS_NONE) return false;
   const uint32_t *rk = A.pk + r_off;
   const Fe *rv = A.pv + r_off;
@@ -349,7 +367,7 @@ __device__ inline bool d_merge(const ElimArgs &A, const uint32_t *k, const Fe *v
 }
 // Substitution::apply_substitution with a single change (raw_substitution, algebra.rs:1279-1294):
 // out = src[from := val*rhs]; every rhs key is inserted, zeros kept; both maps hold key 0.
-__device__ inline bool d_raw_sub(const ElimArgs &A, uint64_t s_off, uint32_t s_len, uint32_t from, uint64_t r_off,
+__device__ inline bool d_raw_sub(const ElimArgs &A, Alloc &al, uint64_t s_off, uint32_t s_len, uint32_t from, uint64_t r_off,
                                  uint32_t r_len, uint64_t &o_off, uint32_t &o_len) {
   const FieldP &F = A.F;
   const uint32_t *sk = A.pk + s_off;
@@ -361,7 +379,7 @@ __device__ inline bool d_raw_sub(const ElimArgs &A, uint64_t s_off, uint32_t s_l
   for (uint32_t i = 0; i < s_len; ++i)
     if (sk[i] == from) { val = sv[i]; fi = i; break; }
   if (fi == RS_NONE) { o_off = s_off; o_len = s_len; return true; }
-  uint64_t o = pool_alloc(A, (uint64_t)s_len + r_len);
+  uint64_t o = pool_alloc(A, al, (uint64_t)s_len + r_len);
   if (o == RS_NONE) return false;
   uint32_t i = 0, j = 0, w = 0;
   while (i < s_len || j < r_len) {
@@ -431,7 +449,7 @@ __device__ inline void d_heap_sort_u32(uint32_t *a, uint32_t n) {
 
 // normalize_substitutions (:414-437) + create_nonoverlapping_substitutions(_4) (:451-479).
 // Slots [b, b+m) hold the holder; `seq` lists the signals in composition order.
-__device__ inline bool d_normalize_compose(const ElimArgs &A, uint64_t b, uint32_t m, const uint32_t *seq) {
+__device__ inline bool d_normalize_compose(const ElimArgs &A, Alloc &al, uint64_t b, uint32_t m, const uint32_t *seq) {
   const FieldP &F = A.F;
   if (m == 0) return true;
   // batch inversion (Montgomery's trick; exact inverses, so order-free)
@@ -463,7 +481,7 @@ __device__ inline bool d_normalize_compose(const ElimArgs &A, uint64_t b, uint32
         int32_t ns = A.noov[kk[t]];
         if (ns >= 0) bound += A.h_len[ns];
       }
-      uint64_t buf0 = pool_alloc(A, bound), buf1 = pool_alloc(A, bound);
+      uint64_t buf0 = pool_alloc(A, al, bound), buf1 = pool_alloc(A, al, bound);
       if (buf0 == RS_NONE || buf1 == RS_NONE) return false;
       uint64_t orig_off = off;
       uint32_t orig_len = len;
@@ -488,6 +506,7 @@ __device__ inline bool d_normalize_compose(const ElimArgs &A, uint64_t b, uint32
 
 __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
+  Alloc al;
   for (uint64_t ci = gtid(); ci < n_ids; ci += gstride()) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
@@ -508,7 +527,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
           for (uint32_t i = len; i-- > 0;)
             if (!A.forb[k[i]]) { oi = i; break; }
           if (oi == RS_NONE) {  // no takeable signal: leftover
-            uint64_t o = pool_alloc(A, len);
+            uint64_t o = pool_alloc(A, al, len);
             if (o == RS_NONE) { ok = false; break; }
             for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
             A.l_off[b + nl] = o;
@@ -522,7 +541,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
             Fe coef;
             uint64_t to_off;
             uint32_t to_len;
-            if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+            if (!d_clear_nn(A, al, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
             A.holder_idx[out] = (int32_t)(b + m);
             A.h_sig[b + m] = out;
             A.h_coef[b + m] = coef;
@@ -533,7 +552,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
           }
           uint64_t w_off;
           uint32_t w_len;
-          if (!d_merge(A, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
+          if (!d_merge(A, al, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
             ok = false;
             break;
           }
@@ -545,7 +564,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
       // BTreeMap order: ascending signal
       for (uint32_t i = 0; i < m; ++i) A.tmp[b + i] = A.h_sig[b + i];
       d_heap_sort_u32(A.tmp + b, m);
-      if (ok) ok = d_normalize_compose(A, b, m, A.tmp + b);
+      if (ok) ok = d_normalize_compose(A, al, b, m, A.tmp + b);
     } else {
       // ---- substitution_process_4 (:156-185), SignalsInformation (:60-113)
       uint32_t n_touch = 0;
@@ -553,7 +572,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
       {
         uint64_t tot = 0;
         for (uint64_t idx = b; idx < e; ++idx) tot += A.rows.len[A.perm[idx]];
-        touch_off = pool_alloc(A, tot + 1);
+        touch_off = pool_alloc(A, al, tot + 1);
         if (touch_off == RS_NONE) ok = false;
       }
       uint32_t *touch = A.pk + touch_off;
@@ -571,7 +590,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
       }
       // uniques in ascending signal order (scratch after the touched list; can exceed n)
       uint32_t n_u = 0;
-      uint64_t uniq_off = ok ? pool_alloc(A, (uint64_t)n_touch + 1) : RS_NONE;
+      uint64_t uniq_off = ok ? pool_alloc(A, al, (uint64_t)n_touch + 1) : RS_NONE;
       if (uniq_off == RS_NONE) ok = false;
       uint32_t *uniq = A.pk + (ok ? uniq_off : 0);
       if (ok) {
@@ -598,7 +617,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
         Fe coef;
         uint64_t to_off;
         uint32_t to_len;
-        if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+        if (!d_clear_nn(A, al, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
         A.holder_idx[s] = (int32_t)(b + m);
         A.h_sig[b + m] = s;
         A.h_coef[b + m] = coef;
@@ -631,7 +650,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
             else if (c2 == occ_ret && k[oi] < s) oi = i;
           }
           if (oi == RS_NONE) {
-            uint64_t o = pool_alloc(A, len);
+            uint64_t o = pool_alloc(A, al, len);
             if (o == RS_NONE) { ok = false; break; }
             for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
             A.l_off[b + nl] = o;
@@ -645,7 +664,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
             Fe coef;
             uint64_t to_off;
             uint32_t to_len;
-            if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
+            if (!d_clear_nn(A, al, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
             A.holder_idx[out] = (int32_t)(b + m);
             A.h_sig[b + m] = out;
             A.h_coef[b + m] = coef;
@@ -659,7 +678,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
           }
           uint64_t w_off;
           uint32_t w_len;
-          if (!d_merge(A, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
+          if (!d_merge(A, al, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
             ok = false;
             break;
           }
@@ -673,7 +692,7 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
       // composition order: deletion order, newest first
       uint32_t *seq = A.tmp + b;
       for (uint32_t t = 0; t < nd; ++t) seq[t] = A.order[b + nd - 1 - t];
-      if (ok) ok = d_normalize_compose(A, b, m, seq);
+      if (ok) ok = d_normalize_compose(A, al, b, m, seq);
     }
     for (uint32_t i = 0; i < m; ++i) {
       uint32_t s = A.h_sig[b + i];
@@ -695,44 +714,46 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
 }
 
 
-// ---------------------------------------------------------------- large clusters (process_4)
-// One workgroup per cluster of 350 <= n < 1e6 rows (simplification_utils.rs:548-553, 156-185).
-// Exactness of the parallel phases:
-//  * SignalsInformation::new counts are order-free (atomics);
-//  * the uniques loop (:170-176) consumes every row by the SMALLEST unique signal it holds, rows
-//    are independent (a unique occurs in one row) and remove_constraint decrements commute;
-//  * the main loop (:178-183, treat_constraint_4) stays sequential (one lane);
-//  * normalisation is per substitution (exact inverses);
-//  * create_nonoverlapping_substitutions_4 (:465-479) only ever applies substitutions of NEWER
-//    deletions, all fully resolved, so resolving the dependency DAG level by level yields the
-//    same values and the same key sets as the newest-first sequential loop.
-__global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
-  const FieldP &F = A.F;
-  __shared__ uint32_t s_m, s_touch, s_nl, s_left_todo, s_ok, s_progress;
+
+// ================================================================ large clusters (process_4)
+// Three launches per round, one workgroup per cluster (largest first):
+//   k_big_prep   (256 lanes) SignalsInformation::new + the uniques pass           (:296-316)
+//   k_big_main   ( 64 lanes) the ordered main loop (treat_constraint_4 + take_signal_4, :317-366):
+//                the row walk is inherently sequential, so one wave runs it cooperatively -- the work
+//                list lives in LDS, the pivot is a wave reduction, and each conflict is a merge-path
+//                merge whose 256-bit products are spread over the lanes.
+//   k_big_finish (256 lanes) normalize_substitutions + create_nonoverlapping_substitutions_4
+//                (:414-479) as a dependency worklist (Kahn order), emit and scratch reset.
+__global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  __shared__ uint32_t s_m, s_touch, s_ok;
+  __shared__ unsigned long long s_tot;
+  __shared__ uint64_t s_touch_off;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  Alloc al;
+  al.chunk = 128;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     const uint32_t n = (uint32_t)(e - b);
+    unsigned long long t_0 = wall_clock64();
     uint64_t tot = 0;
-    if (tid == 0) { s_m = 0; s_touch = 0; s_nl = 0; s_ok = 1; }
-    // scratch: touched signals (<= total entries)
+    if (tid == 0) { s_m = 0; s_touch = 0; s_ok = 1; s_tot = 0; }
     for (uint32_t pos = tid; pos < n; pos += nt) tot += A.rows.len[A.perm[b + pos]];
-    __syncthreads();
-    __shared__ unsigned long long s_tot;
-    __shared__ uint64_t s_touch_off;
-    if (tid == 0) s_tot = 0;
     __syncthreads();
     atomicAdd(&s_tot, (unsigned long long)tot);
     __syncthreads();
     if (tid == 0) {
-      s_touch_off = pool_alloc(A, s_tot + 1);
+      s_touch_off = pool_alloc_global(A, s_tot + 1);
       if (s_touch_off == RS_NONE) s_ok = 0;
     }
     __syncthreads();
-    if (!s_ok) { if (tid == 0) { A.n_sub[c] = 0; A.n_left[c] = 0; atomicOr(A.err, 8); } continue; }
+    if (!s_ok) {
+      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; atomicOr(A.err, 8); }
+      __syncthreads();
+      continue;
+    }
     uint32_t *touch = A.pk + s_touch_off;
-    // ---- SignalsInformation::new: occ (init -1 = absent), first position
+    // SignalsInformation::new: occurrences (init -1 = absent) over non-forbidden signals
     for (uint32_t pos = tid; pos < n; pos += nt) {
       uint32_t r = A.perm[b + pos];
       const uint32_t *k = A.rows.key + A.rows.off[r];
@@ -742,7 +763,6 @@ __global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_
         uint32_t s = k[i];
         if (A.forb[s]) continue;
         int32_t old = atomicAdd(&A.occ[s], 1);
-        atomicMin((uint32_t *)&A.rep_pos[s], pos);
         if (old == -1) touch[atomicAdd(&s_touch, 1u)] = s;
       }
     }
@@ -750,7 +770,7 @@ __global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_
     const uint32_t n_touch = s_touch;
     for (uint32_t t = tid; t < n_touch; t += nt) A.occ[touch[t]] += 1;  // -1 based -> count
     __syncthreads();
-    // ---- uniques: each row is consumed by its smallest unique signal
+    // uniques: each row is consumed by its smallest unique signal
     for (uint32_t pos = tid; pos < n; pos += nt) {
       uint32_t r = A.perm[b + pos];
       const uint32_t *k = A.rows.key + A.rows.off[r];
@@ -772,12 +792,11 @@ __global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_
       uint32_t r = A.perm[b + pos];
       const uint32_t *k = A.rows.key + A.rows.off[r];
       const Fe *v = A.rows.val + A.rows.off[r];
-      uint32_t len = A.rows.len[r];
-      uint32_t oi = A.order[b + pos];  // the row's smallest unique signal (chosen above)
+      uint32_t oi = A.order[b + pos];
       Fe coef;
       uint64_t to_off;
       uint32_t to_len;
-      if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { s_ok = 0; continue; }
+      if (!d_clear_nn(A, al, k, v, A.rows.len[r], oi, coef, to_off, to_len)) { s_ok = 0; continue; }
       uint32_t slot = atomicAdd(&s_m, 1u);
       uint32_t s = k[oi];
       A.holder_idx[s] = (int32_t)(b + slot);
@@ -788,153 +807,442 @@ __global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_
       A.del[s] = 1;
     }
     __syncthreads();
-    // remove_signal for the consumed uniques
-    for (uint32_t i = tid; i < s_m; i += nt) A.occ[A.h_sig[b + i]] = -1;
-    __syncthreads();
-    // ---- main loop (treat_constraint_4 + take_signal_4), one lane
-    if (tid == 0 && s_ok) {
-      uint32_t m = s_m, nl = 0;
-      bool ok = true;
-      for (uint64_t idx = e; idx-- > b && ok;) {
-        if (A.dead[idx]) continue;
-        uint32_t r = A.perm[idx];
-        const uint32_t *k = A.rows.key + A.rows.off[r];
-        const Fe *v = A.rows.val + A.rows.off[r];
-        uint32_t len = A.rows.len[r];
-        for (uint32_t i = 0; i < len; ++i)
-          if (!A.forb[k[i]] && A.occ[k[i]] >= 0) A.occ[k[i]]--;
-        for (;;) {
-          if (len == 0) break;
-          uint32_t oi = RS_NONE;
-          int32_t occ_ret = -1;
-          for (uint32_t i = 0; i < len; ++i) {
-            uint32_t s = k[i];
-            if (A.forb[s]) continue;
-            if (A.del[s]) { oi = i; break; }
-            int32_t c2 = A.occ[s];
-            if (c2 < 0) { atomicOr(A.err, 16); c2 = 0; }
-            if (occ_ret < 0 || c2 < occ_ret) { oi = i; occ_ret = c2; }
-            else if (c2 == occ_ret && k[oi] < s) oi = i;
-          }
-          if (oi == RS_NONE) {
-            uint64_t o = pool_alloc(A, len);
-            if (o == RS_NONE) { ok = false; break; }
-            for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
-            A.l_off[b + nl] = o;
-            A.l_len[b + nl] = len;
-            ++nl;
-            break;
-          }
-          uint32_t out = k[oi];
-          int32_t hi = A.holder_idx[out];
-          if (hi < 0) {
-            Fe coef;
-            uint64_t to_off;
-            uint32_t to_len;
-            if (!d_clear_nn(A, k, v, len, oi, coef, to_off, to_len)) { ok = false; break; }
-            A.holder_idx[out] = (int32_t)(b + m);
-            A.h_sig[b + m] = out;
-            A.h_coef[b + m] = coef;
-            A.h_off[b + m] = to_off;
-            A.h_len[b + m] = to_len;
-            ++m;
-            A.occ[out] = -1;
-            A.del[out] = 1;
-            break;
-          }
-          uint64_t w_off;
-          uint32_t w_len;
-          if (!d_merge(A, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) {
-            ok = false;
-            break;
-          }
-          k = A.pk + w_off;
-          v = A.pv + w_off;
-          len = w_len;
-        }
-      }
-      s_m = m;
-      s_nl = nl;
-      if (!ok) s_ok = 0;
-    }
-    __syncthreads();
-    const uint32_t m = s_m;
-    // ---- normalize_substitutions: per-thread chunks with Montgomery's batch inversion
-    if (s_ok) {
-      uint32_t per = (m + nt - 1) / nt;
-      uint32_t lo = tid * per, hi = min(m, lo + per);
-      if (lo < hi) {
-        Fe acc = A.h_coef[b + lo];
-        A.ftmp[b + lo] = acc;
-        for (uint32_t i = lo + 1; i < hi; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
-        Fe inv = finv(F, acc);
-        for (uint32_t i = hi; i-- > lo;) {
-          Fe inv_i = i > lo ? fmul(F, A.ftmp[b + i - 1], inv) : inv;
-          inv = fmul(F, inv, A.h_coef[b + i]);
-          Fe *vv = A.pv + A.h_off[b + i];
-          for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
-        }
+    for (uint32_t i = tid; i < s_m; i += nt) A.occ[A.h_sig[b + i]] = -1;  // remove_signal
+    if (tid == 0) {
+      A.n_sub[c] = s_m;
+      A.big_touch_off[ci] = s_touch_off;
+      A.big_touch_n[ci] = n_touch;
+      if (!s_ok) atomicOr(A.err, 8);
+      if (A.prof) {
+        unsigned long long *P = A.prof + 16 * ci;
+        P[0] = n; P[4] = wall_clock64() - t_0; P[12] = n_touch;
       }
     }
     __syncthreads();
-    // ---- composition, level by level over the dependency DAG
-    for (uint32_t i = tid; i < m; i += nt) A.tmp[b + i] = 0;  // resolved flags
+  }
+}
+
+// The rest of one row's treat_constraint_4 loop on a work list in the pool (single lane; used when
+// a list does not fit the LDS buffers of k_big_main).
+__device__ inline bool d_treat4_scalar(const ElimArgs &A, Alloc &al, uint64_t b, const uint32_t *k, const Fe *v,
+                                       uint32_t len, uint32_t &m, uint32_t &nl) {
+  const FieldP &F = A.F;
+  for (;;) {
+    if (len == 0) return true;
+    uint32_t oi = RS_NONE;
+    int32_t occ_ret = -1;
+    for (uint32_t i = 0; i < len; ++i) {
+      uint32_t s = k[i];
+      if (A.forb[s]) continue;
+      if (A.del[s]) { oi = i; break; }
+      int32_t c2 = A.occ[s];
+      if (c2 < 0) { atomicOr(A.err, 16); c2 = 0; }
+      if (occ_ret < 0 || c2 < occ_ret) { oi = i; occ_ret = c2; }
+      else if (c2 == occ_ret && k[oi] < s) oi = i;
+    }
+    if (oi == RS_NONE) {
+      uint64_t o = pool_alloc(A, al, len);
+      if (o == RS_NONE) return false;
+      for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
+      A.l_off[b + nl] = o;
+      A.l_len[b + nl] = len;
+      ++nl;
+      return true;
+    }
+    uint32_t out = k[oi];
+    int32_t hi = A.holder_idx[out];
+    if (hi < 0) {
+      Fe coef;
+      uint64_t to_off;
+      uint32_t to_len;
+      if (!d_clear_nn(A, al, k, v, len, oi, coef, to_off, to_len)) return false;
+      A.holder_idx[out] = (int32_t)(b + m);
+      A.h_sig[b + m] = out;
+      A.h_coef[b + m] = coef;
+      A.h_off[b + m] = to_off;
+      A.h_len[b + m] = to_len;
+      ++m;
+      A.occ[out] = -1;
+      A.del[out] = 1;
+      return true;
+    }
+    uint64_t w_off;
+    uint32_t w_len;
+    if (!d_merge(A, al, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) return false;
+    k = A.pk + w_off;
+    v = A.pv + w_off;
+    len = w_len;
+  }
+}
+
+// exclusive scan of a[0..n) (LDS) by one 64-lane workgroup; returns the total
+__device__ inline uint32_t wave_excl_scan(uint32_t *a, uint32_t n) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t per = (n + 63) / 64, lo = min(n, lane * per), hi = min(n, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += a[i];
+  uint32_t x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d);
+    if ((int)lane >= d) x += y;
+  }
+  uint32_t acc = x - sum;
+  for (uint32_t i = lo; i < hi; ++i) { uint32_t t = a[i]; a[i] = acc; acc += t; }
+  uint32_t total = __shfl(x, 63);
+  __syncthreads();
+  return total;
+}
+__device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t *a, uint32_t n, uint32_t key) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+constexpr uint32_t kBigCap = 512;  // LDS work-list capacity of k_big_main
+
+__global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const FieldP &F = A.F;
+  __shared__ uint32_t wk[2][kBigCap];
+  __shared__ Fe wv[2][kBigCap];
+  __shared__ uint32_t rk[kBigCap];
+  __shared__ Fe rv[kBigCap];
+  __shared__ uint32_t fw[kBigCap], fr[kBigCap], lbw[kBigCap], lbr[kBigCap];
+  __shared__ uint32_t s_fdel, s_m, s_nl, s_ok, s_rlen;
+  __shared__ unsigned long long s_best;
+  __shared__ uint64_t s_o, s_roff;
+  __shared__ Fe s_c2;
+  const uint32_t tid = threadIdx.x, nt = 64;
+  Alloc al0;  // lane 0's allocator
+  al0.chunk = 16384;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    unsigned long long t_1 = wall_clock64();
+    unsigned long long merges = 0, mwork = 0, rows = 0;
+    if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
-    for (uint32_t iter = 0; s_ok && iter <= m; ++iter) {
-      if (tid == 0) { s_progress = 0; s_left_todo = 0; }
+    for (uint64_t idx = e; idx-- > b;) {
+      if (!s_ok) break;
+      if (A.dead[idx]) continue;
+      ++rows;
+      const uint32_t r = A.perm[idx];
+      const uint32_t *k = A.rows.key + A.rows.off[r];
+      const Fe *v = A.rows.val + A.rows.off[r];
+      uint32_t len = A.rows.len[r];
+      for (uint32_t i = tid; i < len; i += nt) {  // remove_constraint (keys of a row are distinct)
+        uint32_t s = k[i];
+        if (!A.forb[s] && A.occ[s] >= 0) A.occ[s]--;
+      }
+      if (len > kBigCap) {
+        __syncthreads();
+        if (tid == 0) {
+          uint32_t m = s_m, nl = s_nl;
+          if (!d_treat4_scalar(A, al0, b, k, v, len, m, nl)) s_ok = 0;
+          s_m = m;
+          s_nl = nl;
+        }
+        __syncthreads();
+        continue;
+      }
+      for (uint32_t i = tid; i < len; i += nt) { wk[0][i] = k[i]; wv[0][i] = v[i]; }
+      uint32_t cur = 0;
       __syncthreads();
-      // readiness (read-only pass): 1 = ready, 2 = already resolved
+      while (len > 0) {
+        // take_signal_4: the first deleted key (ascending), else min occurrences, ties -> max id
+        if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
+        __syncthreads();
+        for (uint32_t i = tid; i < len; i += nt) {
+          uint32_t s = wk[cur][i];
+          if (A.forb[s]) continue;
+          if (A.del[s]) { atomicMin(&s_fdel, i); continue; }
+          int32_t o = A.occ[s];
+          if (o < 0) { atomicOr(A.err, 16); o = 0; }
+          atomicMin(&s_best, ((unsigned long long)(uint32_t)o << 32) | (0xffffffffu - i));  // sorted keys
+        }
+        __syncthreads();
+        const uint32_t fdel = s_fdel;
+        const unsigned long long best = s_best;
+        if (fdel == RS_NONE && best == ~0ull) {  // nothing takeable: leftover
+          if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
+          __syncthreads();
+          if (s_ok) {
+            const uint64_t o = s_o;
+            for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
+            if (tid == 0) { A.l_off[b + s_nl] = o; A.l_len[b + s_nl] = len; s_nl = s_nl + 1; }
+          }
+          __syncthreads();
+          break;
+        }
+        const uint32_t oi = fdel != RS_NONE ? fdel : 0xffffffffu - (uint32_t)(best & 0xffffffffu);
+        const uint32_t p = wk[cur][oi];
+        if (fdel == RS_NONE) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
+          const uint32_t sh = wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
+          const uint32_t mm = len - 1 + sh;
+          if (tid == 0) { s_o = pool_alloc(A, al0, mm); if (s_o == RS_NONE) s_ok = 0; }
+          __syncthreads();
+          if (s_ok) {
+            const uint64_t o = s_o;
+            for (uint32_t i = tid; i < len; i += nt) {
+              if (i == oi) continue;
+              uint32_t q = (i < oi ? i : i - 1) + sh;
+              A.pk[o + q] = wk[cur][i];
+              A.pv[o + q] = wv[cur][i];
+            }
+            if (tid == 0) {
+              if (sh) { A.pk[o] = 0; A.pv[o] = fe_zero(); }
+              const uint64_t slot = b + s_m;
+              A.holder_idx[p] = (int32_t)slot;
+              A.h_sig[slot] = p;
+              A.h_coef[slot] = fneg(F, wv[cur][oi]);
+              A.h_off[slot] = o;
+              A.h_len[slot] = mm;
+              s_m = s_m + 1;
+              A.occ[p] = -1;
+              A.del[p] = 1;
+            }
+          }
+          __syncthreads();
+          break;
+        }
+        // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p)
+        if (tid == 0) {
+          int32_t hs = A.holder_idx[p];
+          s_roff = A.h_off[hs];
+          s_rlen = A.h_len[hs];
+          s_c2 = A.h_coef[hs];
+        }
+        __syncthreads();
+        const uint32_t rl = s_rlen;
+        const uint64_t roff = s_roff;
+        ++merges;
+        mwork += len + rl;
+        if (rl > kBigCap || len + rl > kBigCap + 1) {  // spill, finish the row on lane 0
+          if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
+          __syncthreads();
+          if (s_ok) {
+            const uint64_t o = s_o;
+            for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
+            __syncthreads();
+            if (tid == 0) {
+              uint32_t m = s_m, nl = s_nl;
+              if (!d_treat4_scalar(A, al0, b, A.pk + o, A.pv + o, len, m, nl)) s_ok = 0;
+              s_m = m;
+              s_nl = nl;
+            }
+          }
+          __syncthreads();
+          break;
+        }
+        const Fe c2 = s_c2;
+        const Fe coef = fneg(F, wv[cur][oi]);
+        for (uint32_t j = tid; j < rl; j += nt) { rk[j] = A.pk[roff + j]; rv[j] = A.pv[roff + j]; }
+        __syncthreads();
+        for (uint32_t i = tid; i < len; i += nt) {
+          if (i == oi) { fw[i] = 0; continue; }
+          const uint32_t key = wk[cur][i];
+          const uint32_t lb = lds_lower_bound(rk, rl, key);
+          Fe x = fneg(F, fmul(F, c2, wv[cur][i]));
+          if (lb < rl && rk[lb] == key) x = fadd(F, fmul(F, coef, rv[lb]), x);
+          wv[cur][i] = x;
+          lbw[i] = lb;
+          fw[i] = fe_is_zero(x) ? 0 : 1;
+        }
+        for (uint32_t j = tid; j < rl; j += nt) {
+          const uint32_t key = rk[j];
+          const uint32_t lb = lds_lower_bound(wk[cur], len, key);
+          if (lb < len && wk[cur][lb] == key) { fr[j] = 0; lbr[j] = RS_NONE; continue; }
+          Fe x = fmul(F, coef, rv[j]);
+          rv[j] = x;
+          lbr[j] = lb;
+          fr[j] = fe_is_zero(x) ? 0 : 1;
+        }
+        __syncthreads();
+        const uint32_t tw = wave_excl_scan(fw, len);
+        const uint32_t tr = wave_excl_scan(fr, rl);
+        const uint32_t nx = cur ^ 1;
+        for (uint32_t i = tid; i < len; i += nt) {
+          if (i == oi || fe_is_zero(wv[cur][i])) continue;
+          const uint32_t lb = lbw[i];
+          const uint32_t q = fw[i] + (lb < rl ? fr[lb] : tr);
+          wk[nx][q] = wk[cur][i];
+          wv[nx][q] = wv[cur][i];
+        }
+        for (uint32_t j = tid; j < rl; j += nt) {
+          const uint32_t lb = lbr[j];
+          if (lb == RS_NONE || fe_is_zero(rv[j])) continue;
+          const uint32_t q = fr[j] + (lb < len ? fw[lb] : tw);
+          wk[nx][q] = rk[j];
+          wv[nx][q] = rv[j];
+        }
+        __syncthreads();
+        cur = nx;
+        len = tw + tr;
+      }
+    }
+    if (tid == 0) {
+      A.n_sub[c] = s_m;
+      A.n_left[c] = s_nl;
+      if (!s_ok) atomicOr(A.err, 8);
+      if (A.prof) {
+        unsigned long long *P = A.prof + 16 * ci;
+        P[2] = rows; P[5] = wall_clock64() - t_1; P[8] = merges; P[9] = mwork;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// block-wide exclusive scan (256 lanes) of a[0..n) in global memory; s_part: 4 words of LDS
+__device__ inline uint32_t blk_excl_scan(uint32_t *a, uint32_t n, uint32_t *s_part) {
+  const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6;
+  uint32_t per = (n + nt - 1) / nt, lo = min(n, tid * per), hi = min(n, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += a[i];
+  uint32_t x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d);
+    if ((int)lane >= d) x += y;
+  }
+  if (lane == 63) s_part[w] = x;
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (uint32_t q = 0; q < nt / 64; ++q) { if (q < w) base += s_part[q]; total += s_part[q]; }
+  uint32_t acc = base + x - sum;
+  for (uint32_t i = lo; i < hi; ++i) { uint32_t t = a[i]; a[i] = acc; acc += t; }
+  __syncthreads();
+  return total;
+}
+
+__global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const FieldP &F = A.F;
+  __shared__ uint32_t s_ok, s_nf, s_part[4];
+  __shared__ uint64_t s_scr;
+  __shared__ unsigned long long s_hsum, s_hmax;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  Alloc al;
+  al.chunk = 512;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b);
+    const uint32_t m = A.n_sub[c];
+    unsigned long long t_2 = wall_clock64();
+    if (tid == 0) s_ok = 1;
+    // ---- normalize_substitutions: each lane batch-inverts the slots i = tid (mod nt)
+    if (tid < m) {
+      Fe acc = A.h_coef[b + tid];
+      A.ftmp[b + tid] = acc;
+      uint32_t last = tid;
+      for (uint32_t i = tid + nt; i < m; i += nt) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; last = i; }
+      Fe inv = finv(F, acc);
+      for (uint32_t i = last;; i -= nt) {
+        Fe inv_i = i >= tid + nt ? fmul(F, A.ftmp[b + i - nt], inv) : inv;
+        inv = fmul(F, inv, A.h_coef[b + i]);
+        Fe *vv = A.pv + A.h_off[b + i];
+        for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
+        if (i < tid + nt) break;
+      }
+    }
+    unsigned long long t_3 = wall_clock64();
+    // ---- composition over the dependency DAG in Kahn order: a substitution is composed once every
+    // deleted key of its right-hand side is final (the result does not depend on the order).
+    // scratch (u32): deg[m], dcnt[m+1], dfill[m], frontier[2][m], dependents[sum deg]
+    if (tid == 0) {
+      s_scr = pool_alloc_global(A, 6ull * m + 8);
+      if (s_scr == RS_NONE) s_ok = 0;
+    }
+    __syncthreads();
+    uint32_t levels = 0;
+    if (s_ok && m) {
+      uint32_t *deg = A.pk + s_scr, *dcnt = deg + m, *dfill = dcnt + m + 1, *fr0 = dfill + m, *fr1 = fr0 + m;
+      for (uint32_t i = tid; i < m; i += nt) { deg[i] = 0; dcnt[i] = 0; dfill[i] = 0; }
+      if (tid == 0) { dcnt[m] = 0; s_nf = 0; }
+      __syncthreads();
       for (uint32_t i = tid; i < m; i += nt) {
-        if (A.tmp[b + i] == 1) continue;  // resolved
         const uint32_t *kk = A.pk + A.h_off[b + i];
-        uint32_t len = A.h_len[b + i];
-        bool ready = true;
-        for (uint32_t t = 0; t < len && ready; ++t) {
-          int32_t hs = A.holder_idx[kk[t]];
-          if (hs >= 0 && A.tmp[hs] != 1) ready = false;
-        }
-        A.order[b + i] = ready ? 1u : 0u;
-        atomicAdd(&s_left_todo, 1u);
-      }
-      __syncthreads();
-      if (s_left_todo == 0) break;
-      for (uint32_t i = tid; i < m; i += nt) {
-        if (A.tmp[b + i] == 1 || A.order[b + i] != 1) continue;
-        uint64_t off = A.h_off[b + i];
-        uint32_t len = A.h_len[b + i];
-        const uint32_t *kk = A.pk + off;
-        uint64_t bound = len;
-        uint32_t n_app = 0;
+        uint32_t len = A.h_len[b + i], d = 0;
         for (uint32_t t = 0; t < len; ++t) {
           int32_t hs = A.holder_idx[kk[t]];
-          if (hs >= 0) { bound += A.h_len[hs]; ++n_app; }
+          if (hs >= 0) { ++d; atomicAdd(&dcnt[hs - b], 1u); }
         }
-        if (n_app) {
-          uint64_t buf0 = pool_alloc(A, bound), buf1 = pool_alloc(A, bound);
-          if (buf0 == RS_NONE || buf1 == RS_NONE) { s_ok = 0; continue; }
-          uint64_t orig_off = off;
-          uint32_t orig_len = len;
-          uint64_t dst = buf0;
-          for (uint32_t t = 0; t < orig_len; ++t) {
-            int32_t hs = A.holder_idx[A.pk[orig_off + t]];
-            if (hs < 0) continue;
-            uint32_t nl2;
-            d_raw_sub_into(A, off, len, A.pk[orig_off + t], A.h_off[hs], A.h_len[hs], dst, nl2);
-            off = dst;
-            len = nl2;
-            dst = dst == buf0 ? buf1 : buf0;
-          }
-          A.h_off[b + i] = off;
-          A.h_len[b + i] = len;
-        }
-        A.order[b + i] = 2;  // resolved at the end of this level
-        s_progress = 1;
+        deg[i] = d;
+        if (!d) fr0[atomicAdd(&s_nf, 1u)] = i;
       }
       __syncthreads();
-      for (uint32_t i = tid; i < m; i += nt)
-        if (A.order[b + i] == 2) A.tmp[b + i] = 1;
+      const uint32_t n_edges = blk_excl_scan(dcnt, m + 1, s_part);
+      if (tid == 0) {
+        s_scr = pool_alloc_global(A, (uint64_t)n_edges + 1);
+        if (s_scr == RS_NONE) s_ok = 0;
+      }
       __syncthreads();
-      if (!s_progress) { if (tid == 0) { s_ok = 0; atomicOr(A.err, 32); } break; }
+      if (s_ok) {
+        uint32_t *dl = A.pk + s_scr;
+        for (uint32_t i = tid; i < m; i += nt) {
+          if (!deg[i]) continue;
+          const uint32_t *kk = A.pk + A.h_off[b + i];
+          uint32_t len = A.h_len[b + i];
+          for (uint32_t t = 0; t < len; ++t) {
+            int32_t hs = A.holder_idx[kk[t]];
+            if (hs >= 0) { uint32_t q = (uint32_t)(hs - b); dl[dcnt[q] + atomicAdd(&dfill[q], 1u)] = i; }
+          }
+        }
+        __syncthreads();
+        uint32_t nf = s_nf, done = nf;
+        uint32_t *cur = fr0, *nxt = fr1;
+        while (nf && s_ok) {
+          __syncthreads();
+          if (tid == 0) s_nf = 0;
+          __syncthreads();
+          for (uint32_t f = tid; f < nf; f += nt) {
+            uint32_t q = cur[f];
+            for (uint32_t t = dcnt[q]; t < dcnt[q + 1]; ++t) {
+              uint32_t d = dl[t];
+              if (atomicSub(&deg[d], 1u) == 1u) nxt[atomicAdd(&s_nf, 1u)] = d;
+            }
+          }
+          __syncthreads();
+          nf = s_nf;
+          for (uint32_t f = tid; f < nf; f += nt) {
+            const uint32_t i = nxt[f];
+            uint64_t off = A.h_off[b + i];
+            uint32_t len = A.h_len[b + i];
+            const uint32_t *kk = A.pk + off;
+            uint64_t bound = len;
+            for (uint32_t t = 0; t < len; ++t) {
+              int32_t hs = A.holder_idx[kk[t]];
+              if (hs >= 0) bound += A.h_len[hs];
+            }
+            uint64_t buf0 = pool_alloc(A, al, bound), buf1 = pool_alloc(A, al, bound);
+            if (buf0 == RS_NONE || buf1 == RS_NONE) { s_ok = 0; continue; }
+            const uint64_t orig_off = off;
+            const uint32_t orig_len = len;
+            uint64_t dst = buf0;
+            for (uint32_t t = 0; t < orig_len; ++t) {  // raw_substitution key by key, ascending
+              uint32_t key = A.pk[orig_off + t];
+              int32_t hs = A.holder_idx[key];
+              if (hs < 0) continue;
+              uint32_t nl2;
+              d_raw_sub_into(A, off, len, key, A.h_off[hs], A.h_len[hs], dst, nl2);
+              off = dst;
+              len = nl2;
+              dst = dst == buf0 ? buf1 : buf0;
+            }
+            A.h_off[b + i] = off;
+            A.h_len[b + i] = len;
+          }
+          done += nf;
+          ++levels;
+          uint32_t *t = cur; cur = nxt; nxt = t;
+          __syncthreads();  // s_ok is read by every lane in the loop condition
+        }
+        __syncthreads();
+        if (s_ok && done != m) { if (tid == 0) { s_ok = 0; atomicOr(A.err, 32); } }
+      }
     }
     __syncthreads();
     // ---- emit, reset the dense scratch
@@ -945,15 +1253,26 @@ __global__ __launch_bounds__(256) void k_eliminate_big(ElimArgs A, const uint32_
       A.sub_of[s] = (int32_t)(b + i);
       A.deleted[s] = 1;
     }
-    for (uint32_t t = tid; t < n_touch; t += nt) { A.occ[touch[t]] = -1; A.rep_pos[touch[t]] = -1; }
+    const uint32_t *touch = A.pk + A.big_touch_off[ci];
+    for (uint32_t t = tid; t < A.big_touch_n[ci]; t += nt) A.occ[touch[t]] = -1;
     uint64_t rows_e = 0, subs_e = 0;
+    uint32_t hmax = 0;
     for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
-    for (uint32_t i = tid; i < m; i += nt) subs_e += A.h_len[b + i];
+    for (uint32_t i = tid; i < m; i += nt) { subs_e += A.h_len[b + i]; hmax = max(hmax, A.h_len[b + i]); }
     atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0)));
+    if (A.prof) {
+      if (tid == 0) { s_hsum = 0; s_hmax = 0; }
+      __syncthreads();
+      atomicAdd(&s_hsum, (unsigned long long)subs_e);
+      atomicMax(&s_hmax, (unsigned long long)hmax);
+      __syncthreads();
+    }
     if (tid == 0) {
-      A.n_sub[c] = m;
-      A.n_left[c] = s_nl;
       if (!s_ok) atomicOr(A.err, 8);
+      if (A.prof) {
+        unsigned long long *P = A.prof + 16 * ci;
+        P[1] = m; P[3] = levels; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3; P[10] = s_hsum; P[11] = s_hmax;
+      }
     }
     __syncthreads();
   }

@@ -131,6 +131,11 @@ typedef struct rs_stats {
   double elim_kernel_ms;       /* device time of the per-cluster elimination (k_eliminate)   */
   uint64_t elim_kernel_launches;
   uint64_t elim_bytes;         /* its algorithmic bytes (sum over launches)                  */
+  double elim_big_ms;          /* device time of the large-cluster kernel (k_eliminate_big)  */
+  double elim_small_ms;        /* device time of the small-cluster kernel                    */
+  double nl_ms;                /* non-linear frames (count, scan, fill, split)               */
+  double map_ms;               /* host copy of the non-linear signal map (rounds >= 2)       */
+  double rounds_ms;            /* storage updates + bookkeeping of rounds >= 2               */
   uint64_t rounds;             /* linear-elimination rounds executed                         */
   uint64_t n_clusters;
   uint64_t n_substitutions;
