@@ -1,0 +1,215 @@
+// cluster.hpp -- build_clusters (constraint_list/src/constraint_simplification.rs:45-99) on the device.
+//
+// The reference walks the linear rows in list order; row j gets arena slot j and, for each of its
+// signals s (canonical order: ascending), merges the cluster of prev(s) -- the last earlier row
+// holding s -- into its own: merged = [j's list] ++ [that cluster's list] (Cluster::merge, :32-38).
+// Because the destination is always the newest row, the root of every cluster is its maximum row
+// index, which gives the device formulation:
+//   1. pairs (s, j) sorted by (s, j)            -> prev(s, j) and a union-find over rows;
+//   2. cluster of a row = max row of its component; clusters are emitted in ascending max row
+//      (arena order, :90-97) and a cluster's rows are first listed by ascending index;
+//   3. the list order inside a cluster is the replay of the arena merges restricted to that cluster
+//      (clusters are independent): one lane per small cluster, one workgroup with LDS-resident u16
+//      state per large cluster, the lane-serial global-memory replay beyond the LDS capacity.
+#pragma once
+#include "kernels.hpp"
+
+namespace rs {
+
+constexpr uint32_t kClRowBit = 0x80000000u;  // stream entry: first pair of a row
+constexpr uint32_t kClNoPrev = 0x7fffffffu;
+constexpr uint32_t kClSmall = 64;     // clusters up to this size: one lane each
+constexpr uint32_t kClLds = 32768;    // clusters up to this size: LDS replay (u16 local ids)
+constexpr uint32_t kClChunk = 4096;   // stream entries staged per LDS chunk
+
+// pairs per row (non-constant keys) and the active-row statistics
+__global__ void k_cl_count(DRows V, uint64_t *npairs, unsigned long long *stat /* [0] nnz, [1] active */) {
+  unsigned long long nnz = 0, act = 0;
+  for (uint64_t r = gtid(); r < V.n; r += gstride()) {
+    uint32_t len = V.len[r];
+    npairs[r] = len - (len && V.key[V.off[r]] == 0 ? 1 : 0);
+    nnz += len;
+    act += len ? 1 : 0;
+  }
+  if (nnz) atomicAdd(&stat[0], nnz);
+  if (act) atomicAdd(&stat[1], act);
+}
+__global__ void k_cl_fill(DRows V, const uint64_t *poff, uint64_t *pkey, uint32_t *pslot) {
+  for (uint64_t r = gtid(); r < V.n; r += gstride()) {
+    uint64_t o = poff[r];
+    const uint32_t *k = V.key + V.off[r];
+    for (uint32_t i = 0; i < V.len[r]; ++i) {
+      if (k[i] == 0) continue;
+      pkey[o] = ((uint64_t)k[i] << 32) | r;
+      pslot[o] = (uint32_t)o;
+      ++o;
+    }
+  }
+}
+__device__ inline void uf_union(uint32_t *uf, uint32_t a, uint32_t b) {
+  for (;;) {
+    a = uf_find(uf, a);
+    b = uf_find(uf, b);
+    if (a == b) return;
+    if (a > b) { uint32_t t = a; a = b; b = t; }
+    uint32_t old = atomicCAS(&uf[b], b, a);
+    if (old == b) return;
+    b = old;
+  }
+}
+// prev(s, j) from the sorted pairs; rows sharing a signal are joined
+__global__ void k_cl_link(const uint64_t *pk, const uint32_t *ps, uint64_t P, uint32_t *prevrow, uint32_t *uf) {
+  for (uint64_t i = gtid(); i < P; i += gstride()) {
+    uint64_t x = pk[i];
+    if (i > 0 && (pk[i - 1] >> 32) == (x >> 32)) {
+      uint32_t p = (uint32_t)pk[i - 1];
+      prevrow[ps[i]] = p;
+      uf_union(uf, p, (uint32_t)x);
+    } else {
+      prevrow[ps[i]] = RS_NONE;
+    }
+  }
+}
+__global__ void k_cl_root(const uint32_t *len, uint64_t n, uint32_t *uf, int32_t *cmax) {
+  for (uint64_t r = gtid(); r < n; r += gstride())
+    if (len[r]) atomicMax(&cmax[uf_find(uf, (uint32_t)r)], (int32_t)r);
+}
+__global__ void k_cl_key(const uint32_t *len, uint64_t n, uint32_t *uf, const int32_t *cmax, uint64_t *rkey,
+                         uint32_t *ridx) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    rkey[r] = len[r] ? ((uint64_t)(uint32_t)cmax[uf_find(uf, (uint32_t)r)] << 32) | r : ~0ull;
+    ridx[r] = (uint32_t)r;
+  }
+}
+__global__ void k_cl_flag(const uint64_t *rkey, uint64_t n_act, uint64_t *flag) {
+  for (uint64_t i = gtid(); i < n_act; i += gstride())
+    flag[i] = (i == 0 || (rkey[i] >> 32) != (rkey[i - 1] >> 32)) ? 1 : 0;
+}
+// cluster starts, cluster of each position, position of each row, pair counts in cluster order
+__global__ void k_cl_starts(const uint64_t *rkey, const uint64_t *fscan, const uint32_t *srow, const uint64_t *npairs,
+                            uint64_t n_act, uint64_t n_cl, uint64_t *cl_off, uint32_t *cid, uint32_t *gpos, uint64_t *qn) {
+  for (uint64_t i = gtid(); i < n_act; i += gstride()) {
+    bool st = i == 0 || (rkey[i] >> 32) != (rkey[i - 1] >> 32);
+    uint64_t c = fscan[i] + (st ? 1 : 0) - 1;
+    if (st) cl_off[c] = i;
+    if (i == 0) cl_off[n_cl] = n_act;
+    cid[i] = (uint32_t)c;
+    uint32_t j = srow[i];
+    gpos[j] = (uint32_t)i;
+    qn[i] = npairs[j];
+  }
+}
+// the per-cluster replay stream: local id of prev(s, j) for each pair, rows in ascending index
+__global__ void k_cl_stream(const uint32_t *srow, const uint64_t *poff, const uint32_t *prevrow, const uint32_t *gpos,
+                            const uint32_t *cid, const uint64_t *cl_off, const uint64_t *q_off, uint64_t n_act,
+                            uint32_t *stream) {
+  for (uint64_t i = gtid(); i < n_act; i += gstride()) {
+    uint32_t j = srow[i];
+    uint64_t base = cl_off[cid[i]], q = q_off[i], np = q_off[i + 1] - q, o = poff[j];
+    for (uint64_t t = 0; t < np; ++t) {
+      uint32_t p = prevrow[o + t];
+      uint32_t loc = p == RS_NONE ? kClNoPrev : (uint32_t)(gpos[p] - base);
+      stream[q + t] = loc | (t == 0 ? kClRowBit : 0u);
+    }
+  }
+}
+
+// lane replay (small clusters, and the global-memory path beyond the LDS capacity)
+__global__ void k_cl_replay_lane(const uint64_t *cl_off, uint64_t n_cl, const uint64_t *q_off, const uint32_t *stream,
+                                 const uint32_t *srow, uint32_t *c2c, uint32_t *tail, uint32_t *next, uint32_t *perm) {
+  for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
+    const uint64_t b = cl_off[c];
+    const uint32_t n = (uint32_t)(cl_off[c + 1] - b);
+    if (n > kClSmall && n <= kClLds) continue;
+    uint32_t *C2 = c2c + b, *T = tail + b, *N = next + b;
+    for (uint32_t t = 0; t < n; ++t) {
+      C2[t] = t;
+      T[t] = t;
+      N[t] = RS_NONE;
+      for (uint64_t q = q_off[b + t]; q < q_off[b + t + 1]; ++q) {
+        uint32_t p = stream[q] & ~kClRowBit;
+        if (p == kClNoPrev) continue;
+        while (C2[p] != p) { uint32_t g = C2[C2[p]]; C2[p] = g; p = g; }  // path halving
+        if (p == t) continue;
+        N[T[t]] = p;
+        T[t] = T[p];
+        C2[p] = t;
+      }
+    }
+    uint32_t x = n - 1, q = 0;
+    while (x != RS_NONE) { perm[b + q++] = srow[b + x]; x = N[x]; }
+  }
+}
+
+// workgroup replay with the union-find state in LDS (kClSmall < n <= kClLds); `ids` lists them
+__global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, const uint32_t *ids, uint64_t n_ids,
+                                                       const uint64_t *q_off, const uint32_t *stream,
+                                                       const uint32_t *srow, uint32_t *next, uint32_t *perm) {
+  __shared__ uint16_t C2[kClLds], T[kClLds];
+  __shared__ uint32_t S[kClChunk];
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = cl_off[c];
+    const uint32_t n = (uint32_t)(cl_off[c + 1] - b);
+    const uint64_t q0 = q_off[b], q1 = q_off[b + n];
+    uint32_t *N = next + b;
+    int32_t t = -1;  // lane 0: current row
+    for (uint64_t qc = q0; qc < q1; qc += kClChunk) {
+      const uint32_t m = (uint32_t)min<uint64_t>(kClChunk, q1 - qc);
+      __syncthreads();
+      for (uint32_t i = tid; i < m; i += nt) S[i] = stream[qc + i];
+      __syncthreads();
+      if (tid == 0) {
+        for (uint32_t i = 0; i < m; ++i) {
+          uint32_t e = S[i];
+          if (e & kClRowBit) {
+            ++t;
+            C2[t] = (uint16_t)t;
+            T[t] = (uint16_t)t;
+            N[t] = RS_NONE;
+          }
+          uint32_t p = e & ~kClRowBit;
+          if (p == kClNoPrev) continue;
+          while (C2[p] != p) { uint32_t g = C2[C2[p]]; C2[p] = (uint16_t)g; p = g; }
+          if (p == (uint32_t)t) continue;
+          N[T[t]] = p;
+          T[t] = T[p];
+          C2[p] = (uint16_t)t;
+        }
+      }
+    }
+    __syncthreads();
+    // next -> LDS (C2 is free now), walk from the root (the last row), gather the rows
+    for (uint32_t i = tid; i < n; i += nt) { uint32_t x = N[i]; C2[i] = (uint16_t)(x == RS_NONE ? 0xffffu : x); }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t x = n - 1, q = 0;
+      while (x != 0xffffu) { T[q++] = (uint16_t)x; x = C2[x]; }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += nt) perm[b + i] = srow[b + T[i]];
+    __syncthreads();
+  }
+}
+
+// cluster-size classes for the elimination kernels: sorted by (size desc, index)
+__global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, uint64_t *skey, uint32_t *sidx,
+                             unsigned long long *cnt /* [0] >= 1e6, [1] process_4 range, [2] LDS replay, [3] > LDS */,
+                             int old_heur) {
+  for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
+    uint64_t sz = cl_off[c + 1] - cl_off[c];
+    skey[c] = ((uint64_t)(0xffffffffu - (uint32_t)sz) << 32) | c;
+    sidx[c] = (uint32_t)c;
+    if (sz >= 1000000) atomicAdd(&cnt[0], 1ull);
+    else if (sz >= 350 && !old_heur) atomicAdd(&cnt[1], 1ull);
+    if (sz > kClSmall && sz <= kClLds) atomicAdd(&cnt[2], 1ull);
+    if (sz > kClLds) atomicAdd(&cnt[3], 1ull);
+  }
+}
+// small list = sorted[0, h) ++ sorted[h + nb, n_cl)
+__global__ void k_cl_small_ids(const uint32_t *sorted, uint64_t n_cl, uint64_t h, uint64_t nb, uint32_t *small) {
+  for (uint64_t i = gtid(); i < n_cl - nb; i += gstride()) small[i] = sorted[i < h ? i : i + nb];
+}
+
+}  // namespace rs

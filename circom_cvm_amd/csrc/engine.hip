@@ -18,10 +18,12 @@
 #include <vector>
 
 #include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include "host_common.hpp"
 #include "kernels.hpp"
+#include "cluster.hpp"
 
 namespace rs {
 
@@ -128,7 +130,6 @@ struct rs_engine {
   std::vector<HostCon> out_host_tail;  // lconst rows appended after the device rows
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
-  std::vector<int32_t> sig2cl;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
@@ -171,6 +172,16 @@ static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, u
   HC(hipMemcpyAsync(&last_out, out + n - 1, 8, hipMemcpyDeviceToHost, E->st));
   HC(hipStreamSynchronize(E->st));
   return last_in + last_out;
+}
+
+template <class K, class V>
+static void sort_pairs(rs_engine *E, const K *kin, K *kout, const V *vin, V *vout, uint64_t n, int end_bit,
+                       const char *tag) {
+  if (!n) return;
+  size_t tb = 0;
+  HC(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, E->st));
+  void *tmp = E->A.get<uint8_t>(std::string("sort.tmp.") + tag, tb);
+  HC(rocprim::radix_sort_pairs(tmp, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, E->st));
 }
 
 __global__ void k_u32_to_u64(const uint32_t *in, uint64_t *out, uint64_t n) {
@@ -284,61 +295,6 @@ __global__ void k_emit_pairs(DRows a, DRows b, DRows c, const uint8_t *flag, uin
 
 // ---------------------------------------------------------------- host clustering
 // build_clusters (constraint_simplification.rs:45-99): arena order + dest ++ src lists.
-static void host_clusters(rs_engine *E, const HostRows &R, uint64_t n, std::vector<uint32_t> &perm,
-                          std::vector<uint64_t> &cl_off) {
-  std::vector<int32_t> &sig2cl = E->sig2cl;
-  if (sig2cl.size() < E->S) sig2cl.assign(E->S, -1);
-  std::vector<int32_t> head, tail, c2c, next(n, -1);
-  std::vector<uint32_t> touched;
-  head.reserve(n);
-  tail.reserve(n);
-  c2c.reserve(n);
-  auto findr = [&](int32_t org) {
-    int32_t cur = org;
-    while (cur != c2c[cur]) cur = c2c[cur];
-    while (org != cur) {
-      int32_t nx = c2c[org];
-      c2c[org] = cur;
-      org = nx;
-    }
-    return cur;
-  };
-  for (uint64_t r = 0; r < n; ++r) {
-    uint32_t L = R.len[r];
-    if (L == 0) continue;
-    const uint32_t *k = R.key.data() + R.off[r];
-    int32_t dest = (int32_t)head.size();
-    head.push_back((int32_t)r);
-    tail.push_back((int32_t)r);
-    c2c.push_back(dest);
-    for (uint32_t i = 0; i < L; ++i) {  // keys sorted & unique; skip the constant key
-      uint32_t s = k[i];
-      if (s == 0) continue;
-      int32_t prev = sig2cl[s];
-      if (prev < 0) touched.push_back(s);
-      sig2cl[s] = dest;
-      if (prev >= 0) {
-        int32_t cd = findr(dest), cs = findr(prev);
-        if (cs != cd) {
-          next[tail[cd]] = head[cs];
-          tail[cd] = tail[cs];
-          head[cs] = -1;
-          c2c[cs] = cd;
-        }
-      }
-    }
-  }
-  for (uint32_t s : touched) sig2cl[s] = -1;
-  perm.clear();
-  cl_off.clear();
-  cl_off.push_back(0);
-  for (size_t slot = 0; slot < head.size(); ++slot) {
-    if (head[slot] < 0) continue;
-    for (int32_t r = head[slot]; r >= 0; r = next[r]) perm.push_back((uint32_t)r);
-    cl_off.push_back(perm.size());
-  }
-}
-
 // D2H of the keys of a ragged view (C parts)
 static void fetch_keys(rs_engine *E, const DRows &V, HostRows &H) {
   H.off.resize(V.n);
@@ -434,43 +390,120 @@ static Pool get_pool(rs_engine *E, uint64_t want) {
 
 // Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
 // the arena hold the substitutions (h_*) and leftovers (l_*), sub_of/deleted are updated.
+// build_clusters (:45-99) on the device (cluster.hpp): cluster offsets and row order in HBM, the
+// process_4 / lane split of the clusters (largest first). Only counts and the cluster offsets (for
+// the host-side round bookkeeping) come back to the host.
+struct DevClusters {
+  uint32_t *perm = nullptr, *big = nullptr, *small = nullptr;
+  uint64_t *cl_off = nullptr;
+  uint64_t n_slots = 0, n_big = 0, n_small = 0, tot_nnz = 0;
+};
+static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, ElimOut &eo) {
+  Arena &A = E->A;
+  hipStream_t st = E->st;
+  DevClusters D;
+  const uint64_t n = V.n;
+  eo.cl_off.assign(1, 0);
+  eo.n_clusters = 0;
+  D.cl_off = A.get<uint64_t>("el.cl", 1);
+  HC(hipMemsetAsync(D.cl_off, 0, 8, st));
+  if (n == 0) return D;
+  uint64_t *npairs = A.get<uint64_t>("cl.np", n);
+  unsigned long long *stat = A.get<unsigned long long>("cl.stat", 8);
+  HC(hipMemsetAsync(stat, 0, 64, st));
+  launch(st, k_cl_count, n, V, npairs, stat);
+  uint64_t *poff = A.get<uint64_t>("cl.poff", n);
+  const uint64_t P = excl_scan_u64(E, npairs, poff, n, "cl1");
+  unsigned long long hs[2];
+  HC(hipMemcpyAsync(hs, stat, 16, hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  D.tot_nnz = hs[0];
+  const uint64_t n_act = hs[1];
+  if (n_act == 0) return D;
+  int sbits = 1;
+  while (sbits < 32 && (1ull << sbits) <= E->S) ++sbits;
+  uint32_t *uf = A.get<uint32_t>("cl.uf", n);
+  launch(st, k_iota_u32, n, uf, n);
+  uint32_t *prevrow = A.get<uint32_t>("cl.prev", P);
+  if (P) {
+    uint64_t *pk = A.get<uint64_t>("cl.pk", P), *pk2 = A.get<uint64_t>("cl.pk2", P);
+    uint32_t *ps = A.get<uint32_t>("cl.ps", P), *ps2 = A.get<uint32_t>("cl.ps2", P);
+    launch(st, k_cl_fill, n, V, (const uint64_t *)poff, pk, ps);
+    sort_pairs(E, (const uint64_t *)pk, pk2, (const uint32_t *)ps, ps2, P, 32 + sbits, "cl1");
+    launch(st, k_cl_link, P, (const uint64_t *)pk2, (const uint32_t *)ps2, P, prevrow, uf);
+  }
+  int32_t *cmax = A.get<int32_t>("cl.cmax", n);
+  launch(st, k_fill_i32, n, cmax, (int32_t)-1, n);
+  launch(st, k_cl_root, n, (const uint32_t *)V.len, n, uf, cmax);
+  uint64_t *rk = A.get<uint64_t>("cl.rk", n), *rk2 = A.get<uint64_t>("cl.rk2", n);
+  uint32_t *ri = A.get<uint32_t>("cl.ri", n), *srow = A.get<uint32_t>("cl.srow", n);
+  launch(st, k_cl_key, n, (const uint32_t *)V.len, n, uf, (const int32_t *)cmax, rk, ri);
+  sort_pairs(E, (const uint64_t *)rk, rk2, (const uint32_t *)ri, srow, n, 64, "cl2");
+  uint64_t *flag = A.get<uint64_t>("cl.flag", n_act), *fscan = A.get<uint64_t>("cl.fscan", n_act);
+  launch(st, k_cl_flag, n_act, (const uint64_t *)rk2, n_act, flag);
+  const uint64_t n_cl = excl_scan_u64(E, flag, fscan, n_act, "cl2");
+  D.cl_off = A.get<uint64_t>("el.cl", n_cl + 1);
+  uint32_t *cid = A.get<uint32_t>("cl.cid", n_act), *gpos = A.get<uint32_t>("cl.gpos", n);
+  uint64_t *qn = A.get<uint64_t>("cl.qn", n_act), *q_off = A.get<uint64_t>("cl.qoff", n_act + 1);
+  launch(st, k_cl_starts, n_act, (const uint64_t *)rk2, (const uint64_t *)fscan, (const uint32_t *)srow,
+         (const uint64_t *)npairs, n_act, n_cl, D.cl_off, cid, gpos, qn);
+  const uint64_t Q = excl_scan_u64(E, qn, q_off, n_act, "cl3");
+  h2d(E, q_off + n_act, &Q, 8);
+  uint32_t *stream = A.get<uint32_t>("cl.stream", Q);
+  launch(st, k_cl_stream, n_act, (const uint32_t *)srow, (const uint64_t *)poff, (const uint32_t *)prevrow,
+         (const uint32_t *)gpos, (const uint32_t *)cid, (const uint64_t *)D.cl_off, (const uint64_t *)q_off, n_act,
+         stream);
+  // size order: (size desc, index asc)
+  uint64_t *sk = A.get<uint64_t>("cl.sk", n_cl), *sk2 = A.get<uint64_t>("cl.sk2", n_cl);
+  uint32_t *si = A.get<uint32_t>("cl.si", n_cl), *sorted = A.get<uint32_t>("el.big", n_cl);
+  unsigned long long *cnt = stat + 2;
+  launch(st, k_cl_sizekey, n_cl, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt, old_heur);
+  sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
+  unsigned long long hc[4];
+  uint64_t first = 0;
+  HC(hipMemcpyAsync(hc, cnt, 32, hipMemcpyDeviceToHost, st));
+  HC(hipMemcpyAsync(&first, sk2, 8, hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  // replay of the arena merges -> row order inside every cluster
+  D.perm = A.get<uint32_t>("el.perm", n_act);
+  uint32_t *c2c = A.get<uint32_t>("cl.c2c", n_act), *tail = A.get<uint32_t>("cl.tail", n_act);
+  uint32_t *next = A.get<uint32_t>("cl.next", n_act);
+  launch(st, k_cl_replay_lane, n_cl, (const uint64_t *)D.cl_off, n_cl, (const uint64_t *)q_off,
+         (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm);
+  if (hc[2]) {
+    hipLaunchKernelGGL(k_cl_replay_lds, dim3((unsigned)std::min<uint64_t>(hc[2], 4096)), dim3(256), 0, st,
+                       (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[2],
+                       (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm);
+    HC(hipGetLastError());
+  }
+  // elimination split: process_4 range [h, h + nb) of the size order, the rest one lane each
+  const uint64_t h = hc[0], nb = hc[1];
+  D.big = sorted + h;
+  D.n_big = nb;
+  D.n_small = n_cl - nb;
+  D.small = A.get<uint32_t>("el.small", D.n_small);
+  if (D.n_small) launch(st, k_cl_small_ids, D.n_small, (const uint32_t *)sorted, n_cl, h, nb, D.small);
+  D.n_slots = n_act;
+  eo.n_clusters = n_cl;
+  eo.cl_off.resize(n_cl + 1);
+  HC(hipMemcpyAsync(eo.cl_off.data(), D.cl_off, 8 * (n_cl + 1), hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  E->stats.n_clusters += n_cl;
+  E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, 0xffffffffull - (first >> 32));
+  return D;
+}
+
+// Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
+// the arena hold the substitutions (h_*) and leftovers (l_*), sub_of/deleted are updated.
 static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
                                       int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted) {
   double t0 = now_ms();
-  HostRows H;
-  fetch_keys(E, view, H);
-  std::vector<uint32_t> perm;
-  host_clusters(E, H, view.n, perm, eo.cl_off);
-  eo.n_clusters = eo.cl_off.size() - 1;
-  E->stats.n_clusters += eo.n_clusters;
-  for (uint64_t c = 0; c < eo.n_clusters; ++c)
-    E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, eo.cl_off[c + 1] - eo.cl_off[c]);
+  DevClusters D = gpu_clusters(E, view, old_heur, eo);
   double t1 = now_ms();
   E->stats.cluster_ms += t1 - t0;
-  uint64_t n_slots = perm.size();
-  uint32_t *d_perm = E->A.get<uint32_t>("el.perm", n_slots);
-  uint64_t *d_cl = E->A.get<uint64_t>("el.cl", eo.n_clusters + 1);
-  if (n_slots) h2d(E, d_perm, perm.data(), 4 * n_slots);
-  h2d(E, d_cl, eo.cl_off.data(), 8 * (eo.n_clusters + 1));
-  uint64_t tot_nnz = 0;
-  for (uint64_t i = 0; i < n_slots; ++i) tot_nnz += H.len[perm[i]];
-  // process_4 clusters go to the workgroup kernel; the rest, largest first, one lane each
-  std::vector<uint32_t> big, small;
-  for (uint64_t c = 0; c < eo.n_clusters; ++c) {
-    uint64_t n = eo.cl_off[c + 1] - eo.cl_off[c];
-    if (n >= 350 && n < 1000000 && !old_heur) big.push_back((uint32_t)c);
-    else small.push_back((uint32_t)c);
-  }
-  std::stable_sort(small.begin(), small.end(), [&](uint32_t x, uint32_t y) {
-    return eo.cl_off[x + 1] - eo.cl_off[x] > eo.cl_off[y + 1] - eo.cl_off[y];
-  });
-  std::stable_sort(big.begin(), big.end(), [&](uint32_t x, uint32_t y) {
-    return eo.cl_off[x + 1] - eo.cl_off[x] > eo.cl_off[y + 1] - eo.cl_off[y];
-  });
-  uint64_t n_big = big.size(), n_small = small.size();
-  uint32_t *d_big = E->A.get<uint32_t>("el.big", n_big), *d_small = E->A.get<uint32_t>("el.small", n_small);
-  h2d(E, d_big, big.data(), 4 * n_big);
-  h2d(E, d_small, small.data(), 4 * n_small);
+  const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz, n_big = D.n_big, n_small = D.n_small;
+  uint32_t *d_perm = D.perm, *d_big = D.big, *d_small = D.small;
+  uint64_t *d_cl = D.cl_off;
   uint64_t want = std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots));
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
