@@ -21,6 +21,7 @@ constexpr uint32_t kClNoPrev = 0x7fffffffu;
 constexpr uint32_t kClSmall = 64;     // clusters up to this size: one lane each
 constexpr uint32_t kClLds = 32768;    // clusters up to this size: LDS replay (u16 local ids)
 constexpr uint32_t kClChunk = 4096;   // stream entries staged per LDS chunk
+constexpr uint32_t kWaveMin = 32;     // clusters from this size on are eliminated by the workgroup kernels
 
 // pairs per row (non-constant keys) and the active-row statistics
 __global__ void k_cl_count(DRows V, uint64_t *npairs, unsigned long long *stat /* [0] nnz, [1] active */) {
@@ -195,14 +196,13 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
 
 // cluster-size classes for the elimination kernels: sorted by (size desc, index)
 __global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, uint64_t *skey, uint32_t *sidx,
-                             unsigned long long *cnt /* [0] >= 1e6, [1] process_4 range, [2] LDS replay, [3] > LDS */,
-                             int old_heur) {
+                             unsigned long long *cnt /* [0] >= 1e6, [1] workgroup kernels, [2] LDS replay, [3] > LDS */) {
   for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
     uint64_t sz = cl_off[c + 1] - cl_off[c];
     skey[c] = ((uint64_t)(0xffffffffu - (uint32_t)sz) << 32) | c;
     sidx[c] = (uint32_t)c;
     if (sz >= 1000000) atomicAdd(&cnt[0], 1ull);
-    else if (sz >= 350 && !old_heur) atomicAdd(&cnt[1], 1ull);
+    if (sz >= kWaveMin) atomicAdd(&cnt[1], 1ull);
     if (sz > kClSmall && sz <= kClLds) atomicAdd(&cnt[2], 1ull);
     if (sz > kClLds) atomicAdd(&cnt[3], 1ull);
   }

@@ -107,6 +107,7 @@ struct HostCon {  // canonical, sorted keys
 using namespace rs;
 
 struct rs_engine {
+  uint64_t pool_want = 0;  // substitution pool size (entries) that fitted last time
   int device = 0;
   hipStream_t st = nullptr;
   Arena A;
@@ -457,7 +458,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, Elim
   uint64_t *sk = A.get<uint64_t>("cl.sk", n_cl), *sk2 = A.get<uint64_t>("cl.sk2", n_cl);
   uint32_t *si = A.get<uint32_t>("cl.si", n_cl), *sorted = A.get<uint32_t>("el.big", n_cl);
   unsigned long long *cnt = stat + 2;
-  launch(st, k_cl_sizekey, n_cl, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt, old_heur);
+  launch(st, k_cl_sizekey, n_cl, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt);
   sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
   unsigned long long hc[4];
   uint64_t first = 0;
@@ -476,8 +477,10 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, Elim
                        (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm);
     HC(hipGetLastError());
   }
-  // elimination split: process_4 range [h, h + nb) of the size order, the rest one lane each
-  const uint64_t h = hc[0], nb = hc[1];
+  // elimination split: clusters of kWaveMin rows or more (a prefix of the size order) go to the
+  // workgroup kernels (process_3 or process_4 per cluster), the rest one lane each
+  (void)old_heur;
+  const uint64_t h = 0, nb = hc[1];
   D.big = sorted + h;
   D.n_big = nb;
   D.n_small = n_cl - nb;
@@ -504,7 +507,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz, n_big = D.n_big, n_small = D.n_small;
   uint32_t *d_perm = D.perm, *d_big = D.big, *d_small = D.small;
   uint64_t *d_cl = D.cl_off;
-  uint64_t want = std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots));
+  uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots)), E->pool_want);
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
     HC(hipMemsetAsync(P.top, 0, 8, E->st));
@@ -549,10 +552,12 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_big) {
-        const unsigned gb = (unsigned)std::min<uint64_t>(n_big, 8192);
+        // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
+        // per-lane pool chunks are bounded by the grid size
+        const unsigned gb = (unsigned)std::min<uint64_t>(n_big, 2048), gm = (unsigned)std::min<uint64_t>(n_big, 8192);
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
-        hipLaunchKernelGGL(k_big_main, dim3(gb), dim3(64), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
         hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
@@ -572,10 +577,17 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     if (err & 8) {
       size_t fr_ = 0, tot_ = 0;
       (void)hipMemGetInfo(&fr_, &tot_);
+      if (getenv("RS_PROF")) {
+        unsigned long long used = 0;
+        HC(hipMemcpy(&used, P.top, 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[rs-debug] pool exhausted: cap %llu entries, top %llu, attempt %d\n",
+                (unsigned long long)want, used, attempt);
+      }
       want = std::min<uint64_t>(want * 4, (uint64_t)(fr_ * 0.8) / 36 + want / 2);
       continue;
     }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
+    E->pool_want = std::max(E->pool_want, want);  // the next run starts from a size that fitted
     if (eo.n_clusters) {
       float ms = 0;
       unsigned long long by = 0;

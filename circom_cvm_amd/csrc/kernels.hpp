@@ -724,18 +724,29 @@ __global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
 //                merge whose 256-bit products are spread over the lanes.
 //   k_big_finish (256 lanes) normalize_substitutions + create_nonoverlapping_substitutions_4
 //                (:414-479) as a dependency worklist (Kahn order), emit and scratch reset.
+// full_simplification (:543-581): process_4 for 350 <= rows < 1e6 unless the old heuristics are
+// requested, process_3 otherwise.
+__device__ __forceinline__ bool d_is_p4(const ElimArgs &A, uint32_t n) {
+  return n >= 350 && n < 1000000 && !A.old_heur;
+}
+
 __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   __shared__ uint32_t s_m, s_touch, s_ok;
   __shared__ unsigned long long s_tot;
   __shared__ uint64_t s_touch_off;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   Alloc al;
-  al.chunk = 128;
+  al.chunk = 64;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     const uint32_t n = (uint32_t)(e - b);
     unsigned long long t_0 = wall_clock64();
+    if (!d_is_p4(A, n)) {  // process_3: no occurrence bookkeeping
+      for (uint32_t pos = tid; pos < n; pos += nt) A.dead[b + pos] = 0;
+      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; }
+      continue;
+    }
     uint64_t tot = 0;
     if (tid == 0) { s_m = 0; s_touch = 0; s_ok = 1; s_tot = 0; }
     for (uint32_t pos = tid; pos < n; pos += nt) tot += A.rows.len[A.perm[b + pos]];
@@ -917,12 +928,13 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
   __shared__ Fe s_c2;
   const uint32_t tid = threadIdx.x, nt = 64;
   Alloc al0;  // lane 0's allocator
-  al0.chunk = 16384;
+  al0.chunk = 4096;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     unsigned long long t_1 = wall_clock64();
     unsigned long long merges = 0, mwork = 0, rows = 0;
+    const bool p4 = d_is_p4(A, (uint32_t)(e - b));
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
     for (uint64_t idx = e; idx-- > b;) {
@@ -952,20 +964,26 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       uint32_t cur = 0;
       __syncthreads();
       while (len > 0) {
-        // take_signal_4: the first deleted key (ascending), else min occurrences, ties -> max id
+        // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
+        // -> max id.  take_signal_3 (:368-377): the max takeable key; a conflict iff it is deleted.
         if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
         __syncthreads();
         for (uint32_t i = tid; i < len; i += nt) {
           uint32_t s = wk[cur][i];
           if (A.forb[s]) continue;
+          if (!p4) { atomicMin(&s_best, 0xffffffffull - i); continue; }
           if (A.del[s]) { atomicMin(&s_fdel, i); continue; }
           int32_t o = A.occ[s];
           if (o < 0) { atomicOr(A.err, 16); o = 0; }
           atomicMin(&s_best, ((unsigned long long)(uint32_t)o << 32) | (0xffffffffu - i));  // sorted keys
         }
         __syncthreads();
-        const uint32_t fdel = s_fdel;
+        uint32_t fdel = s_fdel;
         const unsigned long long best = s_best;
+        if (!p4 && best != ~0ull) {
+          const uint32_t mi = 0xffffffffu - (uint32_t)(best & 0xffffffffu);
+          if (A.del[wk[cur][mi]]) fdel = mi;
+        }
         if (fdel == RS_NONE && best == ~0ull) {  // nothing takeable: leftover
           if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
           __syncthreads();
@@ -1125,7 +1143,7 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
   __shared__ unsigned long long s_hsum, s_hmax;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   Alloc al;
-  al.chunk = 512;
+  al.chunk = 128;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
