@@ -58,10 +58,16 @@ __device__ inline void uf_union(uint32_t *uf, uint32_t a, uint32_t b) {
     b = old;
   }
 }
-// prev(s, j) from the sorted pairs; rows sharing a signal are joined
-__global__ void k_cl_link(const uint64_t *pk, const uint32_t *ps, uint64_t P, uint32_t *prevrow, uint32_t *uf) {
+// prev(s, j) from the sorted pairs; rows sharing a signal are joined.  A row holding a non-forbidden
+// signal that no other row of the list holds is marked: process_4 consumes such rows in its uniques
+// phase, independently of their order (simplification_utils.rs:166-172).
+__global__ void k_cl_link(const uint64_t *pk, const uint32_t *ps, uint64_t P, uint32_t *prevrow, uint32_t *uf,
+                          const uint8_t *forb, uint8_t *has_unique) {
   for (uint64_t i = gtid(); i < P; i += gstride()) {
     uint64_t x = pk[i];
+    if ((i == 0 || (pk[i - 1] >> 32) != (x >> 32)) && (i + 1 == P || (pk[i + 1] >> 32) != (x >> 32)) &&
+        !forb[x >> 32])
+      has_unique[(uint32_t)x] = 1;
     if (i > 0 && (pk[i - 1] >> 32) == (x >> 32)) {
       uint32_t p = (uint32_t)pk[i - 1];
       prevrow[ps[i]] = p;
@@ -88,7 +94,8 @@ __global__ void k_cl_flag(const uint64_t *rkey, uint64_t n_act, uint64_t *flag) 
 }
 // cluster starts, cluster of each position, position of each row, pair counts in cluster order
 __global__ void k_cl_starts(const uint64_t *rkey, const uint64_t *fscan, const uint32_t *srow, const uint64_t *npairs,
-                            uint64_t n_act, uint64_t n_cl, uint64_t *cl_off, uint32_t *cid, uint32_t *gpos, uint64_t *qn) {
+                            uint64_t n_act, uint64_t n_cl, uint64_t *cl_off, uint32_t *cid, uint32_t *gpos, uint64_t *qn,
+                            const uint8_t *has_unique, uint32_t *n_ordered) {
   for (uint64_t i = gtid(); i < n_act; i += gstride()) {
     bool st = i == 0 || (rkey[i] >> 32) != (rkey[i - 1] >> 32);
     uint64_t c = fscan[i] + (st ? 1 : 0) - 1;
@@ -98,7 +105,12 @@ __global__ void k_cl_starts(const uint64_t *rkey, const uint64_t *fscan, const u
     uint32_t j = srow[i];
     gpos[j] = (uint32_t)i;
     qn[i] = npairs[j];
+    if (!has_unique[j]) atomicAdd(&n_ordered[c], 1u);  // rows whose order matters to process_4
   }
+}
+// process_4 cluster (:548-553) whose every row is consumed by the uniques phase: any order is exact
+__device__ __forceinline__ bool d_cl_order_free(uint32_t n, int old_heur, const uint32_t *n_ordered, uint64_t c) {
+  return n >= 350 && n < 1000000 && !old_heur && n_ordered[c] == 0;
 }
 // the per-cluster replay stream: local id of prev(s, j) for each pair, rows in ascending index
 __global__ void k_cl_stream(const uint32_t *srow, const uint64_t *poff, const uint32_t *prevrow, const uint32_t *gpos,
@@ -117,11 +129,16 @@ __global__ void k_cl_stream(const uint32_t *srow, const uint64_t *poff, const ui
 
 // lane replay (small clusters, and the global-memory path beyond the LDS capacity)
 __global__ void k_cl_replay_lane(const uint64_t *cl_off, uint64_t n_cl, const uint64_t *q_off, const uint32_t *stream,
-                                 const uint32_t *srow, uint32_t *c2c, uint32_t *tail, uint32_t *next, uint32_t *perm) {
+                                 const uint32_t *srow, uint32_t *c2c, uint32_t *tail, uint32_t *next, uint32_t *perm,
+                                 const uint32_t *n_ordered, int old_heur) {
   for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
     const uint64_t b = cl_off[c];
     const uint32_t n = (uint32_t)(cl_off[c + 1] - b);
     if (n > kClSmall && n <= kClLds) continue;
+    if (d_cl_order_free(n, old_heur, n_ordered, c)) {
+      for (uint32_t t = 0; t < n; ++t) perm[b + t] = srow[b + t];
+      continue;
+    }
     uint32_t *C2 = c2c + b, *T = tail + b, *N = next + b;
     for (uint32_t t = 0; t < n; ++t) {
       C2[t] = t;
@@ -145,7 +162,8 @@ __global__ void k_cl_replay_lane(const uint64_t *cl_off, uint64_t n_cl, const ui
 // workgroup replay with the union-find state in LDS (kClSmall < n <= kClLds); `ids` lists them
 __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, const uint32_t *ids, uint64_t n_ids,
                                                        const uint64_t *q_off, const uint32_t *stream,
-                                                       const uint32_t *srow, uint32_t *next, uint32_t *perm) {
+                                                       const uint32_t *srow, uint32_t *next, uint32_t *perm,
+                                                       const uint32_t *n_ordered, int old_heur) {
   __shared__ uint16_t C2[kClLds], T[kClLds];
   __shared__ uint32_t S[kClChunk];
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -153,6 +171,10 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
     const uint64_t c = ids[ci];
     const uint64_t b = cl_off[c];
     const uint32_t n = (uint32_t)(cl_off[c + 1] - b);
+    if (d_cl_order_free(n, old_heur, n_ordered, c)) {
+      for (uint32_t i = tid; i < n; i += nt) perm[b + i] = srow[b + i];
+      continue;
+    }
     const uint64_t q0 = q_off[b], q1 = q_off[b + n];
     uint32_t *N = next + b;
     int32_t t = -1;  // lane 0: current row

@@ -399,7 +399,7 @@ struct DevClusters {
   uint64_t *cl_off = nullptr;
   uint64_t n_slots = 0, n_big = 0, n_small = 0, tot_nnz = 0;
 };
-static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, ElimOut &eo) {
+static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, const uint8_t *d_forb, ElimOut &eo) {
   Arena &A = E->A;
   hipStream_t st = E->st;
   DevClusters D;
@@ -426,12 +426,14 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, Elim
   uint32_t *uf = A.get<uint32_t>("cl.uf", n);
   launch(st, k_iota_u32, n, uf, n);
   uint32_t *prevrow = A.get<uint32_t>("cl.prev", P);
+  uint8_t *has_unique = A.get<uint8_t>("cl.uniq", n);
+  HC(hipMemsetAsync(has_unique, 0, n, st));
   if (P) {
     uint64_t *pk = A.get<uint64_t>("cl.pk", P), *pk2 = A.get<uint64_t>("cl.pk2", P);
     uint32_t *ps = A.get<uint32_t>("cl.ps", P), *ps2 = A.get<uint32_t>("cl.ps2", P);
     launch(st, k_cl_fill, n, V, (const uint64_t *)poff, pk, ps);
     sort_pairs(E, (const uint64_t *)pk, pk2, (const uint32_t *)ps, ps2, P, 32 + sbits, "cl1");
-    launch(st, k_cl_link, P, (const uint64_t *)pk2, (const uint32_t *)ps2, P, prevrow, uf);
+    launch(st, k_cl_link, P, (const uint64_t *)pk2, (const uint32_t *)ps2, P, prevrow, uf, d_forb, has_unique);
   }
   int32_t *cmax = A.get<int32_t>("cl.cmax", n);
   launch(st, k_fill_i32, n, cmax, (int32_t)-1, n);
@@ -446,8 +448,10 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, Elim
   D.cl_off = A.get<uint64_t>("el.cl", n_cl + 1);
   uint32_t *cid = A.get<uint32_t>("cl.cid", n_act), *gpos = A.get<uint32_t>("cl.gpos", n);
   uint64_t *qn = A.get<uint64_t>("cl.qn", n_act), *q_off = A.get<uint64_t>("cl.qoff", n_act + 1);
+  uint32_t *n_ordered = A.get<uint32_t>("cl.nord", n_cl);
+  HC(hipMemsetAsync(n_ordered, 0, 4 * n_cl, st));
   launch(st, k_cl_starts, n_act, (const uint64_t *)rk2, (const uint64_t *)fscan, (const uint32_t *)srow,
-         (const uint64_t *)npairs, n_act, n_cl, D.cl_off, cid, gpos, qn);
+         (const uint64_t *)npairs, n_act, n_cl, D.cl_off, cid, gpos, qn, (const uint8_t *)has_unique, n_ordered);
   const uint64_t Q = excl_scan_u64(E, qn, q_off, n_act, "cl3");
   h2d(E, q_off + n_act, &Q, 8);
   uint32_t *stream = A.get<uint32_t>("cl.stream", Q);
@@ -470,16 +474,17 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, Elim
   uint32_t *c2c = A.get<uint32_t>("cl.c2c", n_act), *tail = A.get<uint32_t>("cl.tail", n_act);
   uint32_t *next = A.get<uint32_t>("cl.next", n_act);
   launch(st, k_cl_replay_lane, n_cl, (const uint64_t *)D.cl_off, n_cl, (const uint64_t *)q_off,
-         (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm);
+         (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm, (const uint32_t *)n_ordered,
+         old_heur);
   if (hc[2]) {
     hipLaunchKernelGGL(k_cl_replay_lds, dim3((unsigned)std::min<uint64_t>(hc[2], 4096)), dim3(256), 0, st,
                        (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[2],
-                       (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm);
+                       (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
+                       (const uint32_t *)n_ordered, old_heur);
     HC(hipGetLastError());
   }
   // elimination split: clusters of kWaveMin rows or more (a prefix of the size order) go to the
   // workgroup kernels (process_3 or process_4 per cluster), the rest one lane each
-  (void)old_heur;
   const uint64_t h = 0, nb = hc[1];
   D.big = sorted + h;
   D.n_big = nb;
@@ -501,7 +506,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, Elim
 static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
                                       int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted) {
   double t0 = now_ms();
-  DevClusters D = gpu_clusters(E, view, old_heur, eo);
+  DevClusters D = gpu_clusters(E, view, old_heur, d_forb, eo);
   double t1 = now_ms();
   E->stats.cluster_ms += t1 - t0;
   const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz, n_big = D.n_big, n_small = D.n_small;
