@@ -37,6 +37,24 @@ def cpu_baseline(rows: int, seed: int, threads: int):
                       f"simplification() only, {ms / 1000.0:.1f} s ({wall:.1f} s incl. load)"}
 
 
+def shard_seed(seed: int, rank: int) -> int:
+    """Rank r simplifies its own circuit shard: the synthetic generator seeded with seed + r."""
+    return seed + rank
+
+
+def reduce_over_ranks(dist, dt: float, n_rows: int, device):
+    """(max over ranks of the timed region, total constraints over ranks); identity without dist."""
+    if dist is None:
+        return dt, n_rows
+    import torch
+    t = torch.tensor([dt, float(n_rows)], device=device, dtype=torch.float64)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = t.clone()
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return float(mx[0]), int(sm[1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,7 +82,7 @@ def main():
     import circom_cvm_amd as M
 
     # each rank: its own shard of instances (seed + rank), staged in HBM once
-    inp = M.Input.synth(0, args.rows, args.seed + rank, args.prime)
+    inp = M.Input.synth(0, args.rows, shard_seed(args.seed, rank), args.prime)
     n_rows = inp.rows()
     eng = M.Engine(local)
     eng.load(inp.c)
@@ -93,16 +111,7 @@ def main():
         apply_launches += st.apply_kernel_launches
     barrier()
     dt = time.perf_counter() - t0
-    total_rows = n_rows
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt, float(n_rows)], device="cuda", dtype=torch.float64)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        dt = float(mx[0])
-        total_rows = int(sm[1])
+    dt, total_rows = reduce_over_ranks(dist, dt, n_rows, "cuda")
     last = eng.stats()
     if rank == 0:
         ms_step = dt * 1000.0 / args.steps

@@ -1,0 +1,192 @@
+"""CPU tests of the drop-in boundary (include/rs_simplify.h, librs_simplify.so): the library loads,
+exports exactly what the header declares, refuses to compute without a gfx950 GPU (no CPU fallback),
+and its host-side pieces -- .r1cs reader/classifier, .r1cs/.sym writers, synthetic generator -- agree
+with the oracle byte for byte.  No GPU compute is called here."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import rsio
+import circom_cvm_amd as M
+from circom_cvm_amd import abi
+
+R = rsio.R
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "rs_simplify.h")
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _header_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(rs_\w+)\s*\(", txt, flags=re.M)))
+
+
+def _gpu_present():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def test_library_exports_every_header_symbol():
+    L = abi.lib()
+    declared = _header_functions()
+    assert declared, "no declarations parsed"
+    for name in declared:
+        assert hasattr(L, name), f"{name} declared in rs_simplify.h but not exported"
+    assert sorted(n for n, _, _ in abi.SYMBOLS) == declared
+
+
+def test_abi_version_matches_header():
+    v = int(re.search(r"#define RS_ABI_VERSION (\d+)", open(HDR).read()).group(1))
+    assert abi.lib().rs_abi_version() == v
+
+
+def test_status_codes_match_header():
+    txt = open(HDR).read()
+    for code, name in abi.ERRORS.items():
+        if code:
+            assert re.search(rf"{name}\s*=\s*{code}\b", txt), name
+
+
+@pytest.mark.skipif(_gpu_present(), reason="checks the no-device path")
+def test_no_cpu_fallback():
+    """Without a gfx950 device every compute entry point fails loudly (RS_E_NODEVICE)."""
+    L = abi.lib()
+    h = C.c_void_p()
+    rc = L.rs_engine_create(0, C.byref(h))
+    assert rc == -6, rc
+    assert b"gfx950" in L.rs_last_error() or b"device" in L.rs_last_error().lower()
+    sys_ = R.System(257, 3, 1, 0, 1, {0, 1}, [R.Con({}, {}, {1: 1, 2: 256})])
+    inp = rsio.InputHolder(sys_)
+    out = C.POINTER(abi.RsOutput)()
+    rc = L.rs_simplify(C.byref(inp.inp), C.byref(rsio.flags("O2")), C.byref(out))
+    assert rc == -6 and not out
+
+
+def test_synth_is_seeded_and_host_side():
+    a = M.Input.synth(0, 20000, 7)
+    b = M.Input.synth(0, 20000, 7)
+    c = M.Input.synth(0, 20000, 8)
+
+    def digest(inp):
+        x = inp.c
+        parts = []
+        for blk in (x.cons_eq, x.eq, x.linear, x.nl_a, x.nl_b, x.nl_c):
+            n = int(blk.n_rows)
+            ptr = np.ctypeslib.as_array(blk.ptr, shape=(n + 1,)).copy()
+            nnz = int(ptr[-1])
+            parts += [ptr.tobytes(), np.ctypeslib.as_array(blk.col, shape=(max(nnz, 1),))[:nnz].tobytes(),
+                      np.ctypeslib.as_array(blk.val, shape=(max(nnz, 1) * 4,))[:4 * nnz].tobytes()]
+        return hash(b"".join(parts))
+
+    assert a.rows() >= 20000
+    assert digest(a) == digest(b) != digest(c)
+
+
+def test_synth_rows_are_clean_and_classified():
+    """Generator rows obey the input contract (sorted distinct columns, no zero, canonical) and land
+    in the block map_tree would put them in (dag/src/map_to_constraint_list.rs:12-44)."""
+    inp = M.Input.synth(0, 5000, 3, "bn128")
+    x = inp.c
+    p = R.PRIMES["bn128"]
+
+    def rows(blk):
+        return rsio._read_block(blk)
+
+    for blk in (x.cons_eq, x.eq, x.linear, x.nl_a, x.nl_b, x.nl_c):
+        for m in rows(blk):
+            assert all(0 < v < p for v in m.values())
+    for m in rows(x.cons_eq):
+        assert R.is_constant_equality(R.Con({}, {}, m))
+    for m in rows(x.eq):
+        assert R.is_equality(R.Con({}, {}, m), p)
+    for m in rows(x.linear):
+        c = R.Con({}, {}, m)
+        assert not R.is_constant_equality(c) and not R.is_equality(c, p)
+    na, nb = rows(x.nl_a), rows(x.nl_b)
+    assert len(na) == len(nb) == x.nl_c.n_rows
+    assert all(a and b for a, b in zip(na, nb))
+
+
+def _write(tmp, name, data):
+    path = os.path.join(tmp, name)
+    with open(path, "wb" if isinstance(data, bytes) else "w") as f:
+        f.write(data)
+    return path
+
+
+def test_r1cs_reader_classifies_like_map_tree():
+    sys_ = rsio.gen_system(31, R.PRIMES["bn128"], n_sig=60, n_rows=120)
+    ident = R.Result(sys_.rows, {i: i for i in range(sys_.max_signal)}, sys_.n_priv_in)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = _write(tmp, "in.r1cs", R.result_to_r1cs(sys_, ident))
+        inp = M.Input.read_r1cs(path)
+        x = inp.c
+        ce, eq, lin, nl = R.classify(sys_)
+        assert rsio._read_block(x.cons_eq) == [c.c for c in ce]
+        assert rsio._read_block(x.eq) == [c.c for c in eq]
+        assert rsio._read_block(x.linear) == [c.c for c in lin]
+        assert rsio._read_block(x.nl_a) == [c.a for c in nl]
+        assert rsio._read_block(x.nl_b) == [c.b for c in nl]
+        assert rsio._read_block(x.nl_c) == [c.c for c in nl]
+        forb = np.ctypeslib.as_array(x.forbidden, shape=(x.n_forbidden,)).tolist()
+        assert forb == sorted(sys_.forbidden)
+        assert (x.max_signal, x.n_pub_out, x.n_pub_in, x.n_priv_in) == (
+            sys_.max_signal, sys_.n_pub_out, sys_.n_pub_in, sys_.n_priv_in)
+
+
+@pytest.mark.parametrize("level", ["O1", "O2"])
+def test_writers_match_oracle_bytes(level):
+    """rs_write_r1cs / rs_write_sym (product) on the oracle's simplification result == the oracle's
+    own byte writer (r1cs_porting.rs:4-124, sym_porting.rs:5-37), for the docs circuit."""
+    with tempfile.TemporaryDirectory() as tmp:
+        inp = M.Input.read_r1cs(os.path.join(GOLD, "docs_basic_O0.r1cs"))
+        lib = rsio.oracle_lib()
+        out = C.POINTER(abi.RsOutput)()
+        ms, rounds = C.c_double(), C.c_uint64()
+        assert lib.refcpu_simplify(C.byref(inp.c), C.byref(rsio.flags(level)), 1, C.byref(out),
+                                   C.byref(ms), C.byref(rounds)) == 0
+        try:
+            r1 = os.path.join(tmp, "o.r1cs")
+            sy = os.path.join(tmp, "o.sym")
+            abi.check(abi.lib().rs_write_r1cs(r1.encode(), C.byref(inp.c), out))
+            abi.check(abi.lib().rs_write_sym(os.path.join(GOLD, "docs_basic_O0.sym").encode(), sy.encode(), out))
+        finally:
+            lib.refcpu_output_free(out)
+        assert open(r1, "rb").read() == open(os.path.join(GOLD, f"docs_basic_{level}.r1cs"), "rb").read()
+        assert open(sy).read() == open(os.path.join(GOLD, f"docs_basic_{level}.sym")).read()
+
+
+def test_writer_key_order_random():
+    """LE-byte key order of the r1cs writer (r1cs_writer.rs:49-72) on rows with many signals > 255."""
+    sys_ = rsio.gen_system(41, R.PRIMES["bls12381"], n_sig=700, n_rows=300, density=3.0)
+    h = rsio.InputHolder(sys_, "bls12381")
+    (cons, sm, nw, npiw), _, _ = rsio.oracle_run(h.inp, rsio.flags("O2"), 2)
+    res = R.Result(cons, sm, npiw)
+    lib = rsio.oracle_lib()
+    out = C.POINTER(abi.RsOutput)()
+    ms, rounds = C.c_double(), C.c_uint64()
+    assert lib.refcpu_simplify(C.byref(h.inp), C.byref(rsio.flags("O2")), 1, C.byref(out), C.byref(ms),
+                               C.byref(rounds)) == 0
+    with tempfile.TemporaryDirectory() as tmp:
+        r1 = os.path.join(tmp, "o.r1cs")
+        try:
+            abi.check(abi.lib().rs_write_r1cs(r1.encode(), C.byref(h.inp), out))
+        finally:
+            lib.refcpu_output_free(out)
+        assert open(r1, "rb").read() == R.result_to_r1cs(sys_, res)
+
+
+def test_cli_usage():
+    exe = os.path.join(ROOT, "circom_cvm_amd", "circom-simplify")
+    assert os.path.exists(exe)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 2 and "usage" in r.stderr
