@@ -225,3 +225,52 @@ def gen_system(seed: int, p: int, n_sig: int = 60, n_rows: int = 80, n_out: int 
                 rows.append(R.Con({}, {}, m))
     forb = {0} | set(range(1, n_out + n_pub + 1))
     return R.System(p, S, n_out, n_pub, n_priv, forb, rows)
+
+
+# --------------------------------------------------------------------------- array comparison
+def _lc_arrays(b: RsLc):
+    n = int(b.n_rows)
+    if n == 0:
+        return np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint64)
+    ptr = np.ctypeslib.as_array(b.ptr, shape=(n + 1,)).copy()
+    nnz = int(ptr[n])
+    col = np.ctypeslib.as_array(b.col, shape=(max(nnz, 1),))[:nnz].copy()
+    val = np.ctypeslib.as_array(b.val, shape=(max(nnz, 1) * 4,))[:4 * nnz].copy()
+    return ptr, col, val
+
+
+def output_arrays(o: RsOutput):
+    """All arrays of an rs_output, copied (numpy): for size-independent comparisons at full size."""
+    d = {"n_constraints": int(o.n_constraints), "n_wires": int(o.n_wires),
+         "npiw": int(o.no_private_inputs_witness), "n_labels": int(o.n_labels)}
+    for nm in ("a", "b", "c"):
+        d[nm] = _lc_arrays(getattr(o, nm))
+    d["l2w"] = np.ctypeslib.as_array(o.label_to_wire, shape=(max(int(o.n_labels), 1),))[: int(o.n_labels)].copy()
+    return d
+
+
+def diff_output_arrays(x, y) -> str | None:
+    for k in ("n_constraints", "n_wires", "npiw", "n_labels"):
+        if x[k] != y[k]:
+            return f"{k}: {x[k]} vs {y[k]}"
+    if not np.array_equal(x["l2w"], y["l2w"]):
+        return f"label_to_wire differs at {int(np.argmax(x['l2w'] != y['l2w']))}"
+    for nm in ("a", "b", "c"):
+        for i, part in enumerate(("ptr", "col", "val")):
+            if not np.array_equal(x[nm][i], y[nm][i]):
+                return f"{nm}.{part} differs"
+    return None
+
+
+def oracle_arrays(inp: RsInput, fl: RsFlags, threads=1):
+    lib = oracle_lib()
+    out = C.POINTER(RsOutput)()
+    ms = C.c_double()
+    rounds = C.c_uint64()
+    rc = lib.refcpu_simplify(C.byref(inp), C.byref(fl), threads, C.byref(out), C.byref(ms), C.byref(rounds))
+    if rc != 0:
+        raise RuntimeError(f"refcpu rc={rc}: {lib.refcpu_last_error().decode()}")
+    try:
+        return output_arrays(out.contents), ms.value
+    finally:
+        lib.refcpu_output_free(out)
