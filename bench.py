@@ -23,18 +23,21 @@ METRIC = "constraints simplified/sec (--O2) on 10M-constraint circuit; bit-exact
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(rows: int, seed: int, threads: int):
+def cpu_baseline(rows: int, seed: int, threads: int, prime: str):
+    """The canonical CPU oracle (oracle/refcpu.cpp) on the same synthetic circuit as rank 0 (or a
+    smaller bounded sample when --cpu-rows is lower), on `threads` host threads."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import rsio
     import circom_cvm_amd as M
-    inp = M.Input.synth(0, rows, seed)
+    inp = M.Input.synth(0, rows, seed, prime)
     t0 = time.time()
-    _, ms, _ = rsio.oracle_run(inp.c, rsio.flags("O2"), threads=threads)
+    _, ms = rsio.oracle_arrays(inp.c, rsio.flags("O2"), threads=threads)
     wall = time.time() - t0
     return {"value": round(inp.rows() / (ms / 1000.0), 1), "unit": "constraints/s", "cores": threads,
             "kind": "port",
-            "sample": f"synth_mixed rows={inp.rows()} seed={seed} bn128 --O2, oracle/refcpu.cpp "
-                      f"simplification() only, {ms / 1000.0:.1f} s ({wall:.1f} s incl. load)"}
+            "sample": f"synth_mixed rows={inp.rows()} seed={seed} {prime} --O2 (the rank-0 workload), "
+                      f"oracle/refcpu.cpp simplification() on {threads} threads: {ms / 1000.0:.1f} s "
+                      f"({wall:.1f} s incl. output copy)"}
 
 
 def shard_seed(seed: int, rank: int) -> int:
@@ -63,7 +66,7 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--prime", default="bn128")
-    ap.add_argument("--cpu-rows", type=int, default=3_000_000)
+    ap.add_argument("--cpu-rows", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -97,18 +100,19 @@ def main():
             dist.barrier()
 
     barrier()
-    elim_ms = elim_bytes = apply_ms = apply_bytes = 0.0
-    elim_launches = apply_launches = 0
+    # device time + algorithmic bytes per kernel over the timed region (HIP events recorded by the
+    # library on its own stream around each launch; bytes counted in-kernel, SURVEY 8(d) B_alg terms)
+    K = {"k_big_main": [0.0, 0, 0], "k_big_finish": [0.0, 0, 0], "k_nl_fill": [0.0, 0, 0]}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.run(fl)  # synchronous: returns after its stream has drained
         st = eng.stats()
-        elim_ms += st.elim_kernel_ms
-        elim_bytes += st.elim_bytes
-        elim_launches += st.elim_kernel_launches
-        apply_ms += st.apply_kernel_ms
-        apply_bytes += st.apply_bytes
-        apply_launches += st.apply_kernel_launches
+        for k, ms, by, n in (("k_big_main", st.big_main_ms, st.big_main_bytes, st.big_launches),
+                             ("k_big_finish", st.big_finish_ms, st.big_finish_bytes, st.big_launches),
+                             ("k_nl_fill", st.apply_kernel_ms, st.apply_bytes, st.apply_kernel_launches)):
+            K[k][0] += ms
+            K[k][1] += by
+            K[k][2] += n
     barrier()
     dt = time.perf_counter() - t0
     dt, total_rows = reduce_over_ranks(dist, dt, n_rows, "cuda")
@@ -116,11 +120,9 @@ def main():
     if rank == 0:
         ms_step = dt * 1000.0 / args.steps
         value = total_rows * args.steps / dt
-        # dominant kernel: the one with the larger device time over the timed region
-        if elim_ms >= apply_ms:
-            k_name, k_ms, k_bytes, k_launch = "k_eliminate", elim_ms, elim_bytes, elim_launches
-        else:
-            k_name, k_ms, k_bytes, k_launch = "k_nl_fill", apply_ms, apply_bytes, apply_launches
+        # dominant kernel: the largest device time over the timed region
+        k_name = max(K, key=lambda k: K[k][0])
+        k_ms, k_bytes, k_launch = K[k_name]
         per_launch_s = (k_ms / 1000.0) / max(k_launch, 1)
         per_launch_bytes = k_bytes / max(k_launch, 1)
         achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
@@ -141,11 +143,13 @@ def main():
                          "traffic": traffic, "launches_per_step": k_launch / args.steps,
                          "avg_launch_ms": round(per_launch_s * 1000.0, 4),
                          "alg_bytes_per_launch": int(per_launch_bytes)},
+            "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in K.items()},
             "phases_ms": {k: round(getattr(last, k), 2) for k in
                           ("total_ms", "eq_ms", "cluster_ms", "elim_ms", "subst_ms", "final_ms")},
         }
         if not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed, args.cpu_threads)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_rows, shard_seed(args.seed, 0), args.cpu_threads,
+                                                args.prime)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

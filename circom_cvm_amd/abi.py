@@ -52,6 +52,8 @@ class RsStats(C.Structure):
                 ("elim_kernel_launches", C.c_uint64), ("elim_bytes", C.c_uint64),
                 ("elim_big_ms", C.c_double), ("elim_small_ms", C.c_double), ("nl_ms", C.c_double),
                 ("map_ms", C.c_double), ("rounds_ms", C.c_double),
+                ("big_prep_ms", C.c_double), ("big_main_ms", C.c_double), ("big_finish_ms", C.c_double),
+                ("big_main_bytes", C.c_uint64), ("big_finish_bytes", C.c_uint64), ("big_launches", C.c_uint64),
                 ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
                 ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
 

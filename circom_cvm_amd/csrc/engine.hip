@@ -131,7 +131,7 @@ struct rs_engine {
   std::vector<HostCon> out_host_tail;  // lconst rows appended after the device rows
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr, ev6 = nullptr;
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
@@ -549,11 +549,13 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.pool_top = P.top;
     a.pool_cap = P.cap;
     a.err = d_err;
-    a.bytes = E->A.get<unsigned long long>("el.bytes", 1);
+    a.bytes = E->A.get<unsigned long long>("el.bytes", 3);
     a.big_touch_off = E->A.get<uint64_t>("el.bt_off", std::max<uint64_t>(n_big, 1));
     a.big_touch_n = E->A.get<uint32_t>("el.bt_n", std::max<uint64_t>(n_big, 1));
     a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", 16 * n_big) : nullptr;
-    HC(hipMemsetAsync(a.bytes, 0, 8, E->st));
+    a.bytes_main = a.bytes + 1;
+    a.bytes_fin = a.bytes + 2;
+    HC(hipMemsetAsync(a.bytes, 0, 24, E->st));
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_big) {
@@ -562,8 +564,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         const unsigned gb = (unsigned)std::min<uint64_t>(n_big, 2048), gm = (unsigned)std::min<uint64_t>(n_big, 8192);
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
+        HC(hipEventRecord(E->ev5, E->st));
         hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
+        HC(hipEventRecord(E->ev6, E->st));
         hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
       }
@@ -601,10 +605,24 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipEventElapsedTime(&mb, E->ev2, E->ev4));
       E->stats.elim_big_ms += mb;
       E->stats.elim_small_ms += ms - mb;
-      HC(hipMemcpy(&by, a.bytes, 8, hipMemcpyDeviceToHost));
+      unsigned long long b3[3] = {0, 0, 0};
+      HC(hipMemcpy(b3, a.bytes, 24, hipMemcpyDeviceToHost));
+      by = b3[0];
       E->stats.elim_kernel_ms += ms;
       E->stats.elim_kernel_launches++;
       E->stats.elim_bytes += by;
+      if (n_big) {
+        float m0 = 0, m1 = 0, m2 = 0;
+        HC(hipEventElapsedTime(&m0, E->ev2, E->ev5));
+        HC(hipEventElapsedTime(&m1, E->ev5, E->ev6));
+        HC(hipEventElapsedTime(&m2, E->ev6, E->ev4));
+        E->stats.big_prep_ms += m0;
+        E->stats.big_main_ms += m1;
+        E->stats.big_finish_ms += m2;
+        E->stats.big_main_bytes += b3[1];
+        E->stats.big_finish_bytes += b3[2];
+        E->stats.big_launches++;
+      }
     }
     if (a.prof) {
       std::vector<unsigned long long> pf(16 * n_big);
@@ -1530,6 +1548,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipEventCreate(&E->ev2));
     HC(hipEventCreate(&E->ev3));
     HC(hipEventCreate(&E->ev4));
+    HC(hipEventCreate(&E->ev5));
+    HC(hipEventCreate(&E->ev6));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {
@@ -1550,6 +1570,8 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->ev2) (void)hipEventDestroy(E->ev2);
   if (E->ev3) (void)hipEventDestroy(E->ev3);
   if (E->ev4) (void)hipEventDestroy(E->ev4);
+  if (E->ev5) (void)hipEventDestroy(E->ev5);
+  if (E->ev6) (void)hipEventDestroy(E->ev6);
   if (E->heap_k) (void)hipFree(E->heap_k);
   if (E->heap_v) (void)hipFree(E->heap_v);
   if (E->st) (void)hipStreamDestroy(E->st);

@@ -300,6 +300,7 @@ struct ElimArgs {
   uint64_t pool_cap;
   int *err;
   unsigned long long *bytes;  // algorithmic bytes (SURVEY 8(d) B_alg terms of this kernel)
+  unsigned long long *bytes_main, *bytes_fin;  // the same, for k_big_main and k_big_finish
   unsigned long long *prof;   // debug: 16 words per big cluster (see run_linear_simplification), or null
   uint64_t *big_touch_off;    // per big cluster: touched-signal list in the pool (k_big_prep)
   uint32_t *big_touch_n;
@@ -933,7 +934,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     unsigned long long t_1 = wall_clock64();
-    unsigned long long merges = 0, mwork = 0, rows = 0;
+    unsigned long long merges = 0, mwork = 0, rows = 0, by = 0;  // by: algorithmic bytes (lane 0)
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
@@ -945,6 +946,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       const uint32_t *k = A.rows.key + A.rows.off[r];
       const Fe *v = A.rows.val + A.rows.off[r];
       uint32_t len = A.rows.len[r];
+      by += 36ull * len;
       for (uint32_t i = tid; i < len; i += nt) {  // remove_constraint (keys of a row are distinct)
         uint32_t s = k[i];
         if (!A.forb[s] && A.occ[s] >= 0) A.occ[s]--;
@@ -987,6 +989,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         if (fdel == RS_NONE && best == ~0ull) {  // nothing takeable: leftover
           if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
           __syncthreads();
+          by += 36ull * len;
           if (s_ok) {
             const uint64_t o = s_o;
             for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
@@ -1000,6 +1003,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         if (fdel == RS_NONE) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
           const uint32_t sh = wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
           const uint32_t mm = len - 1 + sh;
+          by += 36ull * mm;
           if (tid == 0) { s_o = pool_alloc(A, al0, mm); if (s_o == RS_NONE) s_ok = 0; }
           __syncthreads();
           if (s_ok) {
@@ -1098,12 +1102,14 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         }
         __syncthreads();
         cur = nx;
+        by += 36ull * (len + rl + tw + tr);
         len = tw + tr;
       }
     }
     if (tid == 0) {
       A.n_sub[c] = s_m;
       A.n_left[c] = s_nl;
+      atomicAdd(A.bytes_main, by);
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
         unsigned long long *P = A.prof + 16 * ci;
@@ -1150,6 +1156,7 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
     const uint32_t n = (uint32_t)(e - b);
     const uint32_t m = A.n_sub[c];
     unsigned long long t_2 = wall_clock64();
+    unsigned long long by = 0;  // algorithmic bytes of this lane
     if (tid == 0) s_ok = 1;
     // ---- normalize_substitutions: each lane batch-inverts the slots i = tid (mod nt)
     if (tid < m) {
@@ -1163,6 +1170,7 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
         inv = fmul(F, inv, A.h_coef[b + i]);
         Fe *vv = A.pv + A.h_off[b + i];
         for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
+        by += 64ull * (A.h_len[b + i] + 1);
         if (i < tid + nt) break;
       }
     }
@@ -1252,6 +1260,7 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
             }
             A.h_off[b + i] = off;
             A.h_len[b + i] = len;
+            by += 36ull * (bound + len);
           }
           done += nf;
           ++levels;
@@ -1278,6 +1287,7 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
     for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
     for (uint32_t i = tid; i < m; i += nt) { subs_e += A.h_len[b + i]; hmax = max(hmax, A.h_len[b + i]); }
     atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0)));
+    if (by) atomicAdd(A.bytes_fin, by);
     if (A.prof) {
       if (tid == 0) { s_hsum = 0; s_hmax = 0; }
       __syncthreads();

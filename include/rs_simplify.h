@@ -136,6 +136,12 @@ typedef struct rs_stats {
   double nl_ms;                /* non-linear frames (count, scan, fill, split)               */
   double map_ms;               /* host copy of the non-linear signal map (rounds >= 2)       */
   double rounds_ms;            /* storage updates + bookkeeping of rounds >= 2               */
+  double big_prep_ms;          /* k_big_prep   (occurrences + uniques of the workgroup clusters) */
+  double big_main_ms;          /* k_big_main   (ordered elimination loop)                     */
+  double big_finish_ms;        /* k_big_finish (normalisation + composition)                 */
+  uint64_t big_main_bytes;     /* algorithmic bytes of k_big_main (sum over launches)        */
+  uint64_t big_finish_bytes;   /* algorithmic bytes of k_big_finish (sum over launches)      */
+  uint64_t big_launches;       /* launches of each of the three workgroup kernels            */
   uint64_t rounds;             /* linear-elimination rounds executed                         */
   uint64_t n_clusters;
   uint64_t n_substitutions;
