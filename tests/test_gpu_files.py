@@ -94,3 +94,19 @@ def test_golden_on_gpu(fname):
                 k: ex[k] for k in ("constraints", "signal_map", "no_private_inputs_witness")}
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("level", ["O1", "O2"])
+def test_simplifier_mirror_docs(level):
+    """Simplifier(...).simplify_constraints() -> ConstraintList, like constraint_list/src/lib.rs:131-202:
+    json_constraints, r1cs and sym reproduce the reference docs' basic.circom outputs."""
+    inp = M.Input.read_r1cs(os.path.join(GOLD, "docs_basic_O0.r1cs"))
+    smp = M.Simplifier(inp, flag_s=(level == "O1"))
+    cl = smp.simplify_constraints()
+    assert cl.json_constraints() == G.DOCS["constraints"][level]
+    with tempfile.TemporaryDirectory() as tmp:
+        cl.r1cs(os.path.join(tmp, "o.r1cs"))
+        cl.sym(os.path.join(GOLD, "docs_basic_O0.sym"), os.path.join(tmp, "o.sym"))
+        assert open(os.path.join(tmp, "o.r1cs"), "rb").read() == open(os.path.join(GOLD, f"docs_basic_{level}.r1cs"), "rb").read()
+        assert open(os.path.join(tmp, "o.sym")).read().splitlines() == G.DOCS["sym"][level]
+    assert cl.no_wires() == len(cl.get_witness_as_vec())
