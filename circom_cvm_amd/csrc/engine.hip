@@ -562,13 +562,18 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
         // per-lane pool chunks are bounded by the grid size
         const unsigned gb = (unsigned)std::min<uint64_t>(n_big, 2048), gm = (unsigned)std::min<uint64_t>(n_big, 8192);
+        // experiment knobs: dynamic LDS to limit co-resident workgroups per CU
+        const char *xm = getenv("RS_XM"), *xf = getenv("RS_XF"), *gmm = getenv("RS_GM"), *gfb = getenv("RS_GF");
+        const unsigned lm = xm ? (unsigned)atoi(xm) : 0, lf = xf ? (unsigned)atoi(xf) : 0;
+        const unsigned gm2 = gmm ? (unsigned)std::min<uint64_t>(n_big, atoi(gmm)) : gm;
+        const unsigned gf2 = gfb ? (unsigned)std::min<uint64_t>(n_big, atoi(gfb)) : gb;
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev5, E->st));
-        hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        hipLaunchKernelGGL(k_big_main, dim3(gm2), dim3(64), lm, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev6, E->st));
-        hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        hipLaunchKernelGGL(k_big_finish, dim3(gf2), dim3(256), lf, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
         HC(hipGetLastError());
       }
       HC(hipEventRecord(E->ev4, E->st));
@@ -646,8 +651,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 8); ++q) {
         unsigned long long *p = &pf[16 * ix[q]];
         fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu iters=%llu  %.1f / %.1f / %.1f / %.1f  merges=%llu mwork=%llu "
-                "rhs_sum=%llu rhs_max=%llu touched=%llu\n", p[0], p[1], p[2], p[3],
-                p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0, p[8], p[9], p[10], p[11], p[12]);
+                "rhs_sum=%llu rhs_max=%llu touched=%llu | pivot %.1f hold+stage %.1f merge %.1f us\n", p[0], p[1], p[2], p[3],
+                p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0, p[8], p[9], p[10], p[11], p[12],
+                p[13] / 100.0, p[14] / 100.0, p[15] / 100.0);
       }
     }
     eo.n_sub.resize(eo.n_clusters);

@@ -935,6 +935,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     unsigned long long t_1 = wall_clock64();
     unsigned long long merges = 0, mwork = 0, rows = 0, by = 0;  // by: algorithmic bytes (lane 0)
+    unsigned long long tp_piv = 0, tp_hold = 0, tp_merge = 0, tp_x;  // debug phase clocks (A.prof)
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
@@ -966,6 +967,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       uint32_t cur = 0;
       __syncthreads();
       while (len > 0) {
+        tp_x = wall_clock64();
         // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
         // -> max id.  take_signal_3 (:368-377): the max takeable key; a conflict iff it is deleted.
         if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
@@ -1030,6 +1032,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           __syncthreads();
           break;
         }
+        { unsigned long long t = wall_clock64(); tp_piv += t - tp_x; tp_x = t; }
         // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p)
         if (tid == 0) {
           int32_t hs = A.holder_idx[p];
@@ -1059,28 +1062,33 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           __syncthreads();
           break;
         }
+        { unsigned long long t = wall_clock64(); tp_hold += t - tp_x; tp_x = t; }
         const Fe c2 = s_c2;
         const Fe coef = fneg(F, wv[cur][oi]);
         for (uint32_t j = tid; j < rl; j += nt) { rk[j] = A.pk[roff + j]; rv[j] = A.pv[roff + j]; }
         __syncthreads();
-        for (uint32_t i = tid; i < len; i += nt) {
+        // one product per entry, all lanes at once: work entries c2*v, RHS entries coef*rv
+        for (uint32_t q = tid; q < len + rl; q += nt) {
+          if (q < len) wv[cur][q] = fmul(F, c2, wv[cur][q]);
+          else rv[q - len] = fmul(F, coef, rv[q - len]);
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < len; i += nt) {  // work keys: -c2*v (+ coef*rv when the RHS has the key)
           if (i == oi) { fw[i] = 0; continue; }
           const uint32_t key = wk[cur][i];
           const uint32_t lb = lds_lower_bound(rk, rl, key);
-          Fe x = fneg(F, fmul(F, c2, wv[cur][i]));
-          if (lb < rl && rk[lb] == key) x = fadd(F, fmul(F, coef, rv[lb]), x);
+          Fe x = fneg(F, wv[cur][i]);
+          if (lb < rl && rk[lb] == key) x = fadd(F, rv[lb], x);
           wv[cur][i] = x;
           lbw[i] = lb;
           fw[i] = fe_is_zero(x) ? 0 : 1;
         }
-        for (uint32_t j = tid; j < rl; j += nt) {
+        for (uint32_t j = tid; j < rl; j += nt) {  // RHS-only keys: coef*rv
           const uint32_t key = rk[j];
           const uint32_t lb = lds_lower_bound(wk[cur], len, key);
           if (lb < len && wk[cur][lb] == key) { fr[j] = 0; lbr[j] = RS_NONE; continue; }
-          Fe x = fmul(F, coef, rv[j]);
-          rv[j] = x;
           lbr[j] = lb;
-          fr[j] = fe_is_zero(x) ? 0 : 1;
+          fr[j] = fe_is_zero(rv[j]) ? 0 : 1;
         }
         __syncthreads();
         const uint32_t tw = wave_excl_scan(fw, len);
@@ -1103,6 +1111,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         __syncthreads();
         cur = nx;
         by += 36ull * (len + rl + tw + tr);
+        tp_merge += wall_clock64() - tp_x;
         len = tw + tr;
       }
     }
@@ -1114,6 +1123,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       if (A.prof) {
         unsigned long long *P = A.prof + 16 * ci;
         P[2] = rows; P[5] = wall_clock64() - t_1; P[8] = merges; P[9] = mwork;
+        P[13] = tp_piv; P[14] = tp_hold; P[15] = tp_merge;
       }
     }
     __syncthreads();
