@@ -110,6 +110,8 @@ struct rs_engine {
   uint64_t pool_want = 0;  // substitution pool size (entries) that fitted last time
   int device = 0;
   hipStream_t st = nullptr;
+  hipStream_t st2 = nullptr;  // the largest clusters' elimination chain runs here, beside the rest
+  hipEvent_t evx[8] = {};     // [0] join-in, [1..4] head chain, [5] after the lane kernel
   Arena A;
   bool loaded = false;
   bool have_result = false;
@@ -556,24 +558,42 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
     HC(hipMemsetAsync(a.bytes, 0, 24, E->st));
+    // The largest clusters' prep -> main -> finish chain runs on a second stream: the elimination
+    // time is the critical path of the largest cluster, and everything else overlaps it.
+    const char *hd = getenv("RS_HEAD");
+    const uint64_t n_head = std::min<uint64_t>(n_big, hd ? (uint64_t)atoi(hd) : 16), n_tail = n_big - n_head;
+    ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
+    at.big_touch_off += n_head;
+    at.big_touch_n += n_head;
+    if (at.prof) at.prof += 16 * n_head;
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
-      if (n_big) {
+      if (n_head) {
+        HC(hipStreamWaitEvent(E->st2, E->ev2, 0));
+        const unsigned g = (unsigned)n_head;
+        HC(hipEventRecord(E->evx[1], E->st2));
+        hipLaunchKernelGGL(k_big_prep, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
+        HC(hipEventRecord(E->evx[2], E->st2));
+        hipLaunchKernelGGL(k_big_main, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
+        HC(hipEventRecord(E->evx[3], E->st2));
+        hipLaunchKernelGGL(k_big_finish, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
+        HC(hipEventRecord(E->evx[4], E->st2));
+      }
+      if (n_tail) {
         // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
         // per-lane pool chunks are bounded by the grid size
-        const unsigned gb = (unsigned)std::min<uint64_t>(n_big, 2048), gm = (unsigned)std::min<uint64_t>(n_big, 8192);
-        // experiment knobs: dynamic LDS to limit co-resident workgroups per CU
-        const char *xm = getenv("RS_XM"), *xf = getenv("RS_XF"), *gmm = getenv("RS_GM"), *gfb = getenv("RS_GF");
-        const unsigned lm = xm ? (unsigned)atoi(xm) : 0, lf = xf ? (unsigned)atoi(xf) : 0;
-        const unsigned gm2 = gmm ? (unsigned)std::min<uint64_t>(n_big, atoi(gmm)) : gm;
-        const unsigned gf2 = gfb ? (unsigned)std::min<uint64_t>(n_big, atoi(gfb)) : gb;
-        hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        const unsigned gb = (unsigned)std::min<uint64_t>(n_tail, 2048), gm = (unsigned)std::min<uint64_t>(n_tail, 8192);
+        const uint32_t *ids = d_big + n_head;
+        hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev5, E->st));
-        hipLaunchKernelGGL(k_big_main, dim3(gm2), dim3(64), lm, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev6, E->st));
-        hipLaunchKernelGGL(k_big_finish, dim3(gf2), dim3(256), lf, E->st, a, (const uint32_t *)d_big, (uint64_t)n_big);
+        hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
       }
       HC(hipEventRecord(E->ev4, E->st));
@@ -583,6 +603,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
                            (const uint32_t *)d_small, (uint64_t)n_small);
         HC(hipGetLastError());
       }
+      HC(hipEventRecord(E->evx[5], E->st));
+      if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
       HC(hipEventRecord(E->ev3, E->st));
     }
     int err = 0;
@@ -608,15 +630,19 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipEventElapsedTime(&ms, E->ev2, E->ev3));
       float mb = 0;
       HC(hipEventElapsedTime(&mb, E->ev2, E->ev4));
-      E->stats.elim_big_ms += mb;
-      E->stats.elim_small_ms += ms - mb;
+      float msm = 0;
+      HC(hipEventElapsedTime(&msm, E->ev4, E->evx[5]));
+      E->stats.elim_big_ms += ms - msm;  // wall of the workgroup kernels (both streams)
+      E->stats.elim_small_ms += msm;
       unsigned long long b3[3] = {0, 0, 0};
       HC(hipMemcpy(b3, a.bytes, 24, hipMemcpyDeviceToHost));
       by = b3[0];
       E->stats.elim_kernel_ms += ms;
       E->stats.elim_kernel_launches++;
       E->stats.elim_bytes += by;
-      if (n_big) {
+      E->stats.big_main_bytes += b3[1];
+      E->stats.big_finish_bytes += b3[2];
+      if (n_tail) {
         float m0 = 0, m1 = 0, m2 = 0;
         HC(hipEventElapsedTime(&m0, E->ev2, E->ev5));
         HC(hipEventElapsedTime(&m1, E->ev5, E->ev6));
@@ -624,8 +650,16 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.big_prep_ms += m0;
         E->stats.big_main_ms += m1;
         E->stats.big_finish_ms += m2;
-        E->stats.big_main_bytes += b3[1];
-        E->stats.big_finish_bytes += b3[2];
+        E->stats.big_launches++;
+      }
+      if (n_head) {
+        float m0 = 0, m1 = 0, m2 = 0;
+        HC(hipEventElapsedTime(&m0, E->evx[1], E->evx[2]));
+        HC(hipEventElapsedTime(&m1, E->evx[2], E->evx[3]));
+        HC(hipEventElapsedTime(&m2, E->evx[3], E->evx[4]));
+        E->stats.big_prep_ms += m0;
+        E->stats.big_main_ms += m1;
+        E->stats.big_finish_ms += m2;
         E->stats.big_launches++;
       }
     }
@@ -1549,6 +1583,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     std::unique_ptr<rs_engine> E(new rs_engine());
     E->device = device;
     HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
+    for (auto &ev : E->evx) HC(hipEventCreate(&ev));
     HC(hipEventCreate(&E->ev0));
     HC(hipEventCreate(&E->ev1));
     HC(hipEventCreate(&E->ev2));
@@ -1581,6 +1617,9 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->heap_k) (void)hipFree(E->heap_k);
   if (E->heap_v) (void)hipFree(E->heap_v);
   if (E->st) (void)hipStreamDestroy(E->st);
+  if (E->st2) (void)hipStreamDestroy(E->st2);
+  for (auto &ev : E->evx)
+    if (ev) (void)hipEventDestroy(ev);
   delete E;
 }
 
