@@ -923,10 +923,9 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
   __shared__ uint32_t rk[kBigCap];
   __shared__ Fe rv[kBigCap];
   __shared__ uint32_t fw[kBigCap], fr[kBigCap], lbw[kBigCap], lbr[kBigCap];
-  __shared__ uint32_t s_fdel, s_m, s_nl, s_ok, s_rlen;
+  __shared__ uint32_t s_fdel, s_m, s_nl, s_ok;
   __shared__ unsigned long long s_best;
-  __shared__ uint64_t s_o, s_roff;
-  __shared__ Fe s_c2;
+  __shared__ uint64_t s_o;
   const uint32_t tid = threadIdx.x, nt = 64;
   Alloc al0;  // lane 0's allocator
   al0.chunk = 4096;
@@ -970,25 +969,62 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         tp_x = wall_clock64();
         // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
         // -> max id.  take_signal_3 (:368-377): the max takeable key; a conflict iff it is deleted.
-        if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
-        __syncthreads();
-        for (uint32_t i = tid; i < len; i += nt) {
-          uint32_t s = wk[cur][i];
-          if (A.forb[s]) continue;
-          if (!p4) { atomicMin(&s_best, 0xffffffffull - i); continue; }
-          if (A.del[s]) { atomicMin(&s_fdel, i); continue; }
-          int32_t o = A.occ[s];
-          if (o < 0) { atomicOr(A.err, 16); o = 0; }
-          atomicMin(&s_best, ((unsigned long long)(uint32_t)o << 32) | (0xffffffffu - i));  // sorted keys
+        uint32_t oi = RS_NONE;
+        bool conflict = false;
+        int32_t hs = -1;
+        if (len <= 64) {  // one entry per lane: ballots and a butterfly instead of LDS atomics
+          const uint32_t key = tid < len ? wk[cur][tid] : 0u;
+          bool tk = false, dl = false;
+          int32_t oc = 0, hsl = -1;
+          if (tid < len && !A.forb[key]) {
+            tk = true;
+            dl = A.del[key] != 0;
+            if (dl) hsl = A.holder_idx[key];  // fetched speculatively with the pivot search
+            else if (p4) {
+              oc = A.occ[key];
+              if (oc < 0) { atomicOr(A.err, 16); oc = 0; }
+            }
+          }
+          const uint64_t tm = __ballot(tk), dm = __ballot(tk && dl);
+          if (tm) {
+            if (!p4) {
+              oi = 63 - __clzll(tm);
+            } else if (dm) {
+              oi = __ffsll((long long)dm) - 1;
+            } else {
+              unsigned long long v = tk ? ((unsigned long long)(uint32_t)oc << 32) | (0xffffffffu - tid) : ~0ull;
+#pragma unroll
+              for (int d = 32; d >= 1; d >>= 1) {
+                unsigned long long w = __shfl_xor(v, d);
+                v = w < v ? w : v;
+              }
+              oi = 0xffffffffu - (uint32_t)(v & 0xffffffffu);
+            }
+            conflict = (dm >> oi) & 1ull;
+            hs = __shfl(hsl, (int)oi);
+          }
+        } else {
+          if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
+          __syncthreads();
+          for (uint32_t i = tid; i < len; i += nt) {
+            uint32_t s = wk[cur][i];
+            if (A.forb[s]) continue;
+            if (!p4) { atomicMin(&s_best, 0xffffffffull - i); continue; }
+            if (A.del[s]) { atomicMin(&s_fdel, i); continue; }
+            int32_t o = A.occ[s];
+            if (o < 0) { atomicOr(A.err, 16); o = 0; }
+            atomicMin(&s_best, ((unsigned long long)(uint32_t)o << 32) | (0xffffffffu - i));  // sorted keys
+          }
+          __syncthreads();
+          const uint32_t fdel = s_fdel;
+          const unsigned long long best = s_best;
+          if (fdel != RS_NONE || best != ~0ull) {
+            oi = fdel != RS_NONE ? fdel : 0xffffffffu - (uint32_t)(best & 0xffffffffu);
+            conflict = fdel != RS_NONE || (!p4 && A.del[wk[cur][oi]]);
+            if (conflict) hs = A.holder_idx[wk[cur][oi]];
+          }
         }
-        __syncthreads();
-        uint32_t fdel = s_fdel;
-        const unsigned long long best = s_best;
-        if (!p4 && best != ~0ull) {
-          const uint32_t mi = 0xffffffffu - (uint32_t)(best & 0xffffffffu);
-          if (A.del[wk[cur][mi]]) fdel = mi;
-        }
-        if (fdel == RS_NONE && best == ~0ull) {  // nothing takeable: leftover
+        if (oi == RS_NONE) {  // nothing takeable: leftover
           if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
           __syncthreads();
           by += 36ull * len;
@@ -1000,9 +1036,8 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           __syncthreads();
           break;
         }
-        const uint32_t oi = fdel != RS_NONE ? fdel : 0xffffffffu - (uint32_t)(best & 0xffffffffu);
         const uint32_t p = wk[cur][oi];
-        if (fdel == RS_NONE) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
+        if (!conflict) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
           const uint32_t sh = wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
           const uint32_t mm = len - 1 + sh;
           by += 36ull * mm;
@@ -1033,16 +1068,11 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           break;
         }
         { unsigned long long t = wall_clock64(); tp_piv += t - tp_x; tp_x = t; }
-        // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p)
-        if (tid == 0) {
-          int32_t hs = A.holder_idx[p];
-          s_roff = A.h_off[hs];
-          s_rlen = A.h_len[hs];
-          s_c2 = A.h_coef[hs];
-        }
-        __syncthreads();
-        const uint32_t rl = s_rlen;
-        const uint64_t roff = s_roff;
+        // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p); every lane reads the
+        // holder's words itself (same addresses: one request per wave)
+        const uint64_t roff = A.h_off[hs];
+        const uint32_t rl = A.h_len[hs];
+        const Fe c2 = A.h_coef[hs];
         ++merges;
         mwork += len + rl;
         if (rl > kBigCap || len + rl > kBigCap + 1) {  // spill, finish the row on lane 0
@@ -1063,8 +1093,53 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           break;
         }
         { unsigned long long t = wall_clock64(); tp_hold += t - tp_x; tp_x = t; }
-        const Fe c2 = s_c2;
         const Fe coef = fneg(F, wv[cur][oi]);
+        const uint32_t nx = cur ^ 1;
+        if (len <= 64 && rl <= 64) {
+          // ---- register merge: lane l holds work entry l and RHS entry l; positions by ballots
+          const uint32_t l = tid;
+          uint32_t wkey = 0, rkey = RS_NONE;
+          Fe wval = fe_zero(), rval = fe_zero();
+          if (l < rl) { rkey = A.pk[roff + l]; rval = A.pv[roff + l]; }
+          if (l < len) { wkey = wk[cur][l]; wval = wv[cur][l]; }
+          if (l < len) wval = fmul(F, c2, wval);   // one product per entry, both lists at once
+          if (l < rl) rval = fmul(F, coef, rval);
+          if (l < rl) { rk[l] = rkey; rv[l] = rval; }
+          __syncthreads();
+          bool keep_w = false, keep_r = false;
+          uint32_t lb_w = 0, lb_r = 0;
+          if (l < len && l != oi) {  // -c2*v (+ coef*rv when the RHS has the key)
+            lb_w = lds_lower_bound(rk, rl, wkey);
+            wval = fneg(F, wval);
+            if (lb_w < rl && rk[lb_w] == wkey) wval = fadd(F, rv[lb_w], wval);
+            keep_w = !fe_is_zero(wval);
+          }
+          if (l < rl) {  // RHS-only keys: coef*rv
+            lb_r = lds_lower_bound(wk[cur], len, rkey);
+            keep_r = !(lb_r < len && wk[cur][lb_r] == rkey) && !fe_is_zero(rval);
+          }
+          const uint64_t wmk = __ballot(keep_w), rmk = __ballot(keep_r);
+          auto below = [](uint64_t m, uint32_t k) -> uint32_t {
+            return (uint32_t)__popcll(k >= 64 ? m : (m & ((1ull << k) - 1ull)));
+          };
+          if (keep_w) {
+            const uint32_t q = below(wmk, l) + below(rmk, lb_w);
+            wk[nx][q] = wkey;
+            wv[nx][q] = wval;
+          }
+          if (keep_r) {
+            const uint32_t q = below(rmk, l) + below(wmk, lb_r);
+            wk[nx][q] = rkey;
+            wv[nx][q] = rval;
+          }
+          __syncthreads();
+          const uint32_t nlen = (uint32_t)(__popcll(wmk) + __popcll(rmk));
+          cur = nx;
+          by += 36ull * (len + rl + nlen);
+          tp_merge += wall_clock64() - tp_x;
+          len = nlen;
+          continue;
+        }
         for (uint32_t j = tid; j < rl; j += nt) { rk[j] = A.pk[roff + j]; rv[j] = A.pv[roff + j]; }
         __syncthreads();
         // one product per entry, all lanes at once: work entries c2*v, RHS entries coef*rv
@@ -1093,7 +1168,6 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         __syncthreads();
         const uint32_t tw = wave_excl_scan(fw, len);
         const uint32_t tr = wave_excl_scan(fr, rl);
-        const uint32_t nx = cur ^ 1;
         for (uint32_t i = tid; i < len; i += nt) {
           if (i == oi || fe_is_zero(wv[cur][i])) continue;
           const uint32_t lb = lbw[i];
