@@ -23,6 +23,7 @@ struct FieldP {
   Fe r2;        // R^2 mod p
   Fe one;       // R mod p
   Fe pm2;       // p - 2 (Fermat exponent)
+  Fe r3;        // R^3 mod p (Montgomery-form inverse from a plain binary GCD)
 };
 
 __host__ __device__ __forceinline__ bool fe_is_zero(const Fe &a) {
@@ -134,8 +135,8 @@ __host__ __device__ __forceinline__ Fe ffrom_mont(const FieldP &F, const Fe &a) 
   o.l[0] = 1;
   return fmul(F, a, o);
 }
-// a^(p-2) = a^-1 for a != 0 (the value num-bigint's mod_inverse returns).
-__host__ __device__ inline Fe finv(const FieldP &F, const Fe &a) {
+// a^(p-2) = a^-1 for a != 0 (Fermat; kept as the reference implementation of finv).
+__host__ __device__ inline Fe finv_fermat(const FieldP &F, const Fe &a) {
   Fe r = F.one, base = a;
   for (int w = 0; w < 4; ++w) {
     uint64_t e = F.pm2.l[w];
@@ -146,6 +147,45 @@ __host__ __device__ inline Fe finv(const FieldP &F, const Fe &a) {
     }
   }
   return r;
+}
+__host__ __device__ __forceinline__ void shr1c(uint64_t *x, uint64_t top) {  // x = (top:x) >> 1
+  x[0] = (x[0] >> 1) | (x[1] << 63);
+  x[1] = (x[1] >> 1) | (x[2] << 63);
+  x[2] = (x[2] >> 1) | (x[3] << 63);
+  x[3] = (x[3] >> 1) | (top << 63);
+}
+__host__ __device__ __forceinline__ bool is_one4(const uint64_t *x) { return x[0] == 1 && (x[1] | x[2] | x[3]) == 0; }
+// Inverse in Montgomery form: binary extended Euclid on the residue aR (shifts, adds and
+// subtractions only), (aR)^-1 = a^-1 R^-1, then one product by R^3 gives a^-1 R.  The same value
+// as num-bigint's mod_inverse (the inverse is unique); about 30x lower latency than Fermat's
+// ~384 dependent products (tools/micro/fmul_bench.hip).
+__host__ __device__ inline Fe finv(const FieldP &F, const Fe &a) {
+  if (fe_is_zero(a)) return a;
+  uint64_t u[4], v[4], x1[4] = {1, 0, 0, 0}, x2[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) { u[i] = a.l[i]; v[i] = F.p[i]; }
+  while (!is_one4(u) && !is_one4(v)) {
+    while ((u[0] & 1) == 0) {
+      shr1c(u, 0);
+      uint64_t c = (x1[0] & 1) ? add4(x1, x1, F.p) : 0;
+      shr1c(x1, c);
+    }
+    while ((v[0] & 1) == 0) {
+      shr1c(v, 0);
+      uint64_t c = (x2[0] & 1) ? add4(x2, x2, F.p) : 0;
+      shr1c(x2, c);
+    }
+    if (geq4(u, v)) {
+      sub4(u, u, v);
+      if (sub4(x1, x1, x2)) add4(x1, x1, F.p);
+    } else {
+      sub4(v, v, u);
+      if (sub4(x2, x2, x1)) add4(x2, x2, F.p);
+    }
+  }
+  Fe r;
+  const uint64_t *x = is_one4(u) ? x1 : x2;
+  for (int i = 0; i < 4; ++i) r.l[i] = x[i];
+  return fmul(F, r, F.r3);
 }
 
 inline FieldP make_field(const uint64_t prime[4]) {
@@ -164,6 +204,7 @@ inline FieldP make_field(const uint64_t prime[4]) {
   for (int j = 0; j < 4; ++j) F.r2.l[j] = x[j];
   uint64_t two[4] = {2, 0, 0, 0};
   sub4(F.pm2.l, F.p, two);
+  F.r3 = fmul(F, F.r2, F.r2);
   return F;
 }
 

@@ -1095,6 +1095,49 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         { unsigned long long t = wall_clock64(); tp_hold += t - tp_x; tp_x = t; }
         const Fe coef = fneg(F, wv[cur][oi]);
         const uint32_t nx = cur ^ 1;
+        if (len + rl <= 64) {
+          // ---- packed register merge: lanes [0, len) hold the work, lanes [len, len + rl) the
+          // RHS, so the whole step costs one product latency; positions by ballots
+          const uint32_t l = tid;
+          const bool isw = l < len, isr = !isw && l < len + rl;
+          const uint32_t j = l - len;
+          uint32_t key = 0;
+          Fe val = fe_zero();
+          if (isw) { key = wk[cur][l]; val = wv[cur][l]; }
+          if (isr) { key = A.pk[roff + j]; val = A.pv[roff + j]; }
+          if (isw || isr) val = fmul(F, isw ? c2 : coef, val);
+          if (isr) { rk[j] = key; rv[j] = val; }
+          __syncthreads();
+          bool keep = false;
+          uint32_t lb = 0;
+          if (isw && l != oi) {  // -c2*v (+ coef*rv when the RHS has the key)
+            lb = lds_lower_bound(rk, rl, key);
+            val = fneg(F, val);
+            if (lb < rl && rk[lb] == key) val = fadd(F, rv[lb], val);
+            keep = !fe_is_zero(val);
+          }
+          if (isr) {  // RHS-only keys: coef*rv
+            lb = lds_lower_bound(wk[cur], len, key);
+            keep = !(lb < len && wk[cur][lb] == key) && !fe_is_zero(val);
+          }
+          const uint64_t km = __ballot(keep);
+          const uint64_t wmk = len >= 64 ? km : (km & ((1ull << len) - 1ull)), rmk = km >> len;
+          auto below = [](uint64_t m, uint32_t k) -> uint32_t {
+            return (uint32_t)__popcll(k >= 64 ? m : (m & ((1ull << k) - 1ull)));
+          };
+          if (keep) {
+            const uint32_t q = isw ? below(wmk, l) + below(rmk, lb) : below(rmk, j) + below(wmk, lb);
+            wk[nx][q] = key;
+            wv[nx][q] = val;
+          }
+          __syncthreads();
+          const uint32_t nlen = (uint32_t)__popcll(km);
+          cur = nx;
+          by += 36ull * (len + rl + nlen);
+          tp_merge += wall_clock64() - tp_x;
+          len = nlen;
+          continue;
+        }
         if (len <= 64 && rl <= 64) {
           // ---- register merge: lane l holds work entry l and RHS entry l; positions by ballots
           const uint32_t l = tid;
@@ -1226,9 +1269,156 @@ __device__ inline uint32_t blk_excl_scan(uint32_t *a, uint32_t n, uint32_t *s_pa
   return total;
 }
 
+// Lane-serial composition of slot `sl` (raw_substitution key by key, ascending): the fallback for
+// lists the wave path does not hold.
+__device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t sl, unsigned long long &by) {
+  uint64_t off = A.h_off[sl];
+  uint32_t len = A.h_len[sl];
+  const uint32_t *kk = A.pk + off;
+  uint64_t bound = len;
+  for (uint32_t t = 0; t < len; ++t) {
+    int32_t hs = A.holder_idx[kk[t]];
+    if (hs >= 0) bound += A.h_len[hs];
+  }
+  uint64_t buf0 = pool_alloc(A, al, bound), buf1 = pool_alloc(A, al, bound);
+  if (buf0 == RS_NONE || buf1 == RS_NONE) return false;
+  const uint64_t orig_off = off;
+  const uint32_t orig_len = len;
+  uint64_t dst = buf0;
+  for (uint32_t t = 0; t < orig_len; ++t) {
+    uint32_t key = A.pk[orig_off + t];
+    int32_t hs = A.holder_idx[key];
+    if (hs < 0) continue;
+    uint32_t nl2;
+    d_raw_sub_into(A, off, len, key, A.h_off[hs], A.h_len[hs], dst, nl2);
+    off = dst;
+    len = nl2;
+    dst = dst == buf0 ? buf1 : buf0;
+  }
+  A.h_off[sl] = off;
+  A.h_len[sl] = len;
+  by += 36ull * (bound + len);
+  return true;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr uint32_t kComposeCap = 256;  // entries one wave composes in LDS
+
+// Composition of slot `sl` by one wave (every dependency already final): the result is the sum of
+// the slot's non-deleted entries and c_t * R(t) for each deleted key t (coefficient c_t), with
+// every key kept even when its sum is zero -- the value raw_substitution applied key by key gives
+// (algebra.rs:1279-1294), in any order.  Entries are gathered into LDS (one product per
+// dependency entry, spread over the lanes), bitonic-sorted by key, summed per key and written out.
+// Returns 0 on success, 1 when the lists do not fit (caller falls back), 2 on pool exhaustion.
+__device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, uint64_t *S, Fe *V,
+                                     uint32_t *dex, uint64_t *dof, Fe *dmu, unsigned long long &by) {
+  const FieldP &F = A.F;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t off = A.h_off[sl];
+  const uint32_t len = A.h_len[sl];
+  if (len > 64) return 1;
+  uint32_t key = 0;
+  Fe val = fe_zero();
+  int32_t hs = -1;
+  uint32_t dl = 0;
+  uint64_t doff = 0;
+  if (lane < len) {
+    key = A.pk[off + lane];
+    val = A.pv[off + lane];
+    hs = A.holder_idx[key];
+    if (hs >= 0) { dl = A.h_len[hs]; doff = A.h_off[hs]; }
+  }
+  const uint64_t dm = __ballot(hs >= 0), om = __ballot(lane < len && hs < 0);
+  const uint64_t lt = lane ? ((1ull << lane) - 1ull) : 0ull;
+  const uint32_t n_own = (uint32_t)__popcll(om);
+  // exclusive prefix of the dependency lengths
+  uint32_t x = dl;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d);
+    if ((int)lane >= d) x += y;
+  }
+  const uint32_t tot = __shfl(x, 63), ex = x - dl;
+  const uint32_t E = n_own + tot;
+  if (E > kComposeCap) return 1;
+  if (hs >= 0) {
+    const uint32_t r = (uint32_t)__popcll(dm & lt);
+    dex[r] = ex;
+    dof[r] = doff;
+    dmu[r] = val;
+  }
+  if (lane < len && hs < 0) {
+    const uint32_t q = (uint32_t)__popcll(om & lt);
+    S[q] = ((uint64_t)key << 32) | q;
+    V[q] = val;
+  }
+  wave_sync();
+  const uint32_t D = (uint32_t)__popcll(dm);
+  for (uint32_t e = lane; e < tot; e += 64) {  // c_t * R(t), one product per entry
+    uint32_t lo = 0, hi = D;                     // last dependency with dex <= e
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (dex[mid] <= e) lo = mid; else hi = mid;
+    }
+    const uint64_t src = dof[lo] + (e - dex[lo]);
+    const uint32_t q = n_own + e;
+    S[q] = ((uint64_t)A.pk[src] << 32) | q;
+    V[q] = fmul(F, dmu[lo], A.pv[src]);
+  }
+  uint32_t np2 = 1;
+  while (np2 < E) np2 <<= 1;
+  for (uint32_t q = E + lane; q < np2; q += 64) S[q] = ~0ull;
+  wave_sync();
+  for (uint32_t k = 2; k <= np2; k <<= 1) {  // bitonic sort of (key, position)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = lane; t < np2 / 2; t += 64) {
+        const uint32_t i = (t / j) * 2 * j + (t % j), pr = i + j;
+        const uint64_t a = S[i], c = S[pr];
+        if ((a > c) == ((i & k) == 0)) { S[i] = c; S[pr] = a; }
+      }
+      wave_sync();
+    }
+  }
+  uint64_t o = 0;
+  if (lane == 0) o = pool_alloc(A, al, E ? E : 1);
+  o = __shfl(o, 0);
+  if (o == RS_NONE) return 2;
+  uint32_t run = 0;
+  for (uint32_t cb = 0; cb < E; cb += 64) {  // one output entry per distinct key, values summed
+    const uint32_t p = cb + lane;
+    const uint32_t k0 = p < E ? (uint32_t)(S[p] >> 32) : 0u;
+    const bool head = p < E && (p == 0 || (uint32_t)(S[p - 1] >> 32) != k0);
+    const uint64_t hm = __ballot(head);
+    if (head) {
+      Fe v = V[(uint32_t)S[p]];
+      for (uint32_t q = p + 1; q < E && (uint32_t)(S[q] >> 32) == k0; ++q) v = fadd(F, v, V[(uint32_t)S[q]]);
+      const uint64_t w = o + run + (uint32_t)__popcll(hm & lt);
+      A.pk[w] = k0;
+      A.pv[w] = v;
+    }
+    run += (uint32_t)__popcll(hm);
+  }
+  if (lane == 0) {
+    A.h_off[sl] = o;
+    A.h_len[sl] = run;
+    by += 36ull * (len + tot + run);
+  }
+  return 0;
+}
+
 __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
   __shared__ uint32_t s_ok, s_nf, s_part[4];
+  __shared__ uint64_t cw_S[4][kComposeCap];  // per-wave composition buffers
+  __shared__ Fe cw_V[4][kComposeCap];
+  __shared__ uint32_t cw_dex[4][64];
+  __shared__ uint64_t cw_dof[4][64];
+  __shared__ Fe cw_dmu[4][64];
   __shared__ uint64_t s_scr;
   __shared__ unsigned long long s_hsum, s_hmax;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -1317,34 +1507,15 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
           }
           __syncthreads();
           nf = s_nf;
-          for (uint32_t f = tid; f < nf; f += nt) {
-            const uint32_t i = nxt[f];
-            uint64_t off = A.h_off[b + i];
-            uint32_t len = A.h_len[b + i];
-            const uint32_t *kk = A.pk + off;
-            uint64_t bound = len;
-            for (uint32_t t = 0; t < len; ++t) {
-              int32_t hs = A.holder_idx[kk[t]];
-              if (hs >= 0) bound += A.h_len[hs];
+          {  // one wave per substitution of the frontier
+            const uint32_t wv_ = tid >> 6, nw = nt >> 6;
+            for (uint32_t f = wv_; f < nf; f += nw) {
+              const uint64_t sl = b + nxt[f];
+              const int rc = d_compose_wave(A, al, sl, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
+              if (rc == 2) { if ((tid & 63) == 0) s_ok = 0; continue; }
+              if (rc == 1 && (tid & 63) == 0 && !d_compose_serial(A, al, sl, by)) s_ok = 0;
+              wave_sync();
             }
-            uint64_t buf0 = pool_alloc(A, al, bound), buf1 = pool_alloc(A, al, bound);
-            if (buf0 == RS_NONE || buf1 == RS_NONE) { s_ok = 0; continue; }
-            const uint64_t orig_off = off;
-            const uint32_t orig_len = len;
-            uint64_t dst = buf0;
-            for (uint32_t t = 0; t < orig_len; ++t) {  // raw_substitution key by key, ascending
-              uint32_t key = A.pk[orig_off + t];
-              int32_t hs = A.holder_idx[key];
-              if (hs < 0) continue;
-              uint32_t nl2;
-              d_raw_sub_into(A, off, len, key, A.h_off[hs], A.h_len[hs], dst, nl2);
-              off = dst;
-              len = nl2;
-              dst = dst == buf0 ? buf1 : buf0;
-            }
-            A.h_off[b + i] = off;
-            A.h_len[b + i] = len;
-            by += 36ull * (bound + len);
           }
           done += nf;
           ++levels;
