@@ -59,6 +59,16 @@ __global__ void k_chain(FieldP F, Fe *io, int n, unsigned long long *cyc) {
   if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+template <int V>
+__global__ void k_inv(FieldP F, Fe *io, int n, unsigned long long *cyc) {
+  Fe x = io[threadIdx.x];
+  unsigned long long t0 = wall_clock64();
+  for (int i = 0; i < n; ++i) { x = V == 0 ? finv_fermat(F, x) : finv(F, x); x.l[0] ^= 1; }
+  unsigned long long t1 = wall_clock64();
+  io[threadIdx.x] = x;
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
   const uint64_t bn[4] = {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL, 0x30644e72e131a029ULL};
   FieldP F = make_field(bn);
@@ -80,5 +90,13 @@ int main() {
   bool same = true;
   for (int i = 0; i < 64; ++i) for (int j = 0; j < 4; ++j) same &= out[0][i].l[j] == out[1][i].l[j];
   printf("results identical: %s\n", same ? "yes" : "NO");
+  for (int v = 0; v < 2; ++v) {
+    hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice);
+    int n = v ? 200 : 20;
+    if (v == 0) hipLaunchKernelGGL(k_inv<0>, 1, 64, 0, 0, F, d, n, c);
+    else hipLaunchKernelGGL(k_inv<1>, 1, 64, 0, 0, F, d, n, c);
+    unsigned long long cy; hipMemcpy(&cy, c, 8, hipMemcpyDeviceToHost);
+    printf("inverse %s: %.1f us per inversion (one wave, 64 lanes divergent)\n", v ? "binary GCD" : "Fermat", cy * 10.0 / n / 1000.0);
+  }
   return 0;
 }
