@@ -52,8 +52,29 @@ struct RsError : std::runtime_error {
                     std::string(#x) + ": " + hipGetErrorString(e_));                          \
   } while (0)
 
+static bool g_prof_env = getenv("RS_PROF") != nullptr;
+static inline double now_ms();
+// RS_PROF: host timeline of the round loop (synchronising the stream at each mark)
+struct Marks {
+  std::vector<std::pair<const char *, double>> m;
+  hipStream_t st;
+  void mark(const char *what);
+  void dump();
+};
 static inline double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void Marks::mark(const char *what) {
+  if (!g_prof_env) return;
+  (void)hipStreamSynchronize(st);
+  m.push_back({what, now_ms()});
+}
+void Marks::dump() {
+  if (!g_prof_env || m.empty()) return;
+  fprintf(stderr, "[rs-prof]");
+  for (size_t i = 1; i < m.size(); ++i) fprintf(stderr, " %s %.2f", m[i].first, m[i].second - m[i - 1].second);
+  fprintf(stderr, "\n");
 }
 
 // ------------------------------------------------------------------ device buffer arena
@@ -175,6 +196,17 @@ static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, u
   HC(hipMemcpyAsync(&last_out, out + n - 1, 8, hipMemcpyDeviceToHost, E->st));
   HC(hipStreamSynchronize(E->st));
   return last_in + last_out;
+}
+
+// apply_substitution_to_map (:369-377) appends every key of sub.to to the signal map when
+// map[from] is non-empty; only the key set survives the rounds (rebuild_witness), so it is kept as
+// bits.  A round's `from` signals never occur in its (non-overlapping) right-hand sides.
+__global__ void k_append_marks(const uint32_t *usig, const uint64_t *uoff, const uint32_t *ulen, uint64_t nU,
+                               const uint32_t *pk, uint8_t *nlmap) {
+  for (uint64_t i = gtid(); i < nU; i += gstride()) {
+    if (!nlmap[usig[i]]) continue;
+    for (uint32_t t = 0; t < ulen[i]; ++t) nlmap[pk[uoff[i] + t]] = 1;
+  }
 }
 
 template <class K, class V>
@@ -1189,7 +1221,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
 
   // ======================= rounds >= 2 (:613-646)
   bool apply_round = apply_linear && no_rounds > 0 && n_wl > 0;
-  std::vector<uint32_t> extra_keys;  // keys appended to the signal map that no final row may hold
   if (getenv("RS_DEBUG")) {
     HC(hipStreamSynchronize(st));
     fprintf(stderr, "[rs-debug] heap %p cap %llu top %llu n_st %llu n_wl %llu\n", (void *)heap_k,
@@ -1255,7 +1286,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       }
       launch(st, k_unmark_list, q.size(), (const uint32_t *)d_q, (uint64_t)q.size(), qflag);
     };
-    std::vector<uint8_t> extra_mark;
     E->stats.subst_ms += now_ms() - Tm;
     E->stats.map_ms += now_ms() - Tm;
     int32_t *rank_of = A.get<int32_t>("rank_of", S);
@@ -1268,7 +1298,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       HC(hipMemsetAsync(r_sub_of, 0xff, 4 * S, st));
       run_linear_simplification(E, lv, fl->use_old_heuristics, er, P, d_err, d_forb, r_sub_of, d_deleted);
       E->stats.rounds++;
+      Marks MK;
+      MK.st = st;
+      MK.mark("start");
       collect_leftovers(E, er, P, lconst);
+      MK.mark("leftovers");
       double Tr = now_ms();
       // ordered substitutions of the round: cluster order, ascending `from`
       uint64_t n_slots = er.cl_off.back();
@@ -1290,20 +1324,18 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         U.insert(U.end(), sl.begin(), sl.end());
       }
       uint64_t nU = U.size();
+      MK.mark("order");
       // RHS keys of the substitutions (for the map appends)
       std::vector<uint64_t> uoff(nU);
       std::vector<uint32_t> ulen(nU), ukeys;
       std::vector<uint64_t> uvals, uptr;
       for (uint64_t i = 0; i < nU; ++i) { uoff[i] = hoff[U[i]]; ulen[i] = hlen[U[i]]; }
       fetch_pool_maps(E, uoff, ulen, P.pk, P.pv, ukeys, uvals, uptr);
+      MK.mark("fetch_rhs");
       std::vector<uint32_t> usig(nU);
       std::vector<int32_t> urank(nU);
       for (uint64_t i = 0; i < nU; ++i) { usig[i] = hsig[U[i]]; urank[i] = (int32_t)i; }
-      {
-        double Tq = now_ms();
-        query_initial(usig);
-        E->stats.map_ms += now_ms() - Tq;
-      }
+      MK.mark("query");
       uint32_t *d_us = A.get<uint32_t>("r.us", nU);
       int32_t *d_ur = A.get<int32_t>("r.ur", nU);
       if (nU) {
@@ -1346,7 +1378,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         ra.tmpk = A.get<uint32_t>("r.tmpk", 2 * (qc + 1));
         ra.tmpv = A.get<Fe>("r.tmpv", 2 * (qc + 1));
         ra.c_base = heap_top - qc;  // row scratch = 2 * (its C offset - c_base)
+        MK.mark("count");
         launch(st, k_round_fill, n_st, ra);
+        MK.mark("fill");
         if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qa + qb + qc);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
         // turned rows
@@ -1360,6 +1394,15 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         if (n_turn) HC(hipMemcpyAsync(htids.data(), tids, 4 * n_turn, hipMemcpyDeviceToHost, st));
         HC(hipMemcpyAsync(hturn.data(), ra.turn, 4 * n_st, hipMemcpyDeviceToHost, st));
         HC(hipStreamSynchronize(st));
+        {  // initial map lists of the turning substitutions' signals only
+          double Tq = now_ms();
+          std::vector<uint32_t> qs;
+          for (uint32_t r : htids) qs.push_back(usig[hturn[r]]);
+          std::sort(qs.begin(), qs.end());
+          qs.erase(std::unique(qs.begin(), qs.end()), qs.end());
+          query_initial(qs);
+          E->stats.map_ms += now_ms() - Tq;
+        }
         // order key: (rank of the turning substitution, first position in map[from])
         for (uint32_t r : htids) {
           int32_t q = hturn[r];
@@ -1378,6 +1421,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           turned.push_back({((uint64_t)q << 32) | (pos & 0xffffffffu), r});
         }
         std::sort(turned.begin(), turned.end());
+        MK.mark("turned");
         if (getenv("RS_DEBUG")) {
           std::vector<uint8_t> tch(n_st);
           HC(hipMemcpy(tch.data(), ra.touched, n_st, hipMemcpyDeviceToHost));
@@ -1389,24 +1433,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           fprintf(stderr, "\n");
         }
       }
-      // map appends (:369-377): every key of sub.to gets every visited row
-      for (uint64_t i = 0; i < nU; ++i) {
-        uint32_t from = usig[i];
-        const std::vector<uint32_t> &L0 = minit[from];
-        uint64_t n0 = L0.size();
-        auto it = mext.find(from);
-        uint64_t n1 = it == mext.end() ? 0 : it->second.size();
-        if (n0 + n1 == 0) continue;
-        std::vector<uint32_t> visit(L0.begin(), L0.end());
-        if (n1) visit.insert(visit.end(), it->second.begin(), it->second.end());
-        for (uint64_t t = uptr[i]; t < uptr[i + 1]; ++t) {
-          uint32_t k = ukeys[t];
-          std::vector<uint32_t> &dst = mext[k];
-          dst.insert(dst.end(), visit.begin(), visit.end());
-          if (extra_mark.empty()) extra_mark.assign(S, 0);
-          if (!extra_mark[k]) { extra_mark[k] = 1; extra_keys.push_back(k); }
-        }
-      }
+      MK.mark("appends");
       if (nU) {  // reset the dense rank index
         std::vector<int32_t> neg(nU, -1);
         h2d(E, d_ur, neg.data(), 4 * nU);
@@ -1424,6 +1451,37 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           if (clen[t.second]) next_ids.push_back(t.second);
       }
       uint64_t nn = next_ids.size();
+      // map appends (:369-377): the key set on the device; the row lists (positions for a later
+      // round's ordering) only when another round follows
+      if (nU) {
+        uint64_t *d_uoff = A.get<uint64_t>("r.uoff", nU);
+        uint32_t *d_ulen = A.get<uint32_t>("r.ulen", nU);
+        h2d(E, d_uoff, uoff.data(), 8 * nU);
+        h2d(E, d_ulen, ulen.data(), 4 * nU);
+        launch(st, k_append_marks, nU, (const uint32_t *)d_us, (const uint64_t *)d_uoff, (const uint32_t *)d_ulen, nU,
+               (const uint32_t *)P.pk, nlmap);
+      }
+      const bool another = nn > 0 && (no_rounds > 0 ? no_rounds - 1 : 0) > 0;
+      if (another) {
+        double Tq = now_ms();
+        query_initial(usig);
+        E->stats.map_ms += now_ms() - Tq;
+        for (uint64_t i = 0; i < nU; ++i) {
+          uint32_t from = usig[i];
+          const std::vector<uint32_t> &L0 = minit[from];
+          uint64_t n0 = L0.size();
+          auto it = mext.find(from);
+          uint64_t n1 = it == mext.end() ? 0 : it->second.size();
+          if (n0 + n1 == 0) continue;
+          std::vector<uint32_t> visit(L0.begin(), L0.end());
+          if (n1) visit.insert(visit.end(), it->second.begin(), it->second.end());
+          for (uint64_t t = uptr[i]; t < uptr[i + 1]; ++t) {
+            std::vector<uint32_t> &dst = mext[ukeys[t]];
+            dst.insert(dst.end(), visit.begin(), visit.end());
+          }
+        }
+      }
+      MK.mark("appends2");
       lv.n = nn;
       lv.off = A.get<uint64_t>("lv.off", nn);
       lv.len = A.get<uint32_t>("lv.len", nn);
@@ -1457,6 +1515,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           fprintf(stderr, "\n");
         }
       }
+      MK.mark("next");
+      MK.dump();
+      if (g_prof_env) fprintf(stderr, "[rs-prof] round: nU %llu n_st %llu next %llu\n", (unsigned long long)nU, (unsigned long long)n_st, (unsigned long long)nn);
       E->stats.subst_ms += now_ms() - Tr;
       E->stats.rounds_ms += now_ms() - Tr;
       if (no_rounds > 0) no_rounds--;
@@ -1467,11 +1528,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   double Tf = now_ms();
   // leftover linear rows (rounds exhausted): appended after the storage rows
   if (lv.n) launch(st, k_mark_keys, lv.n, lv, nlmap);
-  if (!extra_keys.empty()) {
-    uint32_t *d_x = A.get<uint32_t>("fin.extra", extra_keys.size());
-    h2d(E, d_x, extra_keys.data(), 4 * extra_keys.size());
-    launch(st, k_mark_list, extra_keys.size(), (const uint32_t *)d_x, (uint64_t)extra_keys.size(), nlmap);
-  }
   for (auto &c : lconst) host_fix(c);
   {
     std::vector<uint32_t> lk;
