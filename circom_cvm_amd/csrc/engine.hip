@@ -610,6 +610,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_main, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
+        hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
         hipLaunchKernelGGL(k_big_finish, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[4], E->st2));
@@ -625,6 +627,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev6, E->st));
+        hipLaunchKernelGGL(k_batch_inv, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
+        HC(hipGetLastError());
         hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
       }

@@ -1269,6 +1269,33 @@ __device__ inline uint32_t blk_excl_scan(uint32_t *a, uint32_t n, uint32_t *s_pa
   return total;
 }
 
+// multi_inv (modular_arithmetic.rs:71-91) of the pivot coefficients of every workgroup cluster,
+// before normalisation: one block per cluster, each lane inverts chunks of 64 slots with one
+// inversion per chunk (Montgomery's trick), so no cluster waits on an inversion chain of its own.
+// ftmp[slot] <- h_coef[slot]^-1.
+__global__ __launch_bounds__(64) void k_batch_inv(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const FieldP &F = A.F;
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c];
+    const uint32_t m = A.n_sub[c];
+    for (uint32_t c0 = tid * 64; c0 < m; c0 += 64 * 64) {
+      const uint32_t c1 = min(m, c0 + 64);
+      Fe acc = A.h_coef[b + c0];
+      A.ftmp[b + c0] = acc;
+      for (uint32_t i = c0 + 1; i < c1; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
+      Fe inv = finv(F, acc);
+      for (uint32_t i = c1 - 1; i > c0; --i) {
+        const Fe inv_i = fmul(F, A.ftmp[b + i - 1], inv);
+        inv = fmul(F, inv, A.h_coef[b + i]);
+        A.ftmp[b + i] = inv_i;
+      }
+      A.ftmp[b + c0] = inv;
+    }
+  }
+}
+
 // Lane-serial composition of slot `sl` (raw_substitution key by key, ascending): the fallback for
 // lists the wave path does not hold.
 __device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t sl, unsigned long long &by) {
@@ -1432,22 +1459,14 @@ __global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *
     unsigned long long t_2 = wall_clock64();
     unsigned long long by = 0;  // algorithmic bytes of this lane
     if (tid == 0) s_ok = 1;
-    // ---- normalize_substitutions: each lane batch-inverts the slots i = tid (mod nt)
-    if (tid < m) {
-      Fe acc = A.h_coef[b + tid];
-      A.ftmp[b + tid] = acc;
-      uint32_t last = tid;
-      for (uint32_t i = tid + nt; i < m; i += nt) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; last = i; }
-      Fe inv = finv(F, acc);
-      for (uint32_t i = last;; i -= nt) {
-        Fe inv_i = i >= tid + nt ? fmul(F, A.ftmp[b + i - nt], inv) : inv;
-        inv = fmul(F, inv, A.h_coef[b + i]);
-        Fe *vv = A.pv + A.h_off[b + i];
-        for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
-        by += 64ull * (A.h_len[b + i] + 1);
-        if (i < tid + nt) break;
-      }
+    // ---- normalize_substitutions (:414-437): the inverses come from k_batch_inv
+    for (uint32_t i = tid; i < m; i += nt) {
+      const Fe inv_i = A.ftmp[b + i];
+      Fe *vv = A.pv + A.h_off[b + i];
+      for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
+      by += 64ull * (A.h_len[b + i] + 1);
     }
+    __syncthreads();
     unsigned long long t_3 = wall_clock64();
     // ---- composition over the dependency DAG in Kahn order: a substitution is composed once every
     // deleted key of its right-hand side is final (the result does not depend on the order).
