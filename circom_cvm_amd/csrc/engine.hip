@@ -586,6 +586,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.bytes = E->A.get<unsigned long long>("el.bytes", 3);
     a.big_touch_off = E->A.get<uint64_t>("el.bt_off", std::max<uint64_t>(n_big, 1));
     a.big_touch_n = E->A.get<uint32_t>("el.bt_n", std::max<uint64_t>(n_big, 1));
+    a.big_alive = E->A.get<uint32_t>("el.alive", std::max<uint64_t>(n_big, 1));
     a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", 16 * n_big) : nullptr;
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
@@ -597,6 +598,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
     at.big_touch_off += n_head;
     at.big_touch_n += n_head;
+    at.big_alive += n_head;
     if (at.prof) at.prof += 16 * n_head;
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
@@ -610,7 +612,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_main, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
-        hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         hipLaunchKernelGGL(k_big_finish, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -687,6 +689,24 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.big_main_ms += m1;
         E->stats.big_finish_ms += m2;
         E->stats.big_launches++;
+      }
+      if (g_prof_env) {
+        float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if (n_tail) {
+          HC(hipEventElapsedTime(&t0, E->ev2, E->ev5));
+          HC(hipEventElapsedTime(&t1, E->ev5, E->ev6));
+          HC(hipEventElapsedTime(&t2, E->ev6, E->ev4));
+        }
+        HC(hipEventElapsedTime(&t3, E->ev4, E->evx[5]));
+        fprintf(stderr, "[rs-prof] tail(%llu): prep %.2f main %.2f inv+finish %.2f small %.2f", (unsigned long long)n_tail, t0, t1, t2, t3);
+        if (n_head) {
+          float h0 = 0, h1 = 0, h2 = 0;
+          HC(hipEventElapsedTime(&h0, E->evx[1], E->evx[2]));
+          HC(hipEventElapsedTime(&h1, E->evx[2], E->evx[3]));
+          HC(hipEventElapsedTime(&h2, E->evx[3], E->evx[4]));
+          fprintf(stderr, " | head(%llu): prep %.2f main %.2f inv+finish %.2f", (unsigned long long)n_head, h0, h1, h2);
+        }
+        fprintf(stderr, " | wall %.2f\n", ms);
       }
       if (n_head) {
         float m0 = 0, m1 = 0, m2 = 0;

@@ -304,6 +304,7 @@ struct ElimArgs {
   unsigned long long *prof;   // debug: 16 words per big cluster (see run_linear_simplification), or null
   uint64_t *big_touch_off;    // per big cluster: touched-signal list in the pool (k_big_prep)
   uint32_t *big_touch_n;
+  uint32_t *big_alive;        // per big cluster: #rows left for the ordered loop (listed in tmp), RS_NONE = all
 };
 
 __device__ __forceinline__ uint64_t pool_alloc_global(const ElimArgs &A, uint64_t n) {
@@ -732,7 +733,7 @@ __device__ __forceinline__ bool d_is_p4(const ElimArgs &A, uint32_t n) {
 }
 
 __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
-  __shared__ uint32_t s_m, s_touch, s_ok;
+  __shared__ uint32_t s_m, s_touch, s_ok, s_alive_part[256];
   __shared__ unsigned long long s_tot;
   __shared__ uint64_t s_touch_off;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -743,9 +744,8 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     const uint32_t n = (uint32_t)(e - b);
     unsigned long long t_0 = wall_clock64();
-    if (!d_is_p4(A, n)) {  // process_3: no occurrence bookkeeping
-      for (uint32_t pos = tid; pos < n; pos += nt) A.dead[b + pos] = 0;
-      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; }
+    if (!d_is_p4(A, n)) {  // process_3: no occurrence bookkeeping, every row goes to the loop
+      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; A.big_alive[ci] = RS_NONE; }
       continue;
     }
     uint64_t tot = 0;
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
     }
     __syncthreads();
     if (!s_ok) {
-      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; atomicOr(A.err, 8); }
+      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; A.big_alive[ci] = 0; atomicOr(A.err, 8); }
       __syncthreads();
       continue;
     }
@@ -820,6 +820,22 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
     }
     __syncthreads();
     for (uint32_t i = tid; i < s_m; i += nt) A.occ[A.h_sig[b + i]] = -1;  // remove_signal
+    {  // the rows left for the ordered loop, ascending (tmp[b ..]); order kept by a block scan
+      const uint32_t per = (n + nt - 1) / nt, lo = min(n, tid * per), hi = min(n, lo + per);
+      uint32_t cnt = 0;
+      for (uint32_t pos = lo; pos < hi; ++pos) cnt += A.dead[b + pos] ? 0 : 1;
+      s_alive_part[tid] = cnt;
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t q = 0; q < nt; ++q) { uint32_t x = s_alive_part[q]; s_alive_part[q] = acc; acc += x; }
+        A.big_alive[ci] = acc;
+      }
+      __syncthreads();
+      uint32_t w = s_alive_part[tid];
+      for (uint32_t pos = lo; pos < hi; ++pos)
+        if (!A.dead[b + pos]) A.tmp[b + w++] = pos;
+    }
     if (tid == 0) {
       A.n_sub[c] = s_m;
       A.big_touch_off[ci] = s_touch_off;
@@ -834,10 +850,10 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
   }
 }
 
-// The rest of one row's treat_constraint_4 loop on a work list in the pool (single lane; used when
-// a list does not fit the LDS buffers of k_big_main).
-__device__ inline bool d_treat4_scalar(const ElimArgs &A, Alloc &al, uint64_t b, const uint32_t *k, const Fe *v,
-                                       uint32_t len, uint32_t &m, uint32_t &nl) {
+// The rest of one row's treat_constraint_3/4 loop on a work list in the pool (single lane; used
+// when a list does not fit the LDS buffers of k_big_main).
+__device__ inline bool d_treat_scalar(const ElimArgs &A, Alloc &al, uint64_t b, const uint32_t *k, const Fe *v,
+                                      uint32_t len, uint32_t &m, uint32_t &nl, bool p4) {
   const FieldP &F = A.F;
   for (;;) {
     if (len == 0) return true;
@@ -846,6 +862,7 @@ __device__ inline bool d_treat4_scalar(const ElimArgs &A, Alloc &al, uint64_t b,
     for (uint32_t i = 0; i < len; ++i) {
       uint32_t s = k[i];
       if (A.forb[s]) continue;
+      if (!p4) { oi = i; continue; }  // take_signal_3: the max takeable key (keys ascending)
       if (A.del[s]) { oi = i; break; }
       int32_t c2 = A.occ[s];
       if (c2 < 0) { atomicOr(A.err, 16); c2 = 0; }
@@ -938,9 +955,11 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
-    for (uint64_t idx = e; idx-- > b;) {
+    const uint32_t n_alive = A.big_alive[ci];  // RS_NONE: process_3, every row
+    const uint32_t n_loop = n_alive == RS_NONE ? (uint32_t)(e - b) : n_alive;
+    for (uint32_t qi = n_loop; qi-- > 0;) {  // rows from the back (Vec::pop)
       if (!s_ok) break;
-      if (A.dead[idx]) continue;
+      const uint64_t idx = b + (n_alive == RS_NONE ? qi : A.tmp[b + qi]);
       ++rows;
       const uint32_t r = A.perm[idx];
       const uint32_t *k = A.rows.key + A.rows.off[r];
@@ -955,7 +974,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         __syncthreads();
         if (tid == 0) {
           uint32_t m = s_m, nl = s_nl;
-          if (!d_treat4_scalar(A, al0, b, k, v, len, m, nl)) s_ok = 0;
+          if (!d_treat_scalar(A, al0, b, k, v, len, m, nl, p4)) s_ok = 0;
           s_m = m;
           s_nl = nl;
         }
@@ -1084,7 +1103,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
             __syncthreads();
             if (tid == 0) {
               uint32_t m = s_m, nl = s_nl;
-              if (!d_treat4_scalar(A, al0, b, A.pk + o, A.pv + o, len, m, nl)) s_ok = 0;
+              if (!d_treat_scalar(A, al0, b, A.pk + o, A.pv + o, len, m, nl, p4)) s_ok = 0;
               s_m = m;
               s_nl = nl;
             }
@@ -1273,15 +1292,16 @@ __device__ inline uint32_t blk_excl_scan(uint32_t *a, uint32_t n, uint32_t *s_pa
 // before normalisation: one block per cluster, each lane inverts chunks of 64 slots with one
 // inversion per chunk (Montgomery's trick), so no cluster waits on an inversion chain of its own.
 // ftmp[slot] <- h_coef[slot]^-1.
-__global__ __launch_bounds__(64) void k_batch_inv(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+__global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
   const uint32_t tid = threadIdx.x;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c];
     const uint32_t m = A.n_sub[c];
-    for (uint32_t c0 = tid * 64; c0 < m; c0 += 64 * 64) {
-      const uint32_t c1 = min(m, c0 + 64);
+    const uint32_t C = max(64u, (m + blockDim.x - 1) / blockDim.x);  // one chunk per lane on big clusters
+    for (uint32_t c0 = tid * C; c0 < m; c0 += C * blockDim.x) {
+      const uint32_t c1 = min(m, c0 + C);
       Fe acc = A.h_coef[b + c0];
       A.ftmp[b + c0] = acc;
       for (uint32_t i = c0 + 1; i < c1; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
