@@ -198,6 +198,10 @@ static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, u
   return last_in + last_out;
 }
 
+__global__ void k_mark_u8(const uint32_t *ids, uint64_t n, uint8_t *flag) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) flag[ids[i]] = 1;
+}
+
 // apply_substitution_to_map (:369-377) appends every key of sub.to to the signal map when
 // map[from] is non-empty; only the key set survives the rounds (rebuild_witness), so it is kept as
 // bits.  A round's `from` signals never occur in its (non-overlapping) right-hand sides.
@@ -429,7 +433,7 @@ static Pool get_pool(rs_engine *E, uint64_t want) {
 // process_4 / lane split of the clusters (largest first). Only counts and the cluster offsets (for
 // the host-side round bookkeeping) come back to the host.
 struct DevClusters {
-  uint32_t *perm = nullptr, *big = nullptr, *small = nullptr;
+  uint32_t *perm = nullptr, *big = nullptr, *small = nullptr, *cid = nullptr;
   uint64_t *cl_off = nullptr;
   uint64_t n_slots = 0, n_big = 0, n_small = 0, tot_nnz = 0;
 };
@@ -526,6 +530,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   D.small = A.get<uint32_t>("el.small", D.n_small);
   if (D.n_small) launch(st, k_cl_small_ids, D.n_small, (const uint32_t *)sorted, n_cl, h, nb, D.small);
   D.n_slots = n_act;
+  D.cid = cid;
   eo.n_clusters = n_cl;
   eo.cl_off.resize(n_cl + 1);
   HC(hipMemcpyAsync(eo.cl_off.data(), D.cl_off, 8 * (n_cl + 1), hipMemcpyDeviceToHost, st));
@@ -544,7 +549,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   double t1 = now_ms();
   E->stats.cluster_ms += t1 - t0;
   const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz, n_big = D.n_big, n_small = D.n_small;
-  uint32_t *d_perm = D.perm, *d_big = D.big, *d_small = D.small;
+  uint32_t *d_perm = D.perm, *d_big = D.big, *d_small = D.small, *d_cid = D.cid;
   uint64_t *d_cl = D.cl_off;
   uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots)), E->pool_want);
   for (int attempt = 0; attempt < 8; ++attempt) {
@@ -614,7 +619,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipEventRecord(E->evx[3], E->st2));
         hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
-        hipLaunchKernelGGL(k_big_finish, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_big_finish<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[4], E->st2));
       }
@@ -629,9 +634,13 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev6, E->st));
-        hipLaunchKernelGGL(k_batch_inv, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
-        HC(hipGetLastError());
-        hipLaunchKernelGGL(k_big_finish, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
+        {  // tail clusters flagged in cls, then one inversion per 64 slots across clusters
+          uint8_t *cls = E->A.get<uint8_t>("el.cls", eo.n_clusters);
+          HC(hipMemsetAsync(cls, 0, eo.n_clusters, E->st));
+          launch(E->st, k_mark_u8, n_tail, ids, n_tail, cls);
+          launch(E->st, k_batch_inv_flat, (n_slots + 63) / 64, at, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
+        }
+        hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
       }
       HC(hipEventRecord(E->ev4, E->st));

@@ -1316,6 +1316,39 @@ __global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *i
   }
 }
 
+// The same over the slot space of many clusters at once (the tail stream's clusters, cls == 1):
+// chunks of 64 slots cross cluster boundaries, so tens of thousands of small clusters share a few
+// thousand inversions instead of waiting on one each.
+__device__ __forceinline__ bool d_inv_slot(const ElimArgs &A, const uint32_t *cid, const uint8_t *cls, uint64_t sl) {
+  const uint32_t c = cid[sl];
+  return cls[c] == 1 && sl - A.cl_off[c] < A.n_sub[c];
+}
+__global__ void k_batch_inv_flat(ElimArgs A, const uint32_t *cid, const uint8_t *cls, uint64_t n_slots) {
+  const FieldP &F = A.F;
+  for (uint64_t t = gtid(); t * 64 < n_slots; t += gstride()) {
+    const uint64_t s0 = t * 64, s1 = min<uint64_t>(n_slots, s0 + 64);
+    Fe acc = F.one;
+    uint64_t last = RS_NONE;
+    for (uint64_t sl = s0; sl < s1; ++sl) {
+      if (!d_inv_slot(A, cid, cls, sl)) continue;
+      acc = fmul(F, acc, A.h_coef[sl]);
+      A.ftmp[sl] = acc;  // prefix product up to sl
+      last = sl;
+    }
+    if (last == RS_NONE) continue;
+    Fe inv = finv(F, acc);
+    uint64_t cur = last;  // valid slot whose predecessor is being looked for
+    for (uint64_t sl = last; sl-- > s0;) {
+      if (!d_inv_slot(A, cid, cls, sl)) continue;
+      const Fe inv_cur = fmul(F, A.ftmp[sl], inv);
+      inv = fmul(F, inv, A.h_coef[cur]);
+      A.ftmp[cur] = inv_cur;
+      cur = sl;
+    }
+    A.ftmp[cur] = inv;
+  }
+}
+
 // Lane-serial composition of slot `sl` (raw_substitution key by key, ascending): the fallback for
 // lists the wave path does not hold.
 __device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t sl, unsigned long long &by) {
@@ -1458,14 +1491,15 @@ __device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, 
   return 0;
 }
 
-__global__ __launch_bounds__(256) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+template <int NW>  // waves per workgroup
+__global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
-  __shared__ uint32_t s_ok, s_nf, s_part[4];
-  __shared__ uint64_t cw_S[4][kComposeCap];  // per-wave composition buffers
-  __shared__ Fe cw_V[4][kComposeCap];
-  __shared__ uint32_t cw_dex[4][64];
-  __shared__ uint64_t cw_dof[4][64];
-  __shared__ Fe cw_dmu[4][64];
+  __shared__ uint32_t s_ok, s_nf, s_part[NW];
+  __shared__ uint64_t cw_S[NW][kComposeCap];  // per-wave composition buffers
+  __shared__ Fe cw_V[NW][kComposeCap];
+  __shared__ uint32_t cw_dex[NW][64];
+  __shared__ uint64_t cw_dof[NW][64];
+  __shared__ Fe cw_dmu[NW][64];
   __shared__ uint64_t s_scr;
   __shared__ unsigned long long s_hsum, s_hmax;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
