@@ -592,6 +592,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.big_touch_off = E->A.get<uint64_t>("el.bt_off", std::max<uint64_t>(n_big, 1));
     a.big_touch_n = E->A.get<uint32_t>("el.bt_n", std::max<uint64_t>(n_big, 1));
     a.big_alive = E->A.get<uint32_t>("el.alive", std::max<uint64_t>(n_big, 1));
+    a.row_off = E->A.get<uint64_t>("el.row_off", n_slots);
+    a.row_len = E->A.get<uint32_t>("el.row_len", n_slots);
+
     a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", 16 * n_big) : nullptr;
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
@@ -750,7 +753,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 8); ++q) {
         unsigned long long *p = &pf[16 * ix[q]];
         fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu iters=%llu  %.1f / %.1f / %.1f / %.1f  merges=%llu mwork=%llu "
-                "rhs_sum=%llu rhs_max=%llu touched=%llu | pivot %.1f hold+stage %.1f merge %.1f us\n", p[0], p[1], p[2], p[3],
+                "rowstart|rhs_sum=%llu newsub|rhs_max=%llu touched=%llu | pivot %.1f hold+stage %.1f merge %.1f us\n", p[0], p[1], p[2], p[3],
                 p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0, p[8], p[9], p[10], p[11], p[12],
                 p[13] / 100.0, p[14] / 100.0, p[15] / 100.0);
       }

@@ -304,9 +304,21 @@ struct ElimArgs {
   unsigned long long *prof;   // debug: 16 words per big cluster (see run_linear_simplification), or null
   uint64_t *big_touch_off;    // per big cluster: touched-signal list in the pool (k_big_prep)
   uint32_t *big_touch_n;
-  uint32_t *big_alive;        // per big cluster: #rows left for the ordered loop (listed in tmp), RS_NONE = all
+  uint32_t *big_alive;        // per big cluster: #rows left for the ordered loop
+  uint64_t *row_off;          // per slot: (offset, length) of those rows in loop order (k_big_prep)
+  uint32_t *row_len;
+
 };
 
+// Registers substitution `slot` for signal p (holder.insert): slot arrays + the dense per-signal copy
+__device__ __forceinline__ void d_set_holder(const ElimArgs &A, uint32_t p, uint64_t slot, const Fe &coef, uint64_t off,
+                                             uint32_t len) {
+  A.holder_idx[p] = (int32_t)slot;
+  A.h_sig[slot] = p;
+  A.h_coef[slot] = coef;
+  A.h_off[slot] = off;
+  A.h_len[slot] = len;
+}
 __device__ __forceinline__ uint64_t pool_alloc_global(const ElimArgs &A, uint64_t n) {
   unsigned long long o = atomicAdd(A.pool_top, (unsigned long long)n);
   if (o + n > A.pool_cap) { atomicOr(A.err, 8); return RS_NONE; }
@@ -745,7 +757,12 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
     const uint32_t n = (uint32_t)(e - b);
     unsigned long long t_0 = wall_clock64();
     if (!d_is_p4(A, n)) {  // process_3: no occurrence bookkeeping, every row goes to the loop
-      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; A.big_alive[ci] = RS_NONE; }
+      for (uint32_t pos = tid; pos < n; pos += nt) {
+        const uint32_t r = A.perm[b + pos];
+        A.row_off[b + pos] = A.rows.off[r];
+        A.row_len[b + pos] = A.rows.len[r];
+      }
+      if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; A.big_alive[ci] = n; }
       continue;
     }
     uint64_t tot = 0;
@@ -811,11 +828,7 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
       if (!d_clear_nn(A, al, k, v, A.rows.len[r], oi, coef, to_off, to_len)) { s_ok = 0; continue; }
       uint32_t slot = atomicAdd(&s_m, 1u);
       uint32_t s = k[oi];
-      A.holder_idx[s] = (int32_t)(b + slot);
-      A.h_sig[b + slot] = s;
-      A.h_coef[b + slot] = coef;
-      A.h_off[b + slot] = to_off;
-      A.h_len[b + slot] = to_len;
+      d_set_holder(A, s, b + slot, coef, to_off, to_len);
       A.del[s] = 1;
     }
     __syncthreads();
@@ -834,7 +847,12 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
       __syncthreads();
       uint32_t w = s_alive_part[tid];
       for (uint32_t pos = lo; pos < hi; ++pos)
-        if (!A.dead[b + pos]) A.tmp[b + w++] = pos;
+        if (!A.dead[b + pos]) {
+          const uint32_t r = A.perm[b + pos];
+          A.row_off[b + w] = A.rows.off[r];
+          A.row_len[b + w] = A.rows.len[r];
+          ++w;
+        }
     }
     if (tid == 0) {
       A.n_sub[c] = s_m;
@@ -843,7 +861,7 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
         unsigned long long *P = A.prof + 16 * ci;
-        P[0] = n; P[4] = wall_clock64() - t_0; P[12] = n_touch;
+        P[0] = n; P[4] = wall_clock64() - t_0;
       }
     }
     __syncthreads();
@@ -885,11 +903,7 @@ __device__ inline bool d_treat_scalar(const ElimArgs &A, Alloc &al, uint64_t b, 
       uint64_t to_off;
       uint32_t to_len;
       if (!d_clear_nn(A, al, k, v, len, oi, coef, to_off, to_len)) return false;
-      A.holder_idx[out] = (int32_t)(b + m);
-      A.h_sig[b + m] = out;
-      A.h_coef[b + m] = coef;
-      A.h_off[b + m] = to_off;
-      A.h_len[b + m] = to_len;
+      d_set_holder(A, out, b + m, coef, to_off, to_len);
       ++m;
       A.occ[out] = -1;
       A.del[out] = 1;
@@ -951,20 +965,23 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     unsigned long long t_1 = wall_clock64();
     unsigned long long merges = 0, mwork = 0, rows = 0, by = 0;  // by: algorithmic bytes (lane 0)
-    unsigned long long tp_piv = 0, tp_hold = 0, tp_merge = 0, tp_x;  // debug phase clocks (A.prof)
+    unsigned long long tp_piv = 0, tp_hold = 0, tp_merge = 0, tp_x, tp_row = 0, tp_new = 0, tp_r0;  // debug clocks
+    unsigned long long tp_q[4] = {0, 0, 0, 0};
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
-    const uint32_t n_alive = A.big_alive[ci];  // RS_NONE: process_3, every row
-    const uint32_t n_loop = n_alive == RS_NONE ? (uint32_t)(e - b) : n_alive;
+    const uint32_t n_loop = A.big_alive[ci];
+    uint64_t nx_off = n_loop ? A.row_off[b + n_loop - 1] : 0;  // descriptor of the next row, one ahead
+    uint32_t nx_len = n_loop ? A.row_len[b + n_loop - 1] : 0;
     for (uint32_t qi = n_loop; qi-- > 0;) {  // rows from the back (Vec::pop)
       if (!s_ok) break;
-      const uint64_t idx = b + (n_alive == RS_NONE ? qi : A.tmp[b + qi]);
       ++rows;
-      const uint32_t r = A.perm[idx];
-      const uint32_t *k = A.rows.key + A.rows.off[r];
-      const Fe *v = A.rows.val + A.rows.off[r];
-      uint32_t len = A.rows.len[r];
+      tp_r0 = wall_clock64();
+      const uint64_t r_off = nx_off;
+      uint32_t len = nx_len;
+      if (qi) { nx_off = A.row_off[b + qi - 1]; nx_len = A.row_len[b + qi - 1]; }
+      const uint32_t *k = A.rows.key + r_off;
+      const Fe *v = A.rows.val + r_off;
       by += 36ull * len;
       for (uint32_t i = tid; i < len; i += nt) {  // remove_constraint (keys of a row are distinct)
         uint32_t s = k[i];
@@ -984,6 +1001,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       for (uint32_t i = tid; i < len; i += nt) { wk[0][i] = k[i]; wv[0][i] = v[i]; }
       uint32_t cur = 0;
       __syncthreads();
+      tp_row += wall_clock64() - tp_r0;
       while (len > 0) {
         tp_x = wall_clock64();
         // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
@@ -998,8 +1016,9 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           if (tid < len && !A.forb[key]) {
             tk = true;
             dl = A.del[key] != 0;
-            if (dl) hsl = A.holder_idx[key];  // fetched speculatively with the pivot search
-            else if (p4) {
+            if (dl) {  // fetched speculatively with the pivot search
+              hsl = A.holder_idx[key];
+            } else if (p4) {
               oc = A.occ[key];
               if (oc < 0) { atomicOr(A.err, 16); oc = 0; }
             }
@@ -1057,6 +1076,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         }
         const uint32_t p = wk[cur][oi];
         if (!conflict) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
+          const unsigned long long tn0 = wall_clock64();
           const uint32_t sh = wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
           const uint32_t mm = len - 1 + sh;
           by += 36ull * mm;
@@ -1072,18 +1092,14 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
             }
             if (tid == 0) {
               if (sh) { A.pk[o] = 0; A.pv[o] = fe_zero(); }
-              const uint64_t slot = b + s_m;
-              A.holder_idx[p] = (int32_t)slot;
-              A.h_sig[slot] = p;
-              A.h_coef[slot] = fneg(F, wv[cur][oi]);
-              A.h_off[slot] = o;
-              A.h_len[slot] = mm;
+              d_set_holder(A, p, b + s_m, fneg(F, wv[cur][oi]), o, mm);
               s_m = s_m + 1;
               A.occ[p] = -1;
               A.del[p] = 1;
             }
           }
           __syncthreads();
+          tp_new += wall_clock64() - tn0;
           break;
         }
         { unsigned long long t = wall_clock64(); tp_piv += t - tp_x; tp_x = t; }
@@ -1124,21 +1140,34 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           Fe val = fe_zero();
           if (isw) { key = wk[cur][l]; val = wv[cur][l]; }
           if (isr) { key = A.pk[roff + j]; val = A.pv[roff + j]; }
+          const unsigned long long tq0 = wall_clock64();
           if (isw || isr) val = fmul(F, isw ? c2 : coef, val);
+          const unsigned long long tq1 = wall_clock64();
           if (isr) { rk[j] = key; rv[j] = val; }
           __syncthreads();
+          const unsigned long long tq2 = wall_clock64();
+          tp_q[0] += tq0 - tp_x;  // loads
+          tp_q[1] += tq1 - tq0;   // product
+          tp_q[2] += tq2 - tq1;   // barrier
+          // one search per lane in the other list (work lanes in the RHS, RHS lanes in the work)
           bool keep = false;
           uint32_t lb = 0;
-          if (isw && l != oi) {  // -c2*v (+ coef*rv when the RHS has the key)
-            lb = lds_lower_bound(rk, rl, key);
-            val = fneg(F, val);
-            if (lb < rl && rk[lb] == key) val = fadd(F, rv[lb], val);
-            keep = !fe_is_zero(val);
+          if (isw || isr) {
+            const uint32_t *ok = isw ? rk : wk[cur];
+            const uint32_t on = isw ? rl : len;
+            lb = lds_lower_bound(ok, on, key);
+            const bool hit = lb < on && ok[lb] == key;
+            if (isw) {  // -c2*v (+ coef*rv when the RHS has the key)
+              if (l != oi) {
+                val = hit ? fsub(F, rv[lb], val) : fneg(F, val);
+                keep = !fe_is_zero(val);
+              }
+            } else {  // RHS-only keys: coef*rv
+              keep = !hit && !fe_is_zero(val);
+            }
           }
-          if (isr) {  // RHS-only keys: coef*rv
-            lb = lds_lower_bound(wk[cur], len, key);
-            keep = !(lb < len && wk[cur][lb] == key) && !fe_is_zero(val);
-          }
+          const unsigned long long tq3 = wall_clock64();
+          tp_q[3] += tq3 - tq2;  // lookups
           const uint64_t km = __ballot(keep);
           const uint64_t wmk = len >= 64 ? km : (km & ((1ull << len) - 1ull)), rmk = km >> len;
           auto below = [](uint64_t m, uint32_t k) -> uint32_t {
@@ -1259,7 +1288,8 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       if (A.prof) {
         unsigned long long *P = A.prof + 16 * ci;
         P[2] = rows; P[5] = wall_clock64() - t_1; P[8] = merges; P[9] = mwork;
-        P[13] = tp_piv; P[14] = tp_hold; P[15] = tp_merge;
+        P[13] = tp_piv; P[14] = tp_hold; P[15] = tp_merge; P[10] = tp_row; P[11] = tp_new;
+        P[8] = tp_q[0]; P[9] = tp_q[1]; P[3] = tp_q[2]; P[12] = tp_q[3];
       }
     }
     __syncthreads();
@@ -1627,7 +1657,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
         unsigned long long *P = A.prof + 16 * ci;
-        P[1] = m; P[3] = levels; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3; P[10] = s_hsum; P[11] = s_hmax;
+        P[1] = m; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3;
       }
     }
     __syncthreads();
