@@ -1,8 +1,9 @@
 // field.hpp -- F_p arithmetic for the device (and host helpers), p < 2^256 odd.
 //
 // Replaces circom_algebra/src/modular_arithmetic.rs:9-91 (num-bigint-dig BigInt + double
-// remainder per op) with fixed 4x64-bit limbs in Montgomery form (R = 2^256): one CIOS product
-// per field multiplication, carry-propagating add/sub with a single conditional correction.
+// remainder per op) with residues stored as 4 x 64-bit limbs in Montgomery form (R = 2^261): one
+// radix-2^29 Montgomery product per field multiplication, carry-propagating add/sub with a single
+// conditional correction.
 // Results are canonical residues, identical to the reference's ((a % p) + p) % p.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -17,10 +18,15 @@ struct __attribute__((aligned(16))) Fe {
   uint64_t l[4];
 };
 
+constexpr int kLimbBits = 29;  // Montgomery radix 2^29, 9 limbs, R = 2^261
+constexpr int kLimbs = 9;
+constexpr uint32_t kLimbMask = (1u << kLimbBits) - 1;
+
 struct FieldP {
   uint64_t p[4];
-  uint64_t np;  // -p^-1 mod 2^64
-  Fe r2;        // R^2 mod p
+  uint32_t pl[kLimbs];  // p in 29-bit limbs
+  uint32_t np;          // -p^-1 mod 2^29
+  Fe r2;        // R^2 mod p  (R = 2^261)
   Fe one;       // R mod p
   Fe pm2;       // p - 2 (Fermat exponent)
   Fe r3;        // R^3 mod p (Montgomery-form inverse from a plain binary GCD)
@@ -81,53 +87,66 @@ __host__ __device__ __forceinline__ Fe fneg(const FieldP &F, const Fe &a) {
   sub4(r.l, F.p, a.l);
   return r;
 }
-// CIOS Montgomery product over 8 x 32-bit limbs: every step is one 32x32+64 multiply-add, which
-// gfx950 issues natively (v_mad_u64_u32); 30 % lower dependent latency than 4 x 64-bit limbs
-// through unsigned __int128 (tools/micro/fmul_bench.hip: 1.08 vs 1.55 us per product, one wave).
+// 256-bit values <-> 9 limbs of 29 bits
+__host__ __device__ __forceinline__ void to_limbs(const Fe &x, uint32_t *a) {
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) {
+    const int bit = kLimbBits * i, w = bit >> 6, s = bit & 63;
+    uint64_t v = x.l[w] >> s;
+    if (s > 64 - kLimbBits && w < 3) v |= x.l[w + 1] << (64 - s);
+    a[i] = (uint32_t)v & kLimbMask;
+  }
+}
+// Montgomery product a*b*2^-261 mod p, radix 2^29: the 81 limb products of each half go into
+// 64-bit column accumulators with independent multiply-adds (no carry chain inside a column; a
+// column holds at most 18 products < 2^58), then 9 reduction steps and one carry pass.  44 % lower
+// dependent latency than a 8 x 32-bit CIOS on gfx950 (tools/micro/fmul28.hip: 0.60 vs 1.09 us
+// per product for one wave), which is what the ordered elimination loop waits on.
 __host__ __device__ __forceinline__ Fe fmul(const FieldP &F, const Fe &A, const Fe &B) {
-  uint32_t a[8], b[8], p[8], t[10];
+  uint32_t a[kLimbs], b[kLimbs];
+  to_limbs(A, a);
+  to_limbs(B, b);
+  uint64_t T[2 * kLimbs];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    a[2 * i] = (uint32_t)A.l[i];
-    a[2 * i + 1] = (uint32_t)(A.l[i] >> 32);
-    b[2 * i] = (uint32_t)B.l[i];
-    b[2 * i + 1] = (uint32_t)(B.l[i] >> 32);
-    p[2 * i] = (uint32_t)F.p[i];
-    p[2 * i + 1] = (uint32_t)(F.p[i] >> 32);
+  for (int k = 0; k < 2 * kLimbs; ++k) T[k] = 0;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i)
+#pragma unroll
+    for (int j = 0; j < kLimbs; ++j) T[i + j] += (uint64_t)a[i] * b[j];
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) {
+    const uint32_t m = ((uint32_t)T[i] * F.np) & kLimbMask;
+#pragma unroll
+    for (int j = 0; j < kLimbs; ++j) T[i + j] += (uint64_t)m * F.pl[j];
+    T[i + 1] += T[i] >> kLimbBits;
   }
-  const uint32_t np = (uint32_t)F.np;  // -p^-1 mod 2^32 (low word of -p^-1 mod 2^64)
+  uint32_t r[kLimbs];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t c = 0, s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s = (uint64_t)a[j] * b[i] + t[j] + c;
-      t[j] = (uint32_t)s;
-      c = s >> 32;
-    }
-    s = (uint64_t)t[8] + c;
-    t[8] = (uint32_t)s;
-    t[9] = (uint32_t)(s >> 32);
-    const uint32_t m = t[0] * np;
-    s = (uint64_t)m * p[0] + t[0];
-    c = s >> 32;
-#pragma unroll
-    for (int j = 1; j < 8; ++j) {
-      s = (uint64_t)m * p[j] + t[j] + c;
-      t[j - 1] = (uint32_t)s;
-      c = s >> 32;
-    }
-    s = (uint64_t)t[8] + c;
-    t[7] = (uint32_t)s;
-    t[8] = t[9] + (uint32_t)(s >> 32);
+  for (int k = kLimbs; k < 2 * kLimbs - 1; ++k) {
+    T[k + 1] += T[k] >> kLimbBits;
+    r[k - kLimbs] = (uint32_t)T[k] & kLimbMask;
   }
-  Fe r;
+  r[kLimbs - 1] = (uint32_t)T[2 * kLimbs - 1];
+  // r < 2p: one conditional subtraction, limb-wise with borrow
+  uint32_t d[kLimbs];
+  int64_t br = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) r.l[i] = (uint64_t)t[2 * i] | ((uint64_t)t[2 * i + 1] << 32);
-  if (t[8] || geq4(r.l, F.p)) sub4(r.l, r.l, F.p);
-  return r;
+  for (int k = 0; k < kLimbs; ++k) {
+    const int64_t x = (int64_t)r[k] - F.pl[k] + br;
+    d[k] = (uint32_t)x & kLimbMask;
+    br = x >> kLimbBits;
+  }
+  const bool ge = br >= 0;
+  Fe o;
+  o.l[0] = o.l[1] = o.l[2] = o.l[3] = 0;
+#pragma unroll
+  for (int k = 0; k < kLimbs; ++k) {
+    const uint64_t v = ge ? d[k] : r[k];
+    const int bit = kLimbBits * k, w = bit >> 6, s = bit & 63;
+    o.l[w] |= v << s;
+    if (s > 64 - kLimbBits && w < 3) o.l[w + 1] |= v >> (64 - s);
+  }
+  return o;
 }
 __host__ __device__ __forceinline__ Fe fto_mont(const FieldP &F, const Fe &c) { return fmul(F, c, F.r2); }
 __host__ __device__ __forceinline__ Fe ffrom_mont(const FieldP &F, const Fe &a) {
@@ -191,14 +210,18 @@ __host__ __device__ inline Fe finv(const FieldP &F, const Fe &a) {
 inline FieldP make_field(const uint64_t prime[4]) {
   FieldP F;
   for (int i = 0; i < 4; ++i) F.p[i] = prime[i];
-  uint64_t inv = 1;
-  for (int i = 0; i < 7; ++i) inv *= 2 - F.p[0] * inv;
-  F.np = (uint64_t)0 - inv;
+  Fe pf;
+  for (int i = 0; i < 4; ++i) pf.l[i] = prime[i];
+  to_limbs(pf, F.pl);
+  uint32_t inv = 1;  // p^-1 mod 2^29 (Newton)
+  for (int i = 0; i < 5; ++i) inv *= 2 - F.pl[0] * inv;
+  F.np = (0u - inv) & kLimbMask;
   uint64_t x[4] = {1, 0, 0, 0};
-  for (int i = 0; i < 512; ++i) {
+  const int rb = kLimbBits * kLimbs;  // R = 2^rb
+  for (int i = 0; i < 2 * rb; ++i) {
     uint64_t c = add4(x, x, x);
     if (c || geq4(x, F.p)) sub4(x, x, F.p);
-    if (i == 255)
+    if (i == rb - 1)
       for (int j = 0; j < 4; ++j) F.one.l[j] = x[j];
   }
   for (int j = 0; j < 4; ++j) F.r2.l[j] = x[j];
