@@ -963,11 +963,14 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
-    unsigned long long t_1 = wall_clock64();
+    unsigned long long t_1 = 0;
     unsigned long long merges = 0, mwork = 0, rows = 0, by = 0;  // by: algorithmic bytes (lane 0)
     unsigned long long tp_piv = 0, tp_hold = 0, tp_merge = 0, tp_x, tp_row = 0, tp_new = 0, tp_r0;  // debug clocks
     unsigned long long tp_q[4] = {0, 0, 0, 0};
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));
+    const bool prof = A.prof != nullptr;
+    auto clk = [prof]() -> unsigned long long { return prof ? wall_clock64() : 0ull; };
+    t_1 = clk();
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
     const uint32_t n_loop = A.big_alive[ci];
@@ -976,7 +979,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     for (uint32_t qi = n_loop; qi-- > 0;) {  // rows from the back (Vec::pop)
       if (!s_ok) break;
       ++rows;
-      tp_r0 = wall_clock64();
+      tp_r0 = clk();
       const uint64_t r_off = nx_off;
       uint32_t len = nx_len;
       if (qi) { nx_off = A.row_off[b + qi - 1]; nx_len = A.row_len[b + qi - 1]; }
@@ -1001,9 +1004,9 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       for (uint32_t i = tid; i < len; i += nt) { wk[0][i] = k[i]; wv[0][i] = v[i]; }
       uint32_t cur = 0;
       __syncthreads();
-      tp_row += wall_clock64() - tp_r0;
+      tp_row += clk() - tp_r0;
       while (len > 0) {
-        tp_x = wall_clock64();
+        tp_x = clk();
         // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
         // -> max id.  take_signal_3 (:368-377): the max takeable key; a conflict iff it is deleted.
         uint32_t oi = RS_NONE;
@@ -1076,7 +1079,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         }
         const uint32_t p = wk[cur][oi];
         if (!conflict) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
-          const unsigned long long tn0 = wall_clock64();
+          const unsigned long long tn0 = clk();
           const uint32_t sh = wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
           const uint32_t mm = len - 1 + sh;
           by += 36ull * mm;
@@ -1099,10 +1102,10 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
             }
           }
           __syncthreads();
-          tp_new += wall_clock64() - tn0;
+          tp_new += clk() - tn0;
           break;
         }
-        { unsigned long long t = wall_clock64(); tp_piv += t - tp_x; tp_x = t; }
+        { unsigned long long t = clk(); tp_piv += t - tp_x; tp_x = t; }
         // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p); every lane reads the
         // holder's words itself (same addresses: one request per wave)
         const uint64_t roff = A.h_off[hs];
@@ -1127,7 +1130,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           __syncthreads();
           break;
         }
-        { unsigned long long t = wall_clock64(); tp_hold += t - tp_x; tp_x = t; }
+        { unsigned long long t = clk(); tp_hold += t - tp_x; tp_x = t; }
         const Fe coef = fneg(F, wv[cur][oi]);
         const uint32_t nx = cur ^ 1;
         if (len + rl <= 64) {
@@ -1140,12 +1143,12 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           Fe val = fe_zero();
           if (isw) { key = wk[cur][l]; val = wv[cur][l]; }
           if (isr) { key = A.pk[roff + j]; val = A.pv[roff + j]; }
-          const unsigned long long tq0 = wall_clock64();
+          const unsigned long long tq0 = clk();
           if (isw || isr) val = fmul(F, isw ? c2 : coef, val);
-          const unsigned long long tq1 = wall_clock64();
+          const unsigned long long tq1 = clk();
           if (isr) { rk[j] = key; rv[j] = val; }
           __syncthreads();
-          const unsigned long long tq2 = wall_clock64();
+          const unsigned long long tq2 = clk();
           tp_q[0] += tq0 - tp_x;  // loads
           tp_q[1] += tq1 - tq0;   // product
           tp_q[2] += tq2 - tq1;   // barrier
@@ -1166,7 +1169,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
               keep = !hit && !fe_is_zero(val);
             }
           }
-          const unsigned long long tq3 = wall_clock64();
+          const unsigned long long tq3 = clk();
           tp_q[3] += tq3 - tq2;  // lookups
           const uint64_t km = __ballot(keep);
           const uint64_t wmk = len >= 64 ? km : (km & ((1ull << len) - 1ull)), rmk = km >> len;
@@ -1182,7 +1185,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           const uint32_t nlen = (uint32_t)__popcll(km);
           cur = nx;
           by += 36ull * (len + rl + nlen);
-          tp_merge += wall_clock64() - tp_x;
+          tp_merge += clk() - tp_x;
           len = nlen;
           continue;
         }
@@ -1227,7 +1230,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           const uint32_t nlen = (uint32_t)(__popcll(wmk) + __popcll(rmk));
           cur = nx;
           by += 36ull * (len + rl + nlen);
-          tp_merge += wall_clock64() - tp_x;
+          tp_merge += clk() - tp_x;
           len = nlen;
           continue;
         }
@@ -1276,7 +1279,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         __syncthreads();
         cur = nx;
         by += 36ull * (len + rl + tw + tr);
-        tp_merge += wall_clock64() - tp_x;
+        tp_merge += clk() - tp_x;
         len = tw + tr;
       }
     }
@@ -1287,7 +1290,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
         unsigned long long *P = A.prof + 16 * ci;
-        P[2] = rows; P[5] = wall_clock64() - t_1; P[8] = merges; P[9] = mwork;
+        P[2] = rows; P[5] = clk() - t_1; P[8] = merges; P[9] = mwork;
         P[13] = tp_piv; P[14] = tp_hold; P[15] = tp_merge; P[10] = tp_row; P[11] = tp_new;
         P[8] = tp_q[0]; P[9] = tp_q[1]; P[3] = tp_q[2]; P[12] = tp_q[3];
       }
