@@ -21,6 +21,7 @@ constexpr uint32_t kClNoPrev = 0x7fffffffu;
 constexpr uint32_t kClSmall = 64;     // clusters up to this size: one lane each
 constexpr uint32_t kClLds = 32768;    // clusters up to this size: LDS replay (u16 local ids)
 constexpr uint32_t kClChunk = 4096;   // stream entries staged per LDS chunk
+constexpr uint32_t kClMid = 2048;     // mid-size clusters: replay with a small LDS footprint
 constexpr uint32_t kWaveMin = 32;     // clusters from this size on are eliminated by the workgroup kernels
 
 // pairs per row (non-constant keys) and the active-row statistics
@@ -32,8 +33,15 @@ __global__ void k_cl_count(DRows V, uint64_t *npairs, unsigned long long *stat /
     nnz += len;
     act += len ? 1 : 0;
   }
-  if (nnz) atomicAdd(&stat[0], nnz);
-  if (act) atomicAdd(&stat[1], act);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {  // one atomic per wave
+    nnz += __shfl_xor(nnz, d);
+    act += __shfl_xor(act, d);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (nnz) atomicAdd(&stat[0], nnz);
+    if (act) atomicAdd(&stat[1], act);
+  }
 }
 __global__ void k_cl_fill(DRows V, const uint64_t *poff, uint64_t *pkey, uint32_t *pslot) {
   for (uint64_t r = gtid(); r < V.n; r += gstride()) {
@@ -159,12 +167,16 @@ __global__ void k_cl_replay_lane(const uint64_t *cl_off, uint64_t n_cl, const ui
   }
 }
 
-// workgroup replay with the union-find state in LDS (kClSmall < n <= kClLds); `ids` lists them
+// workgroup replay with the union-find state in LDS (kClSmall < n <= CAP); `ids` lists them.  Two
+// instantiations: CAP = kClLds (150 KB of LDS, one workgroup per CU) for the large clusters and
+// CAP = kClMid (small LDS footprint, many workgroups per CU) for the many mid-size ones.
+template <uint32_t CAP, uint32_t CHUNK>
 __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, const uint32_t *ids, uint64_t n_ids,
                                                        const uint64_t *q_off, const uint32_t *stream,
                                                        const uint32_t *srow, uint32_t *next, uint32_t *perm,
                                                        const uint32_t *n_ordered, int old_heur) {
-  __shared__ uint16_t C2[kClLds], T[kClLds];
+  constexpr uint32_t kClChunk = CHUNK;
+  __shared__ uint16_t C2[CAP], T[CAP];
   __shared__ uint32_t S[kClChunk];
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
@@ -178,30 +190,40 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
     const uint64_t q0 = q_off[b], q1 = q_off[b + n];
     uint32_t *N = next + b;
     int32_t t = -1;  // lane 0: current row
+    uint32_t tail = 0;
     for (uint64_t qc = q0; qc < q1; qc += kClChunk) {
       const uint32_t m = (uint32_t)min<uint64_t>(kClChunk, q1 - qc);
       __syncthreads();
       for (uint32_t i = tid; i < m; i += nt) S[i] = stream[qc + i];
       __syncthreads();
       if (tid == 0) {
+        // the current row's list tail lives in a register; T[] holds the tails of earlier roots
         for (uint32_t i = 0; i < m; ++i) {
-          uint32_t e = S[i];
+          const uint32_t e = S[i];
           if (e & kClRowBit) {
+            if (t >= 0) T[t] = (uint16_t)tail;
             ++t;
             C2[t] = (uint16_t)t;
-            T[t] = (uint16_t)t;
             N[t] = RS_NONE;
+            tail = (uint32_t)t;
           }
           uint32_t p = e & ~kClRowBit;
           if (p == kClNoPrev) continue;
-          while (C2[p] != p) { uint32_t g = C2[C2[p]]; C2[p] = (uint16_t)g; p = g; }
+          uint32_t q = C2[p];
+          while (q != p) {  // path halving
+            const uint32_t g = C2[q];
+            C2[p] = (uint16_t)g;
+            p = q == g ? q : g;
+            q = C2[p];
+          }
           if (p == (uint32_t)t) continue;
-          N[T[t]] = p;
-          T[t] = T[p];
+          N[tail] = p;
+          tail = T[p];
           C2[p] = (uint16_t)t;
         }
       }
     }
+    if (tid == 0 && t >= 0) T[t] = (uint16_t)tail;
     __syncthreads();
     // next -> LDS (C2 is free now), walk from the root (the last row), gather the rows
     for (uint32_t i = tid; i < n; i += nt) { uint32_t x = N[i]; C2[i] = (uint16_t)(x == RS_NONE ? 0xffffu : x); }
@@ -218,7 +240,7 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
 
 // cluster-size classes for the elimination kernels: sorted by (size desc, index)
 __global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, uint64_t *skey, uint32_t *sidx,
-                             unsigned long long *cnt /* [0] >= 1e6, [1] workgroup kernels, [2] LDS replay, [3] > LDS */) {
+                             unsigned long long *cnt /* [0] >= 1e6, [1] workgroup kernels, [2] LDS replay, [3] > LDS, [4] large LDS replay */) {
   for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
     uint64_t sz = cl_off[c + 1] - cl_off[c];
     skey[c] = ((uint64_t)(0xffffffffu - (uint32_t)sz) << 32) | c;
@@ -227,6 +249,7 @@ __global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, uint64_t *sk
     if (sz >= kWaveMin) atomicAdd(&cnt[1], 1ull);
     if (sz > kClSmall && sz <= kClLds) atomicAdd(&cnt[2], 1ull);
     if (sz > kClLds) atomicAdd(&cnt[3], 1ull);
+    if (sz > kClMid && sz <= kClLds) atomicAdd(&cnt[4], 1ull);
   }
 }
 // small list = sorted[0, h) ++ sorted[h + nb, n_cl)

@@ -502,9 +502,9 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   unsigned long long *cnt = stat + 2;
   launch(st, k_cl_sizekey, n_cl, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt);
   sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
-  unsigned long long hc[4];
+  unsigned long long hc[5];
   uint64_t first = 0;
-  HC(hipMemcpyAsync(hc, cnt, 32, hipMemcpyDeviceToHost, st));
+  HC(hipMemcpyAsync(hc, cnt, 40, hipMemcpyDeviceToHost, st));
   HC(hipMemcpyAsync(&first, sk2, 8, hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
   // replay of the arena merges -> row order inside every cluster
@@ -514,9 +514,17 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   launch(st, k_cl_replay_lane, n_cl, (const uint64_t *)D.cl_off, n_cl, (const uint64_t *)q_off,
          (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm, (const uint32_t *)n_ordered,
          old_heur);
-  if (hc[2]) {
-    hipLaunchKernelGGL(k_cl_replay_lds, dim3((unsigned)std::min<uint64_t>(hc[2], 4096)), dim3(256), 0, st,
-                       (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[2],
+  if (hc[4]) {  // (kClMid, kClLds]: the largest LDS footprint
+    hipLaunchKernelGGL((k_cl_replay_lds<kClLds, kClChunk>), dim3((unsigned)std::min<uint64_t>(hc[4], 4096)), dim3(256), 0, st,
+                       (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[4],
+                       (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
+                       (const uint32_t *)n_ordered, old_heur);
+    HC(hipGetLastError());
+  }
+  if (hc[2] > hc[4]) {  // (kClSmall, kClMid]
+    const uint64_t nm = hc[2] - hc[4];
+    hipLaunchKernelGGL((k_cl_replay_lds<kClMid, 1024>), dim3((unsigned)std::min<uint64_t>(nm, 16384)), dim3(256), 0, st,
+                       (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3] + hc[4]), nm,
                        (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
                        (const uint32_t *)n_ordered, old_heur);
     HC(hipGetLastError());

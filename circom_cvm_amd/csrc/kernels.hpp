@@ -1775,7 +1775,9 @@ __global__ void k_nl_fill(NLArgs A) {
     A.oc.len[r] = nc;
     bytes += 36ull * (A.a.len[r] + A.b.len[r] + A.c.len[r] + na + nb + nc) + 24;
   }
-  atomicAdd(A.bytes, bytes);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) bytes += __shfl_xor(bytes, d);  // one atomic per wave
+  if ((threadIdx.x & 63) == 0 && bytes) atomicAdd(A.bytes, bytes);
 }
 
 // ---------------------------------------------------------------- rounds >= 2 on the storage
