@@ -58,6 +58,45 @@ def reduce_over_ranks(dist, dt: float, n_rows: int, device):
     return float(mx[0]), int(sm[1])
 
 
+def share_comm_id(dist, rank: int, make):
+    """Rank 0 makes the RCCL unique id (`make()`), every rank returns it (broadcast over the
+    torch.distributed group): the rendezvous of rs_engine_join_rccl."""
+    obj = [make() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def sharded_one_circuit(M, dist, args, world, rank, local, fl, barrier):
+    """The SAME 10M metric circuit on every rank, its clusters dealt to the ranks and the
+    eliminated-signal map exchanged over RCCL (SURVEY 8(e), strong scaling).  Returns the max over
+    ranks of ms/step and the exchange time, measured like the headline."""
+    uid = share_comm_id(dist, rank, M.comm_unique_id)
+    inp = M.Input.synth(0, args.rows, args.seed, args.prime)
+    eng = M.Engine(local)
+    eng.join_rccl(world, rank, uid)
+    eng.load(inp.c)
+    for _ in range(args.warmup):
+        eng.run(fl)
+    barrier()
+    t0 = time.perf_counter()
+    xms = 0.0
+    for _ in range(args.steps):
+        eng.run(fl)
+        xms += eng.stats().exchange_ms
+    barrier()
+    dt = time.perf_counter() - t0
+    dt, _ = reduce_over_ranks(dist, dt, 0, "cuda")
+    xmax, _ = reduce_over_ranks(dist, xms, 0, "cuda")
+    n = inp.rows()
+    st = eng.stats()
+    eng.close()
+    return {"workload": f"synth_mixed rows={args.rows} prime={args.prime} seed={args.seed} --O2, ONE circuit "
+                        f"on {world} ranks (clusters dealt by size, RCCL exchange of the eliminated-signal map)",
+            "scaling": "strong", "constraints": n, "ms_per_step": round(dt * 1000.0 / args.steps, 3),
+            "value": round(n * args.steps / dt, 1), "unit": "constraints/s",
+            "exchange_ms_per_step": round(xmax / args.steps, 3), "exchange_bytes_per_rank": int(st.exchange_bytes)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,6 +108,10 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", choices=("shards", "both"), default="both",
+                    help="N>1: shards = the headline only (each rank its own circuit shard, weak "
+                         "scaling); both = the headline + ONE circuit sharded over all ranks with the "
+                         "RCCL exchange (strong scaling), as the extra object sharded_one_circuit")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,6 +160,10 @@ def main():
     dt = time.perf_counter() - t0
     dt, total_rows = reduce_over_ranks(dist, dt, n_rows, "cuda")
     last = eng.stats()
+    sharded = None
+    if dist is not None and args.mode == "both":
+        eng.close()  # free the headline engine's HBM before the second one
+        sharded = sharded_one_circuit(M, dist, args, world, rank, local, fl, barrier)
     if rank == 0:
         ms_step = dt * 1000.0 / args.steps
         value = total_rows * args.steps / dt
@@ -147,6 +194,8 @@ def main():
             "phases_ms": {k: round(getattr(last, k), 2) for k in
                           ("total_ms", "eq_ms", "cluster_ms", "elim_ms", "subst_ms", "final_ms")},
         }
+        if sharded is not None:
+            line["sharded_one_circuit"] = sharded
         if not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.cpu_rows, shard_seed(args.seed, 0), args.cpu_threads,
                                                 args.prime)

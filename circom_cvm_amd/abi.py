@@ -55,7 +55,8 @@ class RsStats(C.Structure):
                 ("big_prep_ms", C.c_double), ("big_main_ms", C.c_double), ("big_finish_ms", C.c_double),
                 ("big_main_bytes", C.c_uint64), ("big_finish_bytes", C.c_uint64), ("big_launches", C.c_uint64),
                 ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
-                ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64)]
+                ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64),
+                ("exchange_ms", C.c_double), ("exchange_bytes", C.c_uint64), ("world", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -73,6 +74,13 @@ SYMBOLS = [
     ("rs_engine_fetch", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(RsOutput))]),
     ("rs_engine_stats", C.c_int, [C.c_void_p, C.POINTER(RsStats)]),
     ("rs_engine_destroy", None, [C.c_void_p]),
+    ("rs_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("rs_engine_join_rccl", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
+    ("rs_group_create", C.c_void_p, [C.c_int]),
+    ("rs_engine_join_group", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    ("rs_group_destroy", None, [C.c_void_p]),
+    ("rs_simplify_multi", C.c_int, [C.POINTER(RsInput), C.POINTER(RsFlags), C.c_int, C.POINTER(C.c_int),
+                                    C.POINTER(C.POINTER(RsOutput))]),
     ("rs_read_r1cs_o0", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(RsInput))]),
     ("rs_input_free", None, [C.POINTER(RsInput)]),
     ("rs_write_r1cs", C.c_int, [C.c_char_p, C.POINTER(RsInput), C.POINTER(RsOutput)]),
@@ -123,12 +131,54 @@ def make_flags(level: str = "O2", rounds: int | None = None, old: bool = False, 
     return f
 
 
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """rs_comm_unique_id: the RCCL id rank 0 creates and broadcasts before rs_engine_join_rccl."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    check(lib().rs_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Group:
+    """An in-process rank group (rs_group_*): several engines in one process, one per thread, with
+    host-staged collectives -- the sharded path on a single GPU."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self._h = lib().rs_group_create(world)
+        if not self._h:
+            raise ValueError(f"bad world size {world}")
+
+    def close(self):
+        if self._h:
+            lib().rs_group_destroy(self._h)
+            self._h = None
+
+
+def simplify_multi(inp: RsInput, flags: RsFlags, devices) -> "Output":
+    """rs_simplify_multi: one-shot sharded simplification over `devices` (threads in this process)."""
+    arr = (C.c_int * len(devices))(*devices)
+    out = C.POINTER(RsOutput)()
+    check(lib().rs_simplify_multi(C.byref(inp), C.byref(flags), len(devices), arr, C.byref(out)))
+    return Output(out)
+
+
 class Engine:
     """HBM-resident simplification engine (rs_engine_*)."""
 
     def __init__(self, device: int = 0):
         self._h = C.c_void_p()
         check(lib().rs_engine_create(device, C.byref(self._h)))
+
+    def join_rccl(self, world: int, rank: int, uid: bytes):
+        """Rank `rank` of a sharded run over RCCL (collective: every rank must call it)."""
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        check(lib().rs_engine_join_rccl(self._h, world, rank, buf))
+
+    def join_group(self, group: Group, rank: int):
+        check(lib().rs_engine_join_group(self._h, group._h, rank))
 
     def load(self, inp: RsInput):
         check(lib().rs_engine_load(self._h, C.byref(inp)))

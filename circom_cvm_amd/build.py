@@ -11,7 +11,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librs_simplify.so")
 CLI = os.path.join(PKG, "circom-simplify")
 SOURCES = ["engine.hip", "r1cs_io.cpp", "synth.cpp"]
-HEADERS = ["field.hpp", "kernels.hpp", "host_common.hpp", os.path.join("..", "..", "include", "rs_simplify.h")]
+HEADERS = ["field.hpp", "kernels.hpp", "cluster.hpp", "comm.hpp", "host_common.hpp", os.path.join("..", "..", "include", "rs_simplify.h")]
 
 
 def _stale(target, deps):
@@ -26,7 +26,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     if force or _stale(LIB, deps):
         cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES]
+               "-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES] + [
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <stdexcept>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -111,6 +112,10 @@ static void launch(hipStream_t st, K kernel, uint64_t n, Args... args) {
   HC(hipGetLastError());
 }
 
+}  // namespace rs
+#include "comm.hpp"
+namespace rs {
+
 // host view of ragged rows (keys only unless vals requested)
 struct HostRows {
   std::vector<uint64_t> off;
@@ -155,6 +160,8 @@ struct rs_engine {
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr, ev6 = nullptr;
+  // sharded elimination: this engine is rank `comm->rank` of `comm->world`
+  std::unique_ptr<rs::Comm> comm;
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
@@ -328,6 +335,63 @@ __global__ void k_emit_pairs(DRows a, DRows b, DRows c, const uint8_t *flag, uin
         unsigned long long o = atomicAdd(cnt, 1ull);
         if (o < cap) pairs[o] = ((uint64_t)s << 32) | (uint32_t)r;
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- sharded elimination
+// The size-ordered cluster lists are dealt to the ranks in snake order (0,1,..,W-1,W-1,..,0, ...),
+// so every rank gets a near-equal share of each size class and the largest clusters spread first.
+__host__ __device__ inline int snake_rank(uint64_t pos, int W) {
+  uint64_t p = pos % (2 * (uint64_t)W);
+  return p < (uint64_t)W ? (int)p : (int)(2 * (uint64_t)W - 1 - p);
+}
+// number of positions < n that rank r owns
+static uint64_t snake_count(uint64_t n, int W, int r) {
+  uint64_t per = 2 * (uint64_t)W, k = n / per, rem = n % per;
+  return 2 * k + (rem > (uint64_t)r ? 1 : 0) + (rem > per - 1 - r ? 1 : 0);
+}
+// rank r's clusters of a size-ordered list, in list order (closed form: no scan)
+__global__ void k_shard_pick(const uint32_t *ids, uint64_t n_out, int W, int r, uint32_t *out) {
+  const uint64_t per = 2 * (uint64_t)W;
+  for (uint64_t j = gtid(); j < n_out; j += gstride())
+    out[j] = ids[(j / 2) * per + ((j & 1) ? per - 1 - r : (uint64_t)r)];
+}
+__global__ void k_shard_owner(const uint32_t *ids, uint64_t n, int W, uint8_t *owner) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) owner[ids[i]] = (uint8_t)snake_rank(i, W);
+}
+// Before the exchange: the rank's own slots get their pool offsets rebased into the gathered pool;
+// every other slot (and every other cluster's counts) is zeroed, so a sum over ranks assembles the
+// complete per-slot map.
+__global__ void k_shard_rebase(const uint32_t *cid, const uint64_t *cl_off, const uint8_t *owner, int r,
+                               const uint32_t *n_sub, const uint32_t *n_left, uint64_t base, uint32_t *h_sig,
+                               uint64_t *h_off, uint32_t *h_len, uint64_t *l_off, uint32_t *l_len, uint64_t n_slots) {
+  for (uint64_t s = gtid(); s < n_slots; s += gstride()) {
+    const uint32_t c = cid[s];
+    const uint64_t i = s - cl_off[c];
+    if (owner[c] == r) {
+      if (i < n_sub[c]) h_off[s] += base;
+      else { h_sig[s] = 0; h_off[s] = 0; h_len[s] = 0; }
+      if (i < n_left[c]) l_off[s] += base;
+      else { l_off[s] = 0; l_len[s] = 0; }
+    } else {
+      h_sig[s] = 0; h_off[s] = 0; h_len[s] = 0; l_off[s] = 0; l_len[s] = 0;
+    }
+  }
+}
+__global__ void k_shard_zero_counts(const uint8_t *owner, int r, uint64_t n_cl, uint32_t *n_sub, uint32_t *n_left) {
+  for (uint64_t c = gtid(); c < n_cl; c += gstride())
+    if (owner[c] != r) { n_sub[c] = 0; n_left[c] = 0; }
+}
+// After the exchange: the dense signal -> substitution index and the deleted bits of every rank's
+// substitutions (the owner's own entries are rewritten with the same values).
+__global__ void k_shard_subof(const uint32_t *cid, const uint64_t *cl_off, const uint32_t *n_sub, const uint32_t *h_sig,
+                              int32_t *sub_of, uint8_t *deleted, uint64_t n_slots) {
+  for (uint64_t s = gtid(); s < n_slots; s += gstride()) {
+    const uint32_t c = cid[s];
+    if (s - cl_off[c] < n_sub[c]) {
+      sub_of[h_sig[s]] = (int32_t)s;
+      deleted[h_sig[s]] = 1;
     }
   }
 }
@@ -548,6 +612,53 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   return D;
 }
 
+// The exchange step of the sharded elimination: after it every rank holds the complete
+// eliminated-signal map of the round -- per slot (from, RHS offset/length) and leftovers (offset,
+// length), per cluster #subs/#leftovers, the gathered pool those offsets index, and the dense
+// sub_of / deleted of every substitution.  The offsets are rebased into the gathered pool (rank q's
+// entries start at the sum of the lower ranks' pool tops) before a sum-allreduce of the zero-padded
+// per-slot arrays; the pool itself is an allgatherv.
+static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D, const uint8_t *owner, Pool &P) {
+  Comm &CM = *E->comm;
+  hipStream_t st = E->st;
+  const double t0 = now_ms();
+  const uint64_t n_slots = D.n_slots, n_cl = a.n_clusters;
+  uint64_t top = 0;
+  HC(hipMemcpyAsync(&top, P.top, 8, hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  top = std::min<uint64_t>(top, P.cap);
+  const std::vector<uint64_t> tops = CM.gather_u64(top, st);
+  uint64_t base = 0, tot = 0;
+  std::vector<uint64_t> ck(CM.world), cv(CM.world);
+  for (int q = 0; q < CM.world; ++q) {
+    if (q < CM.rank) base += tops[q];
+    tot += tops[q];
+    ck[q] = 4 * tops[q];
+    cv[q] = 32 * tops[q];
+  }
+  launch(st, k_shard_zero_counts, n_cl, owner, CM.rank, n_cl, a.n_sub, a.n_left);
+  launch(st, k_shard_rebase, n_slots, (const uint32_t *)D.cid, (const uint64_t *)D.cl_off, owner, CM.rank,
+         (const uint32_t *)a.n_sub, (const uint32_t *)a.n_left, base, a.h_sig, a.h_off, a.h_len, a.l_off, a.l_len, n_slots);
+  uint32_t *gk = E->A.get<uint32_t>("pool.gk", tot);
+  Fe *gv = E->A.get<Fe>("pool.gv", tot);
+  CM.allgatherv(P.pk, gk, ck, st);
+  CM.allgatherv(P.pv, gv, cv, st);
+  CM.allreduce_sum(a.h_sig, n_slots, 4, st);
+  CM.allreduce_sum(a.h_off, n_slots, 8, st);
+  CM.allreduce_sum(a.h_len, n_slots, 4, st);
+  CM.allreduce_sum(a.l_off, n_slots, 8, st);
+  CM.allreduce_sum(a.l_len, n_slots, 4, st);
+  CM.allreduce_sum(a.n_sub, n_cl, 4, st);
+  CM.allreduce_sum(a.n_left, n_cl, 4, st);
+  launch(st, k_shard_subof, n_slots, (const uint32_t *)D.cid, (const uint64_t *)D.cl_off, (const uint32_t *)a.n_sub,
+         (const uint32_t *)a.h_sig, a.sub_of, a.deleted, n_slots);
+  HC(hipStreamSynchronize(st));
+  P.pk = gk;
+  P.pv = gv;
+  E->stats.exchange_ms += now_ms() - t0;
+  E->stats.exchange_bytes += 36 * tot + n_slots * 28 + n_cl * 8;
+}
+
 // Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
 // the arena hold the substitutions (h_*) and leftovers (l_*), sub_of/deleted are updated.
 static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
@@ -556,9 +667,27 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   DevClusters D = gpu_clusters(E, view, old_heur, d_forb, eo);
   double t1 = now_ms();
   E->stats.cluster_ms += t1 - t0;
-  const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz, n_big = D.n_big, n_small = D.n_small;
+  const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz;
+  uint64_t n_big = D.n_big, n_small = D.n_small;
   uint32_t *d_perm = D.perm, *d_big = D.big, *d_small = D.small, *d_cid = D.cid;
   uint64_t *d_cl = D.cl_off;
+  // sharded: this rank eliminates its snake share of each size-ordered list
+  Comm *CM = E->comm.get();
+  const int W = CM ? CM->world : 1, RK = CM ? CM->rank : 0;
+  uint8_t *d_owner = nullptr;
+  if (W > 1 && eo.n_clusters) {
+    d_owner = E->A.get<uint8_t>("sh.owner", eo.n_clusters);
+    if (n_big) launch(E->st, k_shard_owner, n_big, (const uint32_t *)d_big, n_big, W, d_owner);
+    if (n_small) launch(E->st, k_shard_owner, n_small, (const uint32_t *)d_small, n_small, W, d_owner);
+    const uint64_t nb = snake_count(n_big, W, RK), ns = snake_count(n_small, W, RK);
+    uint32_t *bb = E->A.get<uint32_t>("sh.big", nb), *ss = E->A.get<uint32_t>("sh.small", ns);
+    if (nb) launch(E->st, k_shard_pick, nb, (const uint32_t *)d_big, nb, W, RK, bb);
+    if (ns) launch(E->st, k_shard_pick, ns, (const uint32_t *)d_small, ns, W, RK, ss);
+    d_big = bb;
+    d_small = ss;
+    n_big = nb;
+    n_small = ns;
+  }
   uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots)), E->pool_want);
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
@@ -668,6 +797,11 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     int err = 0;
     HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
     HC(hipStreamSynchronize(E->st));
+    if (W > 1) {  // every rank takes the same retry / failure decision
+      const uint64_t mine = (uint32_t)err;
+      err = 0;
+      for (uint64_t x : CM->gather_u64(mine, E->st)) err |= (int)x;
+    }
     if (err & 8) {
       size_t fr_ = 0, tot_ = 0;
       (void)hipMemGetInfo(&fr_, &tot_);
@@ -682,6 +816,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
     E->pool_want = std::max(E->pool_want, want);  // the next run starts from a size that fitted
+    if (W > 1 && eo.n_clusters) shard_exchange(E, a, D, d_owner, P);
     if (eo.n_clusters) {
       float ms = 0;
       unsigned long long by = 0;
@@ -894,6 +1029,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   const uint64_t S = E->S;
   hipStream_t st = E->st;
   E->stats = rs_stats{};
+  E->stats.world = E->comm ? (uint64_t)E->comm->world : 1;
   double T0 = now_ms();
   bool apply_linear = !fl->flag_s;
   uint64_t no_rounds = fl->no_rounds;
@@ -1707,6 +1843,7 @@ void rs_engine_destroy(rs_engine *E) {
   if (!E) return;
   (void)hipSetDevice(E->device);
   if (E->st) (void)hipStreamSynchronize(E->st);
+  E->comm.reset();
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
   if (E->ev2) (void)hipEventDestroy(E->ev2);
@@ -1859,6 +1996,103 @@ void rs_output_free(rs_output *o) {
   free_lc(o->c);
   free(o->label_to_wire);
   free(o);
+}
+
+// ------------------------------------------------------------------ multi-GPU (sharded elimination)
+struct rs_group {
+  rs::LocalGroup g;
+  explicit rs_group(int w) : g(w) {}
+};
+
+int rs_comm_unique_id(uint8_t id[RS_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == RS_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) { set_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r)); return RS_E_RCCL; }
+  memcpy(id, &u, RS_COMM_ID_BYTES);
+  return RS_OK;
+}
+
+int rs_engine_join_rccl(rs_engine *E, int world, int rank, const uint8_t id[RS_COMM_ID_BYTES]) {
+  try {
+    if (world < 1 || world > 255 || rank < 0 || rank >= world) { set_error("bad world/rank"); return RS_E_INVALID; }
+    HC(hipSetDevice(E->device));
+    ncclUniqueId u;
+    memcpy(&u, id, RS_COMM_ID_BYTES);
+    ncclComm_t c = nullptr;
+    NC(ncclCommInitRank(&c, world, u, rank));
+    E->comm.reset(new RcclComm(c, rank, world));
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+rs_group *rs_group_create(int world) {
+  if (world < 1 || world > 255) return nullptr;
+  return new rs_group(world);
+}
+void rs_group_destroy(rs_group *g) { delete g; }
+
+int rs_engine_join_group(rs_engine *E, rs_group *g, int rank) {
+  if (!g || rank < 0 || rank >= g->g.world) { set_error("bad group/rank"); return RS_E_INVALID; }
+  E->comm.reset(new LocalComm(&g->g, rank));
+  return RS_OK;
+}
+
+int rs_simplify_multi(const rs_input *in, const rs_flags *fl, int n_dev, const int *devices, rs_output **out) {
+  if (n_dev < 1 || n_dev > 255 || !devices) { set_error("bad device list"); return RS_E_INVALID; }
+  if (n_dev == 1) {
+    rs_flags f = *fl;
+    f.device = devices[0];
+    return rs_simplify(in, &f, out);
+  }
+  std::vector<rs_engine *> eng(n_dev, nullptr);
+  int rc = RS_OK;
+  for (int r = 0; r < n_dev && !rc; ++r) rc = rs_engine_create(devices[r], &eng[r]);
+  bool distinct = true;
+  for (int r = 0; r < n_dev; ++r)
+    for (int q = 0; q < r; ++q) distinct &= devices[q] != devices[r];
+  std::unique_ptr<rs_group> grp;
+  if (!rc) {
+    if (distinct) {  // RCCL: one communicator per device, created together
+      try {
+        std::vector<ncclComm_t> comms(n_dev);
+        NC(ncclCommInitAll(comms.data(), n_dev, devices));
+        for (int r = 0; r < n_dev; ++r) eng[r]->comm.reset(new RcclComm(comms[r], r, n_dev));
+      } catch (const RsError &e) {
+        set_error(e.what());
+        rc = e.code;
+      }
+    } else {
+      grp.reset(new rs_group(n_dev));
+      for (int r = 0; r < n_dev; ++r) eng[r]->comm.reset(new LocalComm(&grp->g, r));
+    }
+  }
+  std::vector<int> rcs(n_dev, RS_OK);
+  std::vector<std::string> errs(n_dev);
+  if (!rc) {
+    std::vector<std::thread> th;
+    for (int r = 0; r < n_dev; ++r)
+      th.emplace_back([&, r] {
+        rs_flags f = *fl;
+        f.device = devices[r];
+        int x = rs_engine_load(eng[r], in);
+        if (!x) x = rs_engine_run(eng[r], &f);
+        if (!x && r == 0) x = rs_engine_fetch(eng[r], out);
+        rcs[r] = x;
+        if (x) errs[r] = rs_last_error();
+      });
+    for (auto &t : th) t.join();
+    for (int r = 0; r < n_dev && !rc; ++r)
+      if (rcs[r]) { rc = rcs[r]; set_error("rank " + std::to_string(r) + ": " + errs[r]); }
+  }
+  for (auto *E : eng) rs_engine_destroy(E);
+  return rc;
 }
 
 int rs_simplify(const rs_input *in, const rs_flags *fl, rs_output **out) {

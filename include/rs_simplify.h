@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 1
+#define RS_ABI_VERSION 2
 
 enum rs_status {
   RS_OK = 0,
@@ -146,6 +146,9 @@ typedef struct rs_stats {
   uint64_t n_clusters;
   uint64_t n_substitutions;
   uint64_t max_cluster;
+  double exchange_ms;          /* sharded runs: the eliminated-signal-map exchange (all rounds) */
+  uint64_t exchange_bytes;     /* bytes each rank received + contributed in those collectives  */
+  uint64_t world;              /* ranks the elimination was sharded over (1 = single GPU)       */
 } rs_stats;
 
 typedef struct rs_engine rs_engine;
@@ -164,6 +167,32 @@ int rs_engine_run(rs_engine *eng, const rs_flags *fl);    /* the timed region   
 int rs_engine_fetch(rs_engine *eng, rs_output **out);     /* D2H of the last result             */
 int rs_engine_stats(rs_engine *eng, rs_stats *st);
 void rs_engine_destroy(rs_engine *eng);
+
+/*
+ * Multi-GPU: ONE circuit sharded over W ranks.  Every rank loads the same input;
+ * the global phases (eq / const-eq renaming, build_clusters) run on every rank, the clusters are
+ * dealt to the ranks by size (snake order), each rank eliminates its own, and the eliminated-signal
+ * map (substitutions, leftovers, their pool entries) is exchanged after every round -- RCCL over
+ * xGMI in production.  Every rank ends with the complete, identical output (byte-identical to a
+ * single-GPU run).  Join before rs_engine_run; all ranks must run with the same flags.
+ *
+ * RCCL, one process per GPU (what bench.py does under torch.distributed.run):
+ *   rank 0: rs_comm_unique_id(id); broadcast the RS_COMM_ID_BYTES bytes to the other ranks;
+ *   every rank: rs_engine_join_rccl(eng, world, rank, id)   (collective: blocks until all joined)
+ * In one process (threads; a device may be listed twice, e.g. to test on one GPU):
+ *   g = rs_group_create(world); rank r's thread: rs_engine_join_group(eng_r, g, r); ...
+ *   rs_group_destroy(g) after every engine of the group is destroyed.
+ * rs_simplify_multi: the one-shot entry point over n_devices GPUs of this process (threads; RCCL
+ * when the devices are distinct, the in-process transport otherwise).
+ */
+#define RS_COMM_ID_BYTES 128
+typedef struct rs_group rs_group;
+int rs_comm_unique_id(uint8_t id[RS_COMM_ID_BYTES]);
+int rs_engine_join_rccl(rs_engine *eng, int world, int rank, const uint8_t id[RS_COMM_ID_BYTES]);
+rs_group *rs_group_create(int world);
+int rs_engine_join_group(rs_engine *eng, rs_group *g, int rank);
+void rs_group_destroy(rs_group *g);
+int rs_simplify_multi(const rs_input *in, const rs_flags *fl, int n_devices, const int *devices, rs_output **out);
 
 /* --O0 .r1cs -> rs_input (host arrays owned by the library; free with rs_input_free).
  * Classifies rows exactly like dag/src/map_to_constraint_list.rs:12-44. */

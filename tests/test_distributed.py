@@ -1,6 +1,7 @@
-"""Multi-process path of bench.py on CPU (gloo, world size 2): shard assignment and the max/sum
-reduction the N-GPU line is computed from.  The data path itself has no collective (DESIGN.md
-"Multi-GPU"): each rank owns an independent circuit shard."""
+"""Multi-process path of bench.py on CPU (gloo, world size 2): shard assignment, the max/sum
+reduction the N-GPU line is computed from, and the unique-id rendezvous of the sharded
+(one-circuit, RCCL exchange) line.  The exchange itself needs GPUs: tests/test_gpu_sharded.py runs
+it with W engines on one device."""
 import os
 import socket
 
@@ -34,7 +35,9 @@ def _worker(rank, world, port, q):
         dt, total = bench.reduce_over_ranks(dist, 1.0 + rank, rows, "cpu")
         g = [None] * world
         dist.all_gather_object(g, (rows, int(inp.c.max_signal)))
-        q.put((rank, dt, total, g))
+        # the RCCL rendezvous of the sharded line: rank 0's id reaches every rank unchanged
+        uid = bench.share_comm_id(dist, rank, lambda: bytes(range(128)))
+        q.put((rank, dt, total, g, uid))
     finally:
         dist.destroy_process_group()
 
@@ -52,9 +55,10 @@ def test_gloo_world2_reduction_and_shards():
         assert p.exitcode == 0
     res.sort()
     rows = [g[0] for g in res[0][3]]
-    for rank, dt, total, g in res:
+    for rank, dt, total, g, uid in res:
         assert dt == 2.0                      # max over ranks of the timed region
         assert total == sum(rows)             # whole-job constraints
+        assert uid == bytes(range(128))       # rs_engine_join_rccl rendezvous id
     assert res[0][3] == res[1][3]
     # distinct shards (different seeds) of the same workload size
     assert all(r >= 3000 for r in rows)

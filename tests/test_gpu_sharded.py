@@ -1,0 +1,122 @@
+"""GPU parity of the SHARDED path: one circuit, W ranks, clusters dealt by size, the
+eliminated-signal map exchanged after every round.  On the one-GPU box the ranks are W engines on
+device 0 in W threads of this process, joined to an in-process group (host-staged collectives); the
+RCCL transport is the same code path behind another Comm (covered at world 1 here, at world N by the
+driver's multi-GPU bench).  Every rank's output must equal the single-GPU oracle's, bit for bit."""
+import threading
+
+import pytest
+
+import rsio
+import circom_cvm_amd as M
+
+R = rsio.R
+pytestmark = pytest.mark.gpu
+
+_GROUPS = {}
+
+
+def group(world):
+    """W engines on device 0 joined to one in-process group (reused across tests)."""
+    if world not in _GROUPS:
+        g = M.Group(world)
+        engs = [M.Engine(0) for _ in range(world)]
+        for r, e in enumerate(engs):
+            e.join_group(g, r)
+        _GROUPS[world] = (g, engs)
+    return _GROUPS[world][1]
+
+
+def sharded_run(inp, fl, world, arrays=False):
+    engs = group(world)
+    outs, errs = [None] * world, [None] * world
+
+    def work(r):
+        try:
+            engs[r].load(inp)
+            engs[r].run(fl)
+            out = engs[r].fetch()
+            outs[r] = (rsio.output_arrays(out.c) if arrays else rsio.output_to_py(out.c), engs[r].stats())
+        except Exception as ex:  # noqa: BLE001 -- reported below
+            errs[r] = ex
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+        assert not t.is_alive(), "sharded run hung"
+    for e in errs:
+        if e is not None:
+            raise e
+    return outs
+
+
+def check(inp, fl, world, threads=1):
+    ref, _, _ = rsio.oracle_run(inp, fl, threads)
+    outs = sharded_run(inp, fl, world)
+    for r, (got, st) in enumerate(outs):
+        if got != ref:
+            diff = rsio.same_result(R.Result(ref[0], ref[1], ref[3]), got)
+            raise AssertionError(f"rank {r}/{world} != oracle: {diff}")
+        assert st.world == world
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("p", [257, R.PRIMES["bn128"], R.PRIMES["goldilocks"]])
+def test_sharded_random_small(world, p):
+    for seed in range(12):
+        sys_ = rsio.gen_system(seed, p, n_sig=40 + seed % 50, n_rows=60 + seed % 80)
+        h = rsio.InputHolder(sys_)
+        for lvl, rd in (("O1", None), ("O2", None), ("O2", 1), ("O2", 2)):
+            check(h.inp, rsio.flags(lvl, rd), world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_process4(world):
+    p = R.PRIMES["bn128"]
+    for seed in range(4):
+        sys_ = rsio.gen_system(2000 + seed, p, n_sig=300, n_rows=250, big_cluster=600 + 40 * seed)
+        h = rsio.InputHolder(sys_)
+        for lvl, rd, old in (("O2", None, False), ("O2", None, True), ("O2", 2, False)):
+            check(h.inp, rsio.flags(lvl, rd, old), world, threads=4)
+
+
+@pytest.mark.parametrize("kind,rows,world", [(0, 200_000, 4), (0, 300_000, 3), (1, 100_000, 2), (2, 50_000, 3)])
+def test_sharded_synth_arrays(kind, rows, world):
+    """Synthetic workloads (mixed / purely linear / deep chains) array for array on every rank."""
+    inp = M.Input.synth(kind, rows, 42)
+    fl = rsio.flags("O2")
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=8)
+    outs = sharded_run(inp.c, fl, world, arrays=True)
+    for r, (got, st) in enumerate(outs):
+        assert rsio.diff_output_arrays(got, ref) is None, f"rank {r}"
+        assert st.world == world and st.exchange_bytes > 0
+    assert len({st.n_substitutions for _, st in outs}) == 1  # every rank holds the whole map
+
+
+def test_simplify_multi_one_device_listed_twice():
+    """rs_simplify_multi (the one-shot entry point) with device 0 listed twice: in-process transport."""
+    sys_ = rsio.gen_system(77, R.PRIMES["bn128"], n_sig=300, n_rows=250, big_cluster=700)
+    h = rsio.InputHolder(sys_)
+    fl = rsio.flags("O2")
+    out = M.simplify_multi(h.inp, fl, [0, 0])
+    ref, _, _ = rsio.oracle_run(h.inp, fl)
+    assert rsio.output_to_py(out.c) == ref
+
+
+def test_rccl_world1_join():
+    """The RCCL transport's plumbing on one GPU: unique id, communicator init, a run at world 1."""
+    e = M.Engine(0)
+    e.join_rccl(1, 0, M.comm_unique_id())
+    inp = M.Input.synth(0, 20_000, 9)
+    fl = rsio.flags("O2")
+    e.load(inp.c)
+    e.run(fl)
+    out = e.fetch()  # keep the owner alive while its arrays are read
+    got = rsio.output_arrays(out.c)
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=4)
+    assert rsio.diff_output_arrays(got, ref) is None
+    assert e.stats().world == 1
+    e.close()
