@@ -25,7 +25,11 @@ def build(verbose: bool = False, force: bool = False) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     if force or _stale(LIB, deps):
+        # every kernel without its own __launch_bounds__ is launched with 256 threads: saying so keeps
+        # the backend from sizing promoted private arrays in LDS for 1024-thread workgroups (which
+        # capped k_nl_fill / k_round_fill at 2 workgroups per CU)
         cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "--gpu-max-threads-per-block=256",
                "-o", LIB] + [os.path.join(CSRC, s) for s in SOURCES] + [
                "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:

@@ -740,7 +740,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     // time is the critical path of the largest cluster, and everything else overlaps it.
     const char *hd = getenv("RS_HEAD");
     const uint64_t n_head = std::min<uint64_t>(n_big, hd ? (uint64_t)atoi(hd) : 16), n_tail = n_big - n_head;
+    a.wide = 1;       // the head's largest process_4 clusters go through the k_wide_* grid
     ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
+    at.wide = 0;
     at.big_touch_off += n_head;
     at.big_touch_n += n_head;
     at.big_alive += n_head;
@@ -751,6 +753,17 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipStreamWaitEvent(E->st2, E->ev2, 0));
         const unsigned g = (unsigned)n_head;
         HC(hipEventRecord(E->evx[1], E->st2));
+        {  // the largest process_4 clusters: occurrences / uniques over a 2-D grid first
+          const dim3 g2(kWideX, g);
+          const uint32_t *ids = d_big;
+          hipLaunchKernelGGL(k_wide_alloc, dim3(g), dim3(256), 0, E->st2, a, ids, n_head);
+          hipLaunchKernelGGL(k_wide_count, g2, dim3(256), 0, E->st2, a, ids, n_head);
+          hipLaunchKernelGGL(k_wide_conv, g2, dim3(256), 0, E->st2, a, ids, n_head);
+          hipLaunchKernelGGL(k_wide_uniq, g2, dim3(256), 0, E->st2, a, ids, n_head);
+          hipLaunchKernelGGL(k_wide_remove, g2, dim3(256), 0, E->st2, a, ids, n_head);
+          hipLaunchKernelGGL(k_wide_clear, g2, dim3(256), 0, E->st2, a, ids, n_head);
+          HC(hipGetLastError());
+        }
         hipLaunchKernelGGL(k_big_prep, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));

@@ -307,6 +307,7 @@ struct ElimArgs {
   uint32_t *big_alive;        // per big cluster: #rows left for the ordered loop
   uint64_t *row_off;          // per slot: (offset, length) of those rows in loop order (k_big_prep)
   uint32_t *row_len;
+  int wide;                   // the k_wide_* kernels prepared this launch's largest p4 clusters
 
 };
 
@@ -518,7 +519,7 @@ __device__ inline bool d_normalize_compose(const ElimArgs &A, Alloc &al, uint64_
   return true;
 }
 
-__global__ void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+__global__ __launch_bounds__(64) void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
   Alloc al;
   for (uint64_t ci = gtid(); ci < n_ids; ci += gstride()) {
@@ -744,6 +745,123 @@ __device__ __forceinline__ bool d_is_p4(const ElimArgs &A, uint32_t n) {
   return n >= 350 && n < 1000000 && !A.old_heur;
 }
 
+// ---- wide preparation of the largest process_4 clusters (SignalsInformation::new, the uniques
+// phase and remove_constraint of substitution_process_4, :156-185): the same work as k_big_prep's
+// first phases, spread over a 2-D grid (x: 64 workgroups per cluster, y: the cluster) so a cluster
+// of tens of thousands of long rows is not serialised on one CU.  Phase boundaries are kernel
+// boundaries; k_big_prep then finishes (remove_signal, rows left for the ordered loop).
+constexpr uint32_t kWideMin = 2048;  // rows
+constexpr uint32_t kWideX = 64;      // workgroups per cluster
+__device__ __forceinline__ bool d_is_wide(const ElimArgs &A, uint32_t n) { return A.wide && d_is_p4(A, n) && n >= kWideMin; }
+
+// per cluster: #entries -> touched-signal list capacity in the pool, counters reset
+__global__ __launch_bounds__(256) void k_wide_alloc(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  __shared__ unsigned long long s_tot;
+  const uint64_t ci = blockIdx.x;
+  if (ci >= n_ids) return;
+  const uint64_t c = ids[ci], b = A.cl_off[c];
+  const uint32_t n = (uint32_t)(A.cl_off[c + 1] - b);
+  if (!d_is_wide(A, n)) return;
+  if (threadIdx.x == 0) s_tot = 0;
+  __syncthreads();
+  unsigned long long tot = 0;
+  for (uint32_t pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    tot += A.rows.len[A.perm[b + pos]];
+    A.dead[b + pos] = 0;
+  }
+  atomicAdd(&s_tot, tot);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t o = pool_alloc_global(A, s_tot + 1);
+    A.big_touch_off[ci] = o == RS_NONE ? 0 : o;
+    A.big_touch_n[ci] = 0;
+    A.n_sub[c] = 0;
+    A.big_alive[ci] = o == RS_NONE ? RS_NONE : 0;  // RS_NONE: failure marker, see k_big_prep
+  }
+}
+// occurrences (init -1 = absent) over non-forbidden signals + the touched list
+__global__ __launch_bounds__(256) void k_wide_count(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const uint64_t ci = blockIdx.y;
+  const uint64_t c = ids[ci], b = A.cl_off[c];
+  const uint32_t n = (uint32_t)(A.cl_off[c + 1] - b);
+  if (!d_is_wide(A, n) || A.big_alive[ci] == RS_NONE) return;
+  uint32_t *touch = A.pk + A.big_touch_off[ci];
+  for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < n; pos += gridDim.x * blockDim.x) {
+    const uint32_t r = A.perm[b + pos];
+    const uint32_t *k = A.rows.key + A.rows.off[r];
+    const uint32_t len = A.rows.len[r];
+    for (uint32_t i = 0; i < len; ++i) {
+      const uint32_t s = k[i];
+      if (A.forb[s]) continue;
+      if (atomicAdd(&A.occ[s], 1) == -1) touch[atomicAdd(&A.big_touch_n[ci], 1u)] = s;
+    }
+  }
+}
+// -1 based -> counts
+__global__ __launch_bounds__(256) void k_wide_conv(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const uint64_t ci = blockIdx.y;
+  const uint64_t c = ids[ci], b = A.cl_off[c];
+  const uint32_t n = (uint32_t)(A.cl_off[c + 1] - b);
+  if (!d_is_wide(A, n) || A.big_alive[ci] == RS_NONE) return;
+  const uint32_t *touch = A.pk + A.big_touch_off[ci];
+  const uint32_t nt = A.big_touch_n[ci];
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) A.occ[touch[t]] += 1;
+}
+// uniques: each row is consumed by its smallest unique signal
+__global__ __launch_bounds__(256) void k_wide_uniq(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const uint64_t ci = blockIdx.y;
+  const uint64_t c = ids[ci], b = A.cl_off[c];
+  const uint32_t n = (uint32_t)(A.cl_off[c + 1] - b);
+  if (!d_is_wide(A, n) || A.big_alive[ci] == RS_NONE) return;
+  for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < n; pos += gridDim.x * blockDim.x) {
+    const uint32_t r = A.perm[b + pos];
+    const uint32_t *k = A.rows.key + A.rows.off[r];
+    const uint32_t len = A.rows.len[r];
+    for (uint32_t i = 0; i < len; ++i)
+      if (!A.forb[k[i]] && A.occ[k[i]] == 1) { A.dead[b + pos] = 1; A.order[b + pos] = i; break; }
+  }
+}
+// remove_constraint of the consumed rows
+__global__ __launch_bounds__(256) void k_wide_remove(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const uint64_t ci = blockIdx.y;
+  const uint64_t c = ids[ci], b = A.cl_off[c];
+  const uint32_t n = (uint32_t)(A.cl_off[c + 1] - b);
+  if (!d_is_wide(A, n) || A.big_alive[ci] == RS_NONE) return;
+  for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < n; pos += gridDim.x * blockDim.x) {
+    if (!A.dead[b + pos]) continue;
+    const uint32_t r = A.perm[b + pos];
+    const uint32_t *k = A.rows.key + A.rows.off[r];
+    const uint32_t len = A.rows.len[r];
+    for (uint32_t i = 0; i < len; ++i)
+      if (!A.forb[k[i]]) atomicSub(&A.occ[k[i]], 1);
+  }
+}
+// the substitutions of the consumed rows (clear_signal_not_normalized; slot order is normalised
+// later, like k_big_prep's atomic slots)
+__global__ __launch_bounds__(256) void k_wide_clear(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const uint64_t ci = blockIdx.y;
+  const uint64_t c = ids[ci], b = A.cl_off[c];
+  const uint32_t n = (uint32_t)(A.cl_off[c + 1] - b);
+  if (!d_is_wide(A, n) || A.big_alive[ci] == RS_NONE) return;
+  Alloc al;
+  al.chunk = 256;
+  for (uint32_t pos = blockIdx.x * blockDim.x + threadIdx.x; pos < n; pos += gridDim.x * blockDim.x) {
+    if (!A.dead[b + pos]) continue;
+    const uint32_t r = A.perm[b + pos];
+    const uint32_t *k = A.rows.key + A.rows.off[r];
+    const Fe *v = A.rows.val + A.rows.off[r];
+    const uint32_t oi = A.order[b + pos];
+    Fe coef;
+    uint64_t to_off;
+    uint32_t to_len;
+    if (!d_clear_nn(A, al, k, v, A.rows.len[r], oi, coef, to_off, to_len)) { atomicOr(A.err, 8); continue; }
+    const uint32_t slot = atomicAdd(&A.n_sub[c], 1u);
+    const uint32_t s = k[oi];
+    d_set_holder(A, s, b + slot, coef, to_off, to_len);
+    A.del[s] = 1;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   __shared__ uint32_t s_m, s_touch, s_ok, s_alive_part[256];
   __shared__ unsigned long long s_tot;
@@ -765,6 +883,21 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
       if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; A.big_alive[ci] = n; }
       continue;
     }
+    if (d_is_wide(A, n)) {  // counted, uniques and their substitutions done by the k_wide_* grid
+      __syncthreads();
+      if (tid == 0) {
+        s_m = A.n_sub[c];
+        s_ok = A.big_alive[ci] != RS_NONE;
+        s_touch_off = A.big_touch_off[ci];
+        s_touch = A.big_touch_n[ci];
+      }
+      __syncthreads();
+      if (!s_ok) {
+        if (tid == 0) { A.n_sub[c] = 0; A.big_touch_n[ci] = 0; A.big_alive[ci] = 0; atomicOr(A.err, 8); }
+        __syncthreads();
+        continue;
+      }
+    } else {
     uint64_t tot = 0;
     if (tid == 0) { s_m = 0; s_touch = 0; s_ok = 1; s_tot = 0; }
     for (uint32_t pos = tid; pos < n; pos += nt) tot += A.rows.len[A.perm[b + pos]];
@@ -831,7 +964,9 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
       d_set_holder(A, s, b + slot, coef, to_off, to_len);
       A.del[s] = 1;
     }
+    }  // not wide
     __syncthreads();
+    const uint32_t n_touch = s_touch;
     for (uint32_t i = tid; i < s_m; i += nt) A.occ[A.h_sig[b + i]] = -1;  // remove_signal
     {  // the rows left for the ordered loop, ascending (tmp[b ..]); order kept by a block scan
       const uint32_t per = (n + nt - 1) / nt, lo = min(n, tid * per), hi = min(n, lo + per);
