@@ -205,6 +205,39 @@ static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, u
   return last_in + last_out;
 }
 
+// one scan over three capacity columns at once (separate [a..][b..][c..] blocks keep neighbouring
+// rows' outputs adjacent, which the fill kernels' writes rely on for coalescing)
+struct U3 {
+  uint64_t a, b, c;
+};
+struct U3Plus {
+  __host__ __device__ U3 operator()(const U3 &x, const U3 &y) const { return U3{x.a + y.a, x.b + y.b, x.c + y.c}; }
+};
+static U3 excl_scan_u3(rs_engine *E, const U3 *in, U3 *out, uint64_t n, const char *tag) {
+  if (n == 0) return U3{0, 0, 0};
+  size_t tb = 0;
+  const U3 zero{0, 0, 0};
+  HC(rocprim::exclusive_scan(nullptr, tb, in, out, zero, (size_t)n, U3Plus(), E->st));
+  void *tmp = E->A.get<uint8_t>(std::string("scan3.tmp.") + tag, tb);
+  HC(rocprim::exclusive_scan(tmp, tb, in, out, zero, (size_t)n, U3Plus(), E->st));
+  U3 li, lo;
+  HC(hipMemcpyAsync(&li, in + n - 1, sizeof(U3), hipMemcpyDeviceToHost, E->st));
+  HC(hipMemcpyAsync(&lo, out + n - 1, sizeof(U3), hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+  return U3Plus()(li, lo);
+}
+__global__ void k_pack3(const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n, U3 *out) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = U3{a[i], b[i], c[i]};
+}
+__global__ void k_set_offsets_u3(const U3 *scan, uint64_t ba, uint64_t bb, uint64_t bc, uint64_t n, uint64_t *oa, uint64_t *ob,
+                                 uint64_t *oc) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    oa[i] = ba + scan[i].a;
+    ob[i] = bb + scan[i].b;
+    oc[i] = bc + scan[i].c;
+  }
+}
+
 __global__ void k_mark_u8(const uint32_t *ids, uint64_t n, uint8_t *flag) {
   for (uint64_t i = gtid(); i < n; i += gstride()) flag[ids[i]] = 1;
 }
@@ -260,6 +293,34 @@ __global__ void k_view_rows(const uint64_t *soff, const uint32_t *slen, const ui
 }
 __global__ void k_set_offsets(const uint64_t *base_scan, uint64_t base, uint64_t *off, uint64_t n) {
   for (uint64_t i = gtid(); i < n; i += gstride()) off[i] = base + base_scan[i];
+}
+// eq_cluster_simplification's forbidden-pair constraints (:181-187): per forbidden signal f
+// {f in an eq cluster, cluster size, min forbidden of the cluster, max row of the cluster}
+__global__ void k_eq_forb_info(const uint32_t *fl, uint64_t nf, const uint32_t *root, const uint8_t *in_eq, const uint32_t *cnt,
+                               const uint32_t *minf, const int32_t *maxrow, uint32_t *out) {
+  for (uint64_t i = gtid(); i < nf; i += gstride()) {
+    const uint32_t f = fl[i], r = root[i];
+    out[4 * i] = in_eq[f];
+    out[4 * i + 1] = cnt[r];
+    out[4 * i + 2] = minf[r];
+    out[4 * i + 3] = (uint32_t)maxrow[r];
+  }
+}
+// rows whose two signals are forbidden: {row, keys, size of the row's cluster, the two values}
+__global__ void k_eq_bf_info(const uint32_t *bf, uint64_t n, const uint64_t *ptr, const uint32_t *key, const Fe *val,
+                             const uint32_t *uf, const uint32_t *cnt, uint64_t *rec) {
+  for (uint64_t q = gtid(); q < n; q += gstride()) {
+    const uint32_t r = bf[q];
+    const uint64_t p0 = ptr[r];
+    const uint32_t k0 = key[p0], k1 = key[p0 + 1];
+    uint32_t x = k0;  // roots are compressed after k_eq_assign; walk to be safe
+    while (uf[x] != x) x = uf[x];
+    uint64_t *o = rec + 11 * q;
+    o[0] = r;
+    o[1] = ((uint64_t)k1 << 32) | k0;
+    o[2] = cnt[x];
+    for (int t = 0; t < 4; ++t) { o[3 + t] = val[p0].l[t]; o[7 + t] = val[p0 + 1].l[t]; }
+  }
 }
 __global__ void k_flag_linear(const uint32_t *la, const uint32_t *lb, uint64_t n, uint64_t *flag_lin, uint64_t *flag_nl) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
@@ -337,6 +398,37 @@ __global__ void k_emit_pairs(DRows a, DRows b, DRows c, const uint8_t *flag, uin
       }
     }
   }
+}
+
+// ---------------------------------------------------------------- round ordering (rounds >= 2)
+// the valid substitution slots of a round (slot - cluster start < #subs of the cluster)
+__global__ void k_sub_valid(const uint32_t *cid, const uint64_t *cl_off, const uint32_t *n_sub, uint64_t n, uint64_t *flag) {
+  for (uint64_t s = gtid(); s < n; s += gstride()) {
+    const uint32_t c = cid[s];
+    flag[s] = s - cl_off[c] < n_sub[c] ? 1 : 0;
+  }
+}
+__global__ void k_sub_keys(const uint32_t *cid, const uint64_t *flag, const uint64_t *pos, const uint32_t *h_sig, uint64_t n,
+                           uint64_t *key, uint32_t *val) {
+  for (uint64_t s = gtid(); s < n; s += gstride())
+    if (flag[s]) {
+      key[pos[s]] = ((uint64_t)cid[s] << 32) | h_sig[s];
+      val[pos[s]] = (uint32_t)s;
+    }
+}
+// the ordered list: `from`, RHS location, and the dense signal -> rank index
+__global__ void k_sub_info(const uint64_t *key, const uint32_t *U, const uint64_t *h_off, const uint32_t *h_len, uint64_t n,
+                           uint32_t *usig, uint64_t *uoff, uint32_t *ulen, int32_t *rank_of) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t s = (uint32_t)key[i];
+    usig[i] = s;
+    uoff[i] = h_off[U[i]];
+    ulen[i] = h_len[U[i]];
+    rank_of[s] = (int32_t)i;
+  }
+}
+__global__ void k_unset_rank(const uint32_t *sig, uint64_t n, int32_t *rank_of) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) rank_of[sig[i]] = -1;
 }
 
 // ---------------------------------------------------------------- sharded elimination
@@ -1100,9 +1192,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     uint32_t *g_root = A.get<uint32_t>("eq.g_root", nf);
     HC(hipMemsetAsync(g_root, 0, 4 * nf, st));
     launch(st, k_gather_u32, nf, (const uint32_t *)uf, (const uint32_t *)fl_d, g_root, nf);
-    std::vector<uint32_t> root(nf), bfv;
     uint32_t nbf = 0;
-    HC(hipMemcpyAsync(root.data(), g_root, 4 * nf, hipMemcpyDeviceToHost, st));
     HC(hipMemcpyAsync(&nbf, bfn, 4, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
     struct EqCon {
@@ -1111,21 +1201,20 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       HostCon c;
     };
     std::vector<EqCon> eqc;
-    auto fetch1 = [&](const void *dptr, size_t bytes, void *h) {
-      HC(hipMemcpyAsync(h, dptr, bytes, hipMemcpyDeviceToHost, st));
-    };
+    // per forbidden signal: in an eq cluster?  cluster size, min forbidden, max row (one gather)
+    std::vector<uint32_t> finfo(4 * nf);
+    if (nf) {
+      uint32_t *d_fi = A.get<uint32_t>("eq.finfo", 4 * nf);
+      launch(st, k_eq_forb_info, nf, (const uint32_t *)fl_d, nf, (const uint32_t *)g_root, (const uint8_t *)in_eq,
+             (const uint32_t *)cnt, (const uint32_t *)minf, (const int32_t *)maxrow, d_fi);
+      HC(hipMemcpyAsync(finfo.data(), d_fi, 16 * nf, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+    }
     for (uint64_t i = 0; i < nf; ++i) {
       uint32_t f = E->forbidden[i];
-      uint8_t in = 0;
-      fetch1(in_eq + f, 1, &in);
-      HC(hipStreamSynchronize(st));
-      if (!in) continue;
-      uint32_t r = root[i], c = 0, mf = 0;
-      int32_t mr = 0;
-      fetch1(cnt + r, 4, &c);
-      fetch1(minf + r, 4, &mf);
-      fetch1(maxrow + r, 4, &mr);
-      HC(hipStreamSynchronize(st));
+      if (!finfo[4 * i]) continue;
+      uint32_t c = finfo[4 * i + 1], mf = finfo[4 * i + 2];
+      int32_t mr = (int32_t)finfo[4 * i + 3];
       if (c <= 1 || f == mf) continue;
       // transform(sub(Signal f, Signal rh)) = {0: 0, rh: 1, f: -1}
       EqCon e;
@@ -1145,39 +1234,21 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       }
       eqc.push_back(std::move(e));
     }
-    if (nbf) {
-      bfv.resize(nbf);
-      HC(hipMemcpyAsync(bfv.data(), bf, 4 * nbf, hipMemcpyDeviceToHost, st));
+    if (nbf) {  // rows with both ends forbidden: kept as is when they are a cluster of their own
+      std::vector<uint64_t> rec(11 * (uint64_t)nbf);
+      uint64_t *d_rec = A.get<uint64_t>("eq.bfrec", 11 * (uint64_t)nbf);
+      launch(st, k_eq_bf_info, nbf, (const uint32_t *)bf, (uint64_t)nbf, (const uint64_t *)E->eq.ptr,
+             (const uint32_t *)E->eq.key, (const Fe *)E->eq.val, (const uint32_t *)uf, (const uint32_t *)cnt, d_rec);
+      HC(hipMemcpyAsync(rec.data(), d_rec, 88 * (uint64_t)nbf, hipMemcpyDeviceToHost, st));
       HC(hipStreamSynchronize(st));
-      for (uint32_t r : bfv) {
-        uint32_t kk[2];
-        uint64_t p0 = 0;
-        HC(hipMemcpyAsync(&p0, E->eq.ptr + r, 8, hipMemcpyDeviceToHost, st));
-        HC(hipStreamSynchronize(st));
-        HC(hipMemcpyAsync(kk, E->eq.key + p0, 8, hipMemcpyDeviceToHost, st));
-        HC(hipStreamSynchronize(st));
-        uint32_t rt = 0, c = 0;
-        // root of the row: the smaller signal's root (roots are compressed after k_eq_assign)
-        uint32_t x = kk[0];
-        for (;;) {
-          uint32_t px = 0;
-          HC(hipMemcpyAsync(&px, uf + x, 4, hipMemcpyDeviceToHost, st));
-          HC(hipStreamSynchronize(st));
-          if (px == x) break;
-          x = px;
-        }
-        rt = x;
-        HC(hipMemcpyAsync(&c, cnt + rt, 4, hipMemcpyDeviceToHost, st));
-        HC(hipStreamSynchronize(st));
-        if (c != 1) continue;  // a single-constraint cluster with both ends forbidden: kept as is
+      for (uint32_t q = 0; q < nbf; ++q) {
+        const uint64_t *x = &rec[11 * (uint64_t)q];
+        if (x[2] != 1) continue;  // a single-constraint cluster with both ends forbidden: kept as is
         EqCon e;
-        e.order = r;
+        e.order = (int64_t)x[0];
         e.f = 0;
-        uint64_t v[8];
-        HC(hipMemcpyAsync(v, E->eq.val + p0, 64, hipMemcpyDeviceToHost, st));
-        HC(hipStreamSynchronize(st));
-        e.c.k[2] = {kk[0], kk[1]};
-        e.c.v[2].assign(v, v + 8);
+        e.c.k[2] = {(uint32_t)x[1], (uint32_t)(x[1] >> 32)};
+        e.c.v[2].assign(x + 3, x + 11);
         eqc.push_back(std::move(e));
       }
     }
@@ -1344,14 +1415,13 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     a.cap_a = ca; a.cap_b = cb; a.cap_c = cc;
     a.bytes = d_bytes;
     launch(st, k_nl_count, n_nl, a);
-    uint64_t ta = excl_scan_u64(E, ca, A.get<uint64_t>("nl.sa", n_nl), n_nl, "a");
-    uint64_t tb = excl_scan_u64(E, cb, A.get<uint64_t>("nl.sb", n_nl), n_nl, "b");
-    uint64_t tc = excl_scan_u64(E, cc, A.get<uint64_t>("nl.sc", n_nl), n_nl, "c");
-    heap_reserve(ta + tb + tc);
-    launch(st, k_set_offsets, n_nl, (const uint64_t *)A.get<uint64_t>("nl.sa", 1), heap_top, sa.off, n_nl);
-    launch(st, k_set_offsets, n_nl, (const uint64_t *)A.get<uint64_t>("nl.sb", 1), heap_top + ta, sb.off, n_nl);
-    launch(st, k_set_offsets, n_nl, (const uint64_t *)A.get<uint64_t>("nl.sc", 1), heap_top + ta + tb, sc.off, n_nl);
-    heap_top += ta + tb + tc;
+    U3 *cap3 = A.get<U3>("nl.c3", n_nl), *sc3 = A.get<U3>("nl.s3", n_nl);
+    launch(st, k_pack3, n_nl, (const uint64_t *)ca, (const uint64_t *)cb, (const uint64_t *)cc, n_nl, cap3);
+    const U3 t3 = excl_scan_u3(E, cap3, sc3, n_nl, "nl");
+    heap_reserve(t3.a + t3.b + t3.c);
+    launch(st, k_set_offsets_u3, n_nl, (const U3 *)sc3, heap_top, heap_top + t3.a, heap_top + t3.a + t3.b, n_nl, sa.off, sb.off,
+           sc.off);
+    heap_top += t3.a + t3.b + t3.c;
     sa.key = sb.key = sc.key = heap_k;
     sa.val = sb.val = sc.val = heap_v;
     a.oa = sa; a.ob = sb; a.oc = sc;
@@ -1497,45 +1567,42 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       collect_leftovers(E, er, P, lconst);
       MK.mark("leftovers");
       double Tr = now_ms();
-      // ordered substitutions of the round: cluster order, ascending `from`
-      uint64_t n_slots = er.cl_off.back();
-      std::vector<uint32_t> hsig(n_slots);
-      std::vector<uint64_t> hoff(n_slots);
-      std::vector<uint32_t> hlen(n_slots);
+      // ordered substitutions of the round: cluster order, ascending `from` -- one sort of the
+      // (cluster, from) keys of the valid slots on the device; the host fetches the list only when
+      // a row turned linear or another round follows
+      const uint64_t n_slots = er.cl_off.back();
+      uint64_t nU = 0;
+      uint32_t *d_us = A.get<uint32_t>("r.us", 1), *d_U = A.get<uint32_t>("r.U", 1), *d_ulen = A.get<uint32_t>("r.ulen", 1);
+      uint64_t *d_uoff = A.get<uint64_t>("r.uoff", 1);
       if (n_slots) {
-        HC(hipMemcpyAsync(hsig.data(), A.get<uint32_t>("el.h_sig", 1), 4 * n_slots, hipMemcpyDeviceToHost, st));
-        HC(hipMemcpyAsync(hoff.data(), A.get<uint64_t>("el.h_off", 1), 8 * n_slots, hipMemcpyDeviceToHost, st));
-        HC(hipMemcpyAsync(hlen.data(), A.get<uint32_t>("el.h_len", 1), 4 * n_slots, hipMemcpyDeviceToHost, st));
+        uint64_t *vf = A.get<uint64_t>("r.vf", n_slots), *vp = A.get<uint64_t>("r.vp", n_slots);
+        launch(st, k_sub_valid, n_slots, (const uint32_t *)A.get<uint32_t>("cl.cid", 1), (const uint64_t *)A.get<uint64_t>("el.cl", 1),
+               (const uint32_t *)A.get<uint32_t>("el.n_sub", 1), n_slots, vf);
+        nU = excl_scan_u64(E, vf, vp, n_slots, "vf");
+        if (nU) {
+          uint64_t *uk = A.get<uint64_t>("r.uk", nU), *uk2 = A.get<uint64_t>("r.uk2", nU);
+          uint32_t *uv = A.get<uint32_t>("r.uv", nU);
+          d_U = A.get<uint32_t>("r.U", nU);
+          d_us = A.get<uint32_t>("r.us", nU);
+          d_uoff = A.get<uint64_t>("r.uoff", nU);
+          d_ulen = A.get<uint32_t>("r.ulen", nU);
+          launch(st, k_sub_keys, n_slots, (const uint32_t *)A.get<uint32_t>("cl.cid", 1), (const uint64_t *)vf,
+                 (const uint64_t *)vp, (const uint32_t *)A.get<uint32_t>("el.h_sig", 1), n_slots, uk, uv);
+          int cbits = 1;
+          while (cbits < 32 && (1ull << cbits) <= er.n_clusters) ++cbits;
+          sort_pairs(E, (const uint64_t *)uk, uk2, (const uint32_t *)uv, d_U, nU, 32 + cbits, "us");
+          launch(st, k_sub_info, nU, (const uint64_t *)uk2, (const uint32_t *)d_U, (const uint64_t *)A.get<uint64_t>("el.h_off", 1),
+                 (const uint32_t *)A.get<uint32_t>("el.h_len", 1), nU, d_us, d_uoff, d_ulen, rank_of);
+        }
+      }
+      std::vector<uint32_t> usig;  // host copy of the ordered `from` list, fetched on demand
+      auto need_usig = [&]() {
+        if (usig.size() == nU) return;
+        usig.resize(nU);
+        HC(hipMemcpyAsync(usig.data(), d_us, 4 * nU, hipMemcpyDeviceToHost, st));
         HC(hipStreamSynchronize(st));
-      }
-      std::vector<uint32_t> U;      // slots in order
-      for (uint64_t c = 0; c < er.n_clusters; ++c) {
-        uint64_t b = er.cl_off[c];
-        std::vector<uint32_t> sl(er.n_sub[c]);
-        for (uint32_t i = 0; i < er.n_sub[c]; ++i) sl[i] = (uint32_t)(b + i);
-        std::sort(sl.begin(), sl.end(), [&](uint32_t x, uint32_t y) { return hsig[x] < hsig[y]; });
-        U.insert(U.end(), sl.begin(), sl.end());
-      }
-      uint64_t nU = U.size();
+      };
       MK.mark("order");
-      // RHS keys of the substitutions (for the map appends)
-      std::vector<uint64_t> uoff(nU);
-      std::vector<uint32_t> ulen(nU), ukeys;
-      std::vector<uint64_t> uvals, uptr;
-      for (uint64_t i = 0; i < nU; ++i) { uoff[i] = hoff[U[i]]; ulen[i] = hlen[U[i]]; }
-      fetch_pool_maps(E, uoff, ulen, P.pk, P.pv, ukeys, uvals, uptr);
-      MK.mark("fetch_rhs");
-      std::vector<uint32_t> usig(nU);
-      std::vector<int32_t> urank(nU);
-      for (uint64_t i = 0; i < nU; ++i) { usig[i] = hsig[U[i]]; urank[i] = (int32_t)i; }
-      MK.mark("query");
-      uint32_t *d_us = A.get<uint32_t>("r.us", nU);
-      int32_t *d_ur = A.get<int32_t>("r.ur", nU);
-      if (nU) {
-        h2d(E, d_us, usig.data(), 4 * nU);
-        h2d(E, d_ur, urank.data(), 4 * nU);
-        launch(st, k_set_rank, nU, (const uint32_t *)d_us, (const int32_t *)d_ur, nU, rank_of);
-      }
       // apply to every storage row (apply_substitution_to_map, :345-396)
       std::vector<std::pair<uint64_t, uint32_t>> turned;  // (order key, storage id)
       if (n_st && nU) {
@@ -1553,28 +1620,28 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         ra.turn = A.get<int32_t>("r.turn", n_st);
         ra.touched = A.get<uint8_t>("r.touched", n_st);
         launch(st, k_round_count, n_st, ra);
-        uint64_t qa = excl_scan_u64(E, ca, A.get<uint64_t>("r.sa", n_st), n_st, "ra");
-        uint64_t qb = excl_scan_u64(E, cb, A.get<uint64_t>("r.sb", n_st), n_st, "rb");
-        uint64_t qc = excl_scan_u64(E, cc, A.get<uint64_t>("r.sc", n_st), n_st, "rc");
-        heap_reserve(qa + qb + qc);
+        U3 *cap3 = A.get<U3>("r.c3", n_st), *sc3 = A.get<U3>("r.s3", n_st);
+        launch(st, k_pack3, n_st, (const uint64_t *)ca, (const uint64_t *)cb, (const uint64_t *)cc, n_st, cap3);
+        const U3 q3 = excl_scan_u3(E, cap3, sc3, n_st, "r");
+        const uint64_t qt = q3.a + q3.b + q3.c;
+        heap_reserve(qt);
         for (DRows *R : {&ta_, &tb_, &tc_, &lv}) { R->key = heap_k; R->val = heap_v; }
         ra.a = ta_; ra.b = tb_; ra.c = tc_;
         DRows oa = ta_, ob = tb_, oc = tc_;
         oa.off = A.get<uint64_t>("r.oa.off", n_st); oa.len = A.get<uint32_t>("r.oa.len", n_st);
         ob.off = A.get<uint64_t>("r.ob.off", n_st); ob.len = A.get<uint32_t>("r.ob.len", n_st);
         oc.off = A.get<uint64_t>("r.oc.off", n_st); oc.len = A.get<uint32_t>("r.oc.len", n_st);
-        launch(st, k_set_offsets, n_st, (const uint64_t *)A.get<uint64_t>("r.sa", 1), heap_top, oa.off, n_st);
-        launch(st, k_set_offsets, n_st, (const uint64_t *)A.get<uint64_t>("r.sb", 1), heap_top + qa, ob.off, n_st);
-        launch(st, k_set_offsets, n_st, (const uint64_t *)A.get<uint64_t>("r.sc", 1), heap_top + qa + qb, oc.off, n_st);
-        heap_top += qa + qb + qc;
+        launch(st, k_set_offsets_u3, n_st, (const U3 *)sc3, heap_top, heap_top + q3.a, heap_top + q3.a + q3.b, n_st, oa.off,
+               ob.off, oc.off);
+        heap_top += qt;
+        ra.c_base = heap_top - q3.c;  // row scratch = 2 * (its C offset - c_base)
         ra.oa = oa; ra.ob = ob; ra.oc = oc;
-        ra.tmpk = A.get<uint32_t>("r.tmpk", 2 * (qc + 1));
-        ra.tmpv = A.get<Fe>("r.tmpv", 2 * (qc + 1));
-        ra.c_base = heap_top - qc;  // row scratch = 2 * (its C offset - c_base)
+        ra.tmpk = A.get<uint32_t>("r.tmpk", 2 * (q3.c + 1));
+        ra.tmpv = A.get<Fe>("r.tmpv", 2 * (q3.c + 1));
         MK.mark("count");
         launch(st, k_round_fill, n_st, ra);
         MK.mark("fill");
-        if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qa + qb + qc);
+        if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qt);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
         // turned rows
         uint64_t *tf = A.get<uint64_t>("r.tf", n_st), *tp = A.get<uint64_t>("r.tp", n_st);
@@ -1583,22 +1650,28 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         uint32_t *tids = A.get<uint32_t>("r.tids", n_turn);
         launch(st, k_scatter_ids, n_st, (const uint64_t *)tf, (const uint64_t *)tp, n_st, tids);
         std::vector<uint32_t> htids(n_turn);
-        std::vector<int32_t> hturn(n_st);
-        if (n_turn) HC(hipMemcpyAsync(htids.data(), tids, 4 * n_turn, hipMemcpyDeviceToHost, st));
-        HC(hipMemcpyAsync(hturn.data(), ra.turn, 4 * n_st, hipMemcpyDeviceToHost, st));
-        HC(hipStreamSynchronize(st));
+        std::vector<int32_t> hturn(n_turn);  // turn value of each turned row (aligned with htids)
+        if (n_turn) {
+          int32_t *d_tt = A.get<int32_t>("r.tturn", n_turn);
+          launch(st, k_gather_u32, n_turn, (const uint32_t *)ra.turn, (const uint32_t *)tids, (uint32_t *)d_tt, n_turn);
+          HC(hipMemcpyAsync(htids.data(), tids, 4 * n_turn, hipMemcpyDeviceToHost, st));
+          HC(hipMemcpyAsync(hturn.data(), d_tt, 4 * n_turn, hipMemcpyDeviceToHost, st));
+          HC(hipStreamSynchronize(st));
+          need_usig();
+        }
         {  // initial map lists of the turning substitutions' signals only
           double Tq = now_ms();
           std::vector<uint32_t> qs;
-          for (uint32_t r : htids) qs.push_back(usig[hturn[r]]);
+          for (uint64_t i = 0; i < n_turn; ++i) qs.push_back(usig[hturn[i]]);
           std::sort(qs.begin(), qs.end());
           qs.erase(std::unique(qs.begin(), qs.end()), qs.end());
           query_initial(qs);
           E->stats.map_ms += now_ms() - Tq;
         }
         // order key: (rank of the turning substitution, first position in map[from])
-        for (uint32_t r : htids) {
-          int32_t q = hturn[r];
+        for (uint64_t ti = 0; ti < n_turn; ++ti) {
+          const uint32_t r = htids[ti];
+          int32_t q = hturn[ti];
           uint32_t from = usig[q];
           uint64_t pos = UINT64_MAX;
           const std::vector<uint32_t> &L0 = minit[from];
@@ -1627,36 +1700,40 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         }
       }
       MK.mark("appends");
-      if (nU) {  // reset the dense rank index
-        std::vector<int32_t> neg(nU, -1);
-        h2d(E, d_ur, neg.data(), 4 * nU);
-        launch(st, k_set_rank, nU, (const uint32_t *)d_us, (const int32_t *)d_ur, nU, rank_of);
-      }
+      if (nU) launch(st, k_unset_rank, nU, (const uint32_t *)d_us, nU, rank_of);  // reset the dense rank index
       // next linear list: the turned rows, non-empty, in linear_id order
       std::vector<uint32_t> next_ids;
       {
-        std::vector<uint32_t> clen(n_st);
-        if (n_st) {
-          HC(hipMemcpyAsync(clen.data(), tc_.len, 4 * n_st, hipMemcpyDeviceToHost, st));
+        if (!turned.empty()) {  // C lengths of the turned rows only
+          std::vector<uint32_t> tid_(turned.size()), tlen(turned.size());
+          for (size_t i = 0; i < turned.size(); ++i) tid_[i] = turned[i].second;
+          uint32_t *d_t = A.get<uint32_t>("r.tid", tid_.size()), *d_tl = A.get<uint32_t>("r.tlen", tid_.size());
+          h2d(E, d_t, tid_.data(), 4 * tid_.size());
+          launch(st, k_gather_u32, tid_.size(), (const uint32_t *)tc_.len, (const uint32_t *)d_t, d_tl, (uint64_t)tid_.size());
+          HC(hipMemcpyAsync(tlen.data(), d_tl, 4 * tlen.size(), hipMemcpyDeviceToHost, st));
           HC(hipStreamSynchronize(st));
+          for (size_t i = 0; i < turned.size(); ++i)
+            if (tlen[i]) next_ids.push_back(turned[i].second);
         }
-        for (auto &t : turned)
-          if (clen[t.second]) next_ids.push_back(t.second);
       }
       uint64_t nn = next_ids.size();
       // map appends (:369-377): the key set on the device; the row lists (positions for a later
       // round's ordering) only when another round follows
       if (nU) {
-        uint64_t *d_uoff = A.get<uint64_t>("r.uoff", nU);
-        uint32_t *d_ulen = A.get<uint32_t>("r.ulen", nU);
-        h2d(E, d_uoff, uoff.data(), 8 * nU);
-        h2d(E, d_ulen, ulen.data(), 4 * nU);
         launch(st, k_append_marks, nU, (const uint32_t *)d_us, (const uint64_t *)d_uoff, (const uint32_t *)d_ulen, nU,
                (const uint32_t *)P.pk, nlmap);
       }
       const bool another = nn > 0 && (no_rounds > 0 ? no_rounds - 1 : 0) > 0;
       if (another) {
         double Tq = now_ms();
+        need_usig();
+        // RHS keys of the substitutions (the map appends of the next round's ordering)
+        std::vector<uint64_t> uoff(nU), uvals, uptr;
+        std::vector<uint32_t> ulen(nU), ukeys;
+        HC(hipMemcpyAsync(uoff.data(), d_uoff, 8 * nU, hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(ulen.data(), d_ulen, 4 * nU, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+        fetch_pool_maps(E, uoff, ulen, P.pk, P.pv, ukeys, uvals, uptr);
         query_initial(usig);
         E->stats.map_ms += now_ms() - Tq;
         for (uint64_t i = 0; i < nU; ++i) {
