@@ -41,7 +41,8 @@ class RsFlags(C.Structure):
 class RsOutput(C.Structure):
     _fields_ = [("n_constraints", C.c_uint64), ("a", RsLc), ("b", RsLc), ("c", RsLc),
                 ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int64)),
-                ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64)]
+                ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64),
+                ("n_log", C.c_uint64), ("log_from", C.POINTER(C.c_uint32)), ("log_to", RsLc)]
 
 
 class RsStats(C.Structure):
@@ -85,6 +86,8 @@ SYMBOLS = [
     ("rs_input_free", None, [C.POINTER(RsInput)]),
     ("rs_write_r1cs", C.c_int, [C.c_char_p, C.POINTER(RsInput), C.POINTER(RsOutput)]),
     ("rs_write_sym", C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(RsOutput)]),
+    ("rs_write_constraints_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),
+    ("rs_write_substitution_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),
     ("rs_synth", C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(RsInput))]),
 ]
 
@@ -117,9 +120,11 @@ def check(rc: int):
         raise RsError(rc, lib().rs_last_error().decode(errors="replace"))
 
 
-def make_flags(level: str = "O2", rounds: int | None = None, old: bool = False, device: int = 0) -> RsFlags:
-    """--O1 / --O2 / --O2round N (circom/src/input_user.rs:286-306)."""
+def make_flags(level: str = "O2", rounds: int | None = None, old: bool = False, device: int = 0,
+               log: bool = False) -> RsFlags:
+    """--O1 / --O2 / --O2round N (circom/src/input_user.rs:286-306); log = --simplification_substitution."""
     f = RsFlags()
+    f.emit_substitution_log = 1 if log else 0
     if level == "O1" or rounds == 0:
         f.flag_s, f.no_rounds = 1, 0
     elif level == "O2":

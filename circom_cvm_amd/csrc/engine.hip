@@ -162,6 +162,10 @@ struct rs_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr, ev6 = nullptr;
   // sharded elimination: this engine is rank `comm->rank` of `comm->world`
   std::unique_ptr<rs::Comm> comm;
+  // substitution log of the last run (rs_flags.emit_substitution_log), canonical values
+  bool log_on = false;
+  std::vector<uint32_t> log_from, log_key;
+  std::vector<uint64_t> log_ptr, log_val;
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
@@ -1046,6 +1050,51 @@ static void collect_leftovers(rs_engine *E, const ElimOut &eo, const Pool &P, st
   }
 }
 
+// ---------------------------------------------------------------- substitution log
+static void log_push(rs_engine *E, uint32_t from, const uint32_t *k, const uint64_t *v, uint64_t n) {
+  E->log_from.push_back(from);
+  E->log_key.insert(E->log_key.end(), k, k + n);
+  E->log_val.insert(E->log_val.end(), v, v + 4 * n);
+  E->log_ptr.push_back(E->log_key.size());
+}
+// linear_simplification's log_substitutions (:318-320) for the round just eliminated: the valid
+// slots in cluster order, ascending `from` inside a cluster (one sort of (cluster, from) keys),
+// then the canonical content of each normalised, non-overlapping right-hand side.
+static void log_linear_round(rs_engine *E, const ElimOut &eo, const Pool &P) {
+  Arena &A = E->A;
+  hipStream_t st = E->st;
+  const uint64_t n_slots = eo.cl_off.empty() ? 0 : eo.cl_off.back();
+  if (!n_slots) return;
+  uint64_t *vf = A.get<uint64_t>("lg.vf", n_slots), *vp = A.get<uint64_t>("lg.vp", n_slots);
+  const uint32_t *cid = A.get<uint32_t>("cl.cid", 1);
+  launch(st, k_sub_valid, n_slots, cid, (const uint64_t *)A.get<uint64_t>("el.cl", 1),
+         (const uint32_t *)A.get<uint32_t>("el.n_sub", 1), n_slots, vf);
+  const uint64_t nU = excl_scan_u64(E, vf, vp, n_slots, "lgvf");
+  if (!nU) return;
+  uint64_t *uk = A.get<uint64_t>("lg.uk", nU), *uk2 = A.get<uint64_t>("lg.uk2", nU);
+  uint32_t *uv = A.get<uint32_t>("lg.uv", nU), *U = A.get<uint32_t>("lg.U", nU);
+  launch(st, k_sub_keys, n_slots, cid, (const uint64_t *)vf, (const uint64_t *)vp,
+         (const uint32_t *)A.get<uint32_t>("el.h_sig", 1), n_slots, uk, uv);
+  int cbits = 1;
+  while (cbits < 32 && (1ull << cbits) <= eo.n_clusters) ++cbits;
+  sort_pairs(E, (const uint64_t *)uk, uk2, (const uint32_t *)uv, U, nU, 32 + cbits, "lgus");
+  std::vector<uint64_t> keys(nU), hoff(nU);
+  std::vector<uint32_t> slots(nU), hlen(nU);
+  uint64_t *d_off = A.get<uint64_t>("lg.off", nU);
+  uint32_t *d_len = A.get<uint32_t>("lg.len", nU);
+  launch(st, k_gather_u64, nU, (const uint64_t *)A.get<uint64_t>("el.h_off", 1), (const uint32_t *)U, d_off, nU);
+  launch(st, k_gather_u32, nU, (const uint32_t *)A.get<uint32_t>("el.h_len", 1), (const uint32_t *)U, d_len, nU);
+  HC(hipMemcpyAsync(keys.data(), uk2, 8 * nU, hipMemcpyDeviceToHost, st));
+  HC(hipMemcpyAsync(hoff.data(), d_off, 8 * nU, hipMemcpyDeviceToHost, st));
+  HC(hipMemcpyAsync(hlen.data(), d_len, 4 * nU, hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  std::vector<uint32_t> rk;
+  std::vector<uint64_t> rv, rptr;
+  fetch_pool_maps(E, hoff, hlen, P.pk, P.pv, rk, rv, rptr);
+  for (uint64_t i = 0; i < nU; ++i)
+    log_push(E, (uint32_t)keys[i], rk.data() + rptr[i], rv.data() + 4 * rptr[i], rptr[i + 1] - rptr[i]);
+}
+
 // ---------------------------------------------------------------- debug: host re-check of a round
 static void d2h_row(rs_engine *E, const DRows &R, uint64_t r, std::vector<uint32_t> &k, std::vector<Fe> &v) {
   uint64_t off = 0;
@@ -1159,6 +1208,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   HC(hipMemsetAsync(sub_of, 0xff, 4 * S, st));
 
   std::vector<HostCon> lconst;
+  E->log_on = fl->emit_substitution_log != 0;
+  E->log_from.clear();
+  E->log_key.clear();
+  E->log_val.clear();
+  E->log_ptr.assign(1, 0);
 
   // ======================= eq_simplification (:198-251) + renaming of linear / cons_eq rows
   int32_t *eq_rep = A.get<int32_t>("eq_rep", S);
@@ -1185,6 +1239,26 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
              (const uint8_t *)d_forb, cnt, maxrow, minf, minr, in_eq);
       launch(st, k_eq_assign, E->eq.n, (const uint64_t *)E->eq.ptr, (const uint32_t *)E->eq.key, E->eq.n, uf,
              (const uint8_t *)d_forb, (const uint32_t *)minf, (const uint32_t *)minr, eq_rep, d_deleted, bf, bfn);
+    }
+    if (E->log_on && E->eq.n) {  // log_substitutions (:249)
+      uint64_t *lk = A.get<uint64_t>("lg.eqk", S), *lk2 = A.get<uint64_t>("lg.eqk2", S);
+      uint32_t *lr = A.get<uint32_t>("lg.eqr", S), *lr2 = A.get<uint32_t>("lg.eqr2", S);
+      unsigned long long *ln = A.get<unsigned long long>("lg.eqn", 1);
+      HC(hipMemsetAsync(ln, 0, 8, st));
+      launch(st, k_eq_log_keys, S, (const int32_t *)eq_rep, uf, (const uint32_t *)cnt, (const int32_t *)maxrow, S, lk, lr, ln);
+      unsigned long long nlog = 0;
+      HC(hipMemcpyAsync(&nlog, ln, 8, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      sort_pairs(E, (const uint64_t *)lk, lk2, (const uint32_t *)lr, lr2, nlog, 64, "lgeq");
+      std::vector<uint64_t> hk(nlog);
+      std::vector<uint32_t> hr(nlog);
+      if (nlog) {
+        HC(hipMemcpyAsync(hk.data(), lk2, 8 * nlog, hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(hr.data(), lr2, 4 * nlog, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+      }
+      const uint64_t one[4] = {1, 0, 0, 0};
+      for (uint64_t i = 0; i < nlog; ++i) log_push(E, (uint32_t)hk[i], &hr[i], one, 1);  // Substitution::new(Signal)
     }
     // eq cons (forbidden-only constraints), ordered by cluster index (= max row) then signal
     uint64_t nf = E->forbidden.size();
@@ -1275,6 +1349,19 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   if (lin.n) launch(st, k_make_ragged, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
                     lin.n, (uint64_t)1, lin.off, lin.len, lin.key, lin.val);
   if (ce.n) launch(st, k_rename_rows, ce.n, E->F, ce, (const int32_t *)eq_rep);
+  if (E->log_on && ce.n) {  // log_substitutions (:271), row order
+    uint32_t *lsig = A.get<uint32_t>("lg.cesig", ce.n);
+    uint64_t *lval = A.get<uint64_t>("lg.ceval", 4 * ce.n);
+    launch(st, k_const_log, ce.n, E->F, ce, (const uint8_t *)d_forb, lsig, lval);
+    std::vector<uint32_t> hs(ce.n);
+    std::vector<uint64_t> hv(4 * ce.n);
+    HC(hipMemcpyAsync(hs.data(), lsig, 4 * ce.n, hipMemcpyDeviceToHost, st));
+    HC(hipMemcpyAsync(hv.data(), lval, 32 * ce.n, hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    const uint32_t k0 = 0;
+    for (uint64_t r = 0; r < ce.n; ++r)
+      if (hs[r] != RS_NONE) log_push(E, hs[r], &k0, &hv[4 * r], is_zero4(&hv[4 * r]) ? 0 : 1);
+  }
 
   // ======================= constant_eq_simplification (:253-273)
   int32_t *ce_last = A.get<int32_t>("ce.last", S);
@@ -1324,6 +1411,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   Pool P = get_pool(E, 1 << 20);
   if (apply_linear) {
     run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted);
+    if (E->log_on) log_linear_round(E, eo, P);
     collect_leftovers(E, eo, P, lconst);
     E->stats.rounds++;
   } else {
@@ -1560,6 +1648,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       ElimOut er;
       HC(hipMemsetAsync(r_sub_of, 0xff, 4 * S, st));
       run_linear_simplification(E, lv, fl->use_old_heuristics, er, P, d_err, d_forb, r_sub_of, d_deleted);
+      if (E->log_on) log_linear_round(E, er, P);
       E->stats.rounds++;
       Marks MK;
       MK.st = st;
@@ -2068,6 +2157,22 @@ int rs_engine_fetch(rs_engine *E, rs_output **out) {
     HC(hipStreamSynchronize(E->st));
     o->n_wires = E->n_wires;
     o->no_private_inputs_witness = E->npiw;
+    if (E->log_on) {
+      const uint64_t n = E->log_from.size(), nnz = E->log_key.size();
+      o->n_log = n;
+      o->log_from = (uint32_t *)malloc(4 * (n ? n : 1));
+      o->log_to.n_rows = n;
+      o->log_to.nnz = nnz;
+      o->log_to.ptr = (uint64_t *)malloc(8 * (n + 1));
+      o->log_to.col = (uint32_t *)malloc(4 * (nnz ? nnz : 1));
+      o->log_to.val = (uint64_t *)malloc(32 * (nnz ? nnz : 1));
+      if (n) memcpy(o->log_from, E->log_from.data(), 4 * n);
+      memcpy(o->log_to.ptr, E->log_ptr.data(), 8 * (n + 1));
+      if (nnz) {
+        memcpy(o->log_to.col, E->log_key.data(), 4 * nnz);
+        memcpy(o->log_to.val, E->log_val.data(), 32 * nnz);
+      }
+    }
     *out = o;
     return RS_OK;
   } catch (const RsError &e) {
@@ -2085,6 +2190,8 @@ void rs_output_free(rs_output *o) {
   free_lc(o->b);
   free_lc(o->c);
   free(o->label_to_wire);
+  free(o->log_from);
+  free_lc(o->log_to);
   free(o);
 }
 

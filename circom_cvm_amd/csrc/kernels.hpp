@@ -190,6 +190,9 @@ __global__ void k_eq_assign(const uint64_t *ptr, const uint32_t *key, uint64_t n
 __global__ void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t *dst, uint64_t n) {
   for (uint64_t i = gtid(); i < n; i += gstride()) dst[i] = src[idx[i]];
 }
+__global__ void k_gather_u64(const uint64_t *src, const uint32_t *idx, uint64_t *dst, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) dst[i] = src[idx[i]];
+}
 
 // ---------------------------------------------------------------- constant equalities (:253-273)
 // Applies the eq frame (fast_encoded_constraint_substitution + fix) to a C-only row in place;
@@ -2087,6 +2090,38 @@ __global__ void k_pool_to_canon(FieldP F, const uint64_t *off, const uint32_t *l
       Fe c = ffrom_mont(F, pv[off[i] + t]);
       for (int q = 0; q < 4; ++q) ov[4 * (o + t) + q] = c.l[q];
     }
+  }
+}
+
+// ---------------------------------------------------------------- substitution log
+// eq_simplification's substitutions (constraint_simplification.rs:198-251) in log order: every
+// renamed signal s (eq_rep[s] = its representative) keyed by (cluster of more than one row,
+// cluster index = max row, s) -- size-1 clusters are logged first (:219-223), the others by
+// cluster id (:240-244), each cluster's removable signals ascending (:188-192, canonical).
+__global__ void k_eq_log_keys(const int32_t *eq_rep, uint32_t *uf, const uint32_t *cnt, const int32_t *maxrow, uint64_t S,
+                              uint64_t *key, uint32_t *rep, unsigned long long *n) {
+  for (uint64_t s = gtid(); s < S; s += gstride()) {
+    const int32_t r = eq_rep[s];
+    if (r < 0) continue;
+    const uint32_t root = uf_find(uf, (uint32_t)s);
+    const unsigned long long i = atomicAdd(n, 1ull);
+    key[i] = ((uint64_t)(cnt[root] > 1) << 63) | ((uint64_t)(uint32_t)maxrow[root] << 32) | s;
+    rep[i] = (uint32_t)r;
+  }
+}
+// constant_eq_simplification's substitutions (:253-273) per cons_eq row, in row order: the row's
+// largest signal s (take_cloned_signals_ordered().pop()) := clear_signal (algebra.rs:1108-1124)
+// = c / (-k) with zeros removed; sig = RS_NONE when s is forbidden (the row stays a constraint).
+__global__ void k_const_log(FieldP F, DRows R, const uint8_t *forb, uint32_t *sig, uint64_t *val) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride()) {
+    const uint32_t *k = R.key + R.off[r];
+    const Fe *v = R.val + R.off[r];
+    const uint32_t n = R.len[r];
+    const uint32_t s = n ? k[n - 1] : 0;
+    sig[r] = (n == 0 || forb[s]) ? RS_NONE : s;
+    Fe x = fe_zero();
+    if (n && !forb[s] && n == 2 && k[0] == 0) x = ffrom_mont(F, fmul(F, v[0], finv(F, fneg(F, v[n - 1]))));
+    for (int q = 0; q < 4; ++q) val[4 * r + q] = x.l[q];
   }
 }
 

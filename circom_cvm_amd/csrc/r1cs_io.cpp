@@ -8,6 +8,9 @@
 //                     keys written in lexicographic order of their minimal little-endian bytes).
 //   rs_write_sym    : constraint_list/src/sym_porting.rs:5-37 -- the --O0 .sym lines with the
 //                     witness column remapped (-1 when the label is not a wire).
+//   rs_write_constraints_json / rs_write_substitution_json : the --json and
+//                     --simplification_substitution outputs (constraint_list/src/json_porting.rs,
+//                     constraint_writers/src/json_writer.rs).
 #include <algorithm>
 #include <cstdio>
 #include <fstream>
@@ -61,6 +64,54 @@ static inline uint64_t le_order_key(uint32_t k) {
 }  // namespace rs
 
 using namespace rs;
+
+// BigInt::to_str_radix(10) of a canonical 4-limb value
+static std::string dec_string(const uint64_t *v) {
+  uint64_t x[4] = {v[0], v[1], v[2], v[3]};
+  char buf[96];
+  int n = 0;
+  do {
+    unsigned __int128 rem = 0;  // x /= 10^19, digits of the remainder
+    for (int i = 3; i >= 0; --i) {
+      unsigned __int128 cur = (rem << 64) | x[i];
+      x[i] = (uint64_t)(cur / 10000000000000000000ull);
+      rem = cur % 10000000000000000000ull;
+    }
+    uint64_t r = (uint64_t)rem;
+    const bool last = (x[0] | x[1] | x[2] | x[3]) == 0;
+    for (int d = 0; d < 19 && (!last || r || d == 0); ++d) { buf[n++] = (char)('0' + r % 10); r /= 10; }
+  } while (x[0] | x[1] | x[2] | x[3]);
+  std::string s(buf, buf + n);
+  std::reverse(s.begin(), s.end());
+  return s;
+}
+
+// hashmap_as_json (json_porting.rs:16-26) + JsonValue::to_string: {"k":"v",...}, keys ascending
+// (as numbers), `ids` mapped through `l2w` when given (apply_correspondence).
+static bool map_json(std::string &o, const rs_lc &L, uint64_t r, const int64_t *l2w, uint64_t n_labels) {
+  std::vector<std::pair<uint64_t, uint64_t>> ord;  // (key, entry)
+  for (uint64_t e = L.ptr[r]; e < L.ptr[r + 1]; ++e) {
+    uint64_t k = L.col[e];
+    if (l2w) {
+      int64_t w = k < n_labels ? l2w[k] : -1;
+      if (w < 0) return false;
+      k = (uint64_t)w;
+    }
+    ord.push_back({k, e});
+  }
+  std::sort(ord.begin(), ord.end());
+  o += '{';
+  for (size_t i = 0; i < ord.size(); ++i) {
+    if (i) o += ',';
+    o += '"';
+    o += std::to_string(ord[i].first);
+    o += "\":\"";
+    o += dec_string(L.val + 4 * ord[i].second);
+    o += '"';
+  }
+  o += '}';
+  return true;
+}
 
 extern "C" {
 
@@ -255,6 +306,53 @@ int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out) {
   put64(hdr, 8 * out->n_wires);
   fwrite(hdr.data(), 1, hdr.size(), f);
   fwrite(w2l.data(), 8, w2l.size(), f);
+  bool ok = !ferror(f);
+  fclose(f);
+  if (!ok) { set_error("write error"); return RS_E_INVALID; }
+  return RS_OK;
+}
+
+int rs_write_constraints_json(const char *path, const rs_output *out) {
+  FILE *f = fopen(path, "wb");
+  if (!f) { set_error(std::string("cannot write ") + path); return RS_E_INVALID; }
+  // ConstraintJSON::new / write_constraint / end (json_writer.rs:10-45)
+  fputs("{\n\"constraints\": [", f);
+  std::string line;
+  const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
+  for (uint64_t r = 0; r < out->n_constraints; ++r) {
+    line.assign(r ? ",\n[" : "\n[");
+    for (int q = 0; q < 3; ++q) {
+      if (q) line += ',';
+      if (!map_json(line, *parts[q], r, out->label_to_wire, out->n_labels)) {
+        fclose(f);
+        set_error("constraint mentions a removed signal (apply_correspondence panics)");
+        return RS_E_INTERNAL;
+      }
+    }
+    line += ']';
+    fwrite(line.data(), 1, line.size(), f);
+  }
+  fputs("\n]\n}", f);
+  bool ok = !ferror(f);
+  fclose(f);
+  if (!ok) { set_error("write error"); return RS_E_INVALID; }
+  return RS_OK;
+}
+
+int rs_write_substitution_json(const char *path, const rs_output *out) {
+  FILE *f = fopen(path, "wb");
+  if (!f) { set_error(std::string("cannot write ") + path); return RS_E_INVALID; }
+  // SubstitutionJSON::new / write_substitution / end (json_writer.rs:99-131)
+  fputs("{", f);
+  std::string line;
+  for (uint64_t i = 0; i < out->n_log; ++i) {
+    line.assign(i ? ",\n\"" : "\n\"");
+    line += std::to_string(out->log_from[i]);
+    line += "\" : ";
+    map_json(line, out->log_to, i, nullptr, 0);
+    fwrite(line.data(), 1, line.size(), f);
+  }
+  fputs("\n}", f);
   bool ok = !ferror(f);
   fclose(f);
   if (!ok) { set_error("write error"); return RS_E_INVALID; }

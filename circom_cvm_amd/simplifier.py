@@ -65,6 +65,34 @@ class ConstraintList:
     def sym(self, o0_sym: str, out: str) -> None:
         check(lib().rs_write_sym(o0_sym.encode(), out.encode(), self._out.ptr))
 
+    def json_constraints_file(self, out: str) -> None:
+        """ConstraintExporter::json_constraints (constraint_list/src/lib.rs:195-201): --json."""
+        check(lib().rs_write_constraints_json(out.encode(), self._out.ptr))
+
+    def substitutions(self) -> list:
+        """The --simplification_substitution log as [(from, {signal: value})] (original ids, reference
+        order); empty unless the Simplifier was built with port_substitution=True."""
+        o = self._out.c
+        n = int(o.n_log)
+        if n == 0:
+            return []
+        frm = np.ctypeslib.as_array(o.log_from, shape=(n,))
+        ptr = np.ctypeslib.as_array(o.log_to.ptr, shape=(n + 1,))
+        nnz = int(ptr[n])
+        col = np.ctypeslib.as_array(o.log_to.col, shape=(max(nnz, 1),))
+        val = np.ctypeslib.as_array(o.log_to.val, shape=(max(nnz, 1) * 4,))
+        res = []
+        for i in range(n):
+            m = {}
+            for e in range(int(ptr[i]), int(ptr[i + 1])):
+                m[int(col[e])] = sum(int(val[4 * e + t]) << (64 * t) for t in range(4))
+            res.append((int(frm[i]), m))
+        return res
+
+    def substitution_json_file(self, out: str) -> None:
+        """SubstitutionJSON (constraint_writers/src/json_writer.rs:94-131) of the log."""
+        check(lib().rs_write_substitution_json(out.encode(), self._out.ptr))
+
     def json_constraints(self) -> list:
         """constraint_list/src/json_porting.rs:8-48 as Python objects (wire ids, decimal strings)."""
         o = self._out.c
@@ -96,12 +124,13 @@ class Simplifier:
     """constraint_list::Simplifier (lib.rs:110-153) over an rs_input bundle."""
 
     def __init__(self, inp: Input | RsInput, no_rounds: int | None = None, flag_s: bool = False,
-                 flag_old_heuristics: bool = False, device: int = 0):
+                 flag_old_heuristics: bool = False, device: int = 0, port_substitution: bool = False):
         self.inp = inp
         if flag_s:
-            self.flags = make_flags("O1", old=flag_old_heuristics, device=device)
+            self.flags = make_flags("O1", old=flag_old_heuristics, device=device, log=port_substitution)
         else:
-            self.flags = make_flags("O2", rounds=no_rounds, old=flag_old_heuristics, device=device)
+            self.flags = make_flags("O2", rounds=no_rounds, old=flag_old_heuristics, device=device,
+                                    log=port_substitution)
         self.device = device
 
     def no_labels(self) -> int:

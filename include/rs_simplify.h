@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 2
+#define RS_ABI_VERSION 3
 
 enum rs_status {
   RS_OK = 0,
@@ -99,7 +99,7 @@ typedef struct rs_flags {
   uint32_t flag_s;             /* --O1: no linear elimination (apply_linear = !flag_s)      */
   uint32_t use_old_heuristics; /* --use_old_simplification_heuristics                        */
   uint64_t no_rounds;          /* UINT64_MAX for --O2, N for --O2round N, 0 for --O1         */
-  uint32_t emit_substitution_log; /* --simplification_substitution (reserved)                */
+  uint32_t emit_substitution_log; /* --simplification_substitution: fill rs_output.log_*     */
   int32_t device;              /* HIP device ordinal                                        */
 } rs_flags;
 
@@ -115,6 +115,16 @@ typedef struct rs_output {
   int64_t *label_to_wire;         /* n_labels entries, -1 = not a wire                      */
   uint64_t n_wires;               /* = SignalMap.len()                                      */
   uint64_t no_private_inputs_witness;
+  /* The substitution log (--simplification_substitution, constraint_simplification.rs:9-17),
+   * only when rs_flags.emit_substitution_log: every Substitution the reference hands to
+   * log_substitutions, in its order -- eq_simplification (:249; size-1 clusters, then the others,
+   * by cluster index), constant_eq_simplification (:271; row order), then each round's
+   * linear_simplification (:320; cluster index order, ascending `from`).  Entry i is
+   * log_from[i] := row i of log_to, with ORIGINAL signal ids, keys ascending and the values the
+   * reference's `to` map holds (zero values included, e.g. the constant key's {0: 0}). */
+  uint64_t n_log;
+  uint32_t *log_from;
+  rs_lc log_to;
 } rs_output;
 
 /* Phase timings of the last rs_engine_run (milliseconds, HIP events + host clock). */
@@ -202,6 +212,13 @@ void rs_input_free(rs_input *in);
 int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out);
 /* Rewrites an --O0 .sym with the witness column of `out` (constraint_list/src/sym_porting.rs). */
 int rs_write_sym(const char *o0_sym, const char *path, const rs_output *out);
+/* --json: <prefix>_constraints.json (constraint_list/src/json_porting.rs:36-48 port_constraints,
+ * constraint_writers/src/json_writer.rs:4-45 ConstraintJSON): the rows in storage order with the
+ * witness correspondence applied, keys ascending, decimal values. */
+int rs_write_constraints_json(const char *path, const rs_output *out);
+/* --simplification_substitution: <prefix>_substitutions.json (json_porting.rs:28-33
+ * port_substitution, json_writer.rs:94-131 SubstitutionJSON) from out->log_*, original ids. */
+int rs_write_substitution_json(const char *path, const rs_output *out);
 
 /* Seeded synthetic --O0 systems for benchmarks/tests (see DESIGN.md "Workloads").
  * kind: 0 = mixed (metric circuit), 1 = purely linear, 2 = chain (deep substitution chains). */

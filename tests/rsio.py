@@ -19,8 +19,13 @@ from circom_cvm_amd.abi import (PRIME_IDS, U64_MAX, RsFlags, RsInput, RsLc, RsOu
                                 RsStats, make_flags)
 
 
-def flags(level="O2", rounds=None, old=False, device=0) -> RsFlags:
-    return make_flags(level, rounds, old, device)
+def flags(level="O2", rounds=None, old=False, device=0, log=False) -> RsFlags:
+    return make_flags(level, rounds, old, device, log)
+
+
+def py_flags(fl: RsFlags) -> "R.Flags":
+    """The pyref Flags of an RsFlags."""
+    return R.Flags(flag_s=bool(fl.flag_s), no_rounds=int(fl.no_rounds), use_old_heuristics=bool(fl.use_old_heuristics))
 
 
 # --------------------------------------------------------------------------- pyref <-> C ABI
@@ -113,6 +118,69 @@ def same_result(res: "R.Result", got) -> str | None:
         if (x.a, x.b, x.c) != (y.a, y.b, y.c):
             return f"constraint {i} differs: {x} vs {y}"
     return None
+
+
+def output_log(o: RsOutput):
+    """The substitution log of an rs_output as [(from, {signal: value})] (reference order)."""
+    n = int(o.n_log)
+    if n == 0:
+        return []
+    frm = np.ctypeslib.as_array(o.log_from, shape=(n,))
+    rows = _read_block(o.log_to)
+    return [(int(frm[i]), rows[i]) for i in range(n)]
+
+
+def pyref_log(log):
+    """pyref's log (list of Sub) as [(from, {signal: value})]."""
+    return [(s.frm, dict(s.to)) for s in log]
+
+
+# --------------------------------------------------------------------------- JSON text formats
+# Restatements of the reference writers, for the tests: json_porting.rs:16-26 (hashmap_as_json, keys
+# sorted as numbers, decimal values) with JsonValue::to_string (compact), ConstraintJSON
+# (json_writer.rs:4-45) and SubstitutionJSON (json_writer.rs:94-131).
+def json_map(m: dict) -> str:
+    return "{" + ",".join(f'"{k}":"{m[k]}"' for k in sorted(m)) + "}"
+
+
+def constraints_json_text(cons, signal_map) -> str:
+    """port_constraints (json_porting.rs:36-48): rows with apply_correspondence."""
+    out = '{\n"constraints": ['
+    for i, c in enumerate(cons):
+        row = ",".join(json_map({signal_map[k]: v for k, v in m.items()}) for m in (c.a, c.b, c.c))
+        out += ("\n[" if i == 0 else ",\n[") + row + "]"
+    return out + "\n]\n}"
+
+
+def substitutions_json_text(log) -> str:
+    """log_substitutions -> SubstitutionJSON::write_substitution for each (from, to)."""
+    out = "{"
+    for i, (frm, to) in enumerate(log):
+        out += ("\n" if i == 0 else ",\n") + f'"{frm}" : ' + json_map(to)
+    return out + "\n}"
+
+
+class OutputHolder:
+    """An RsOutput over numpy arrays, built from a pyref Result (+ log): feeds the product's file
+    writers on the CPU."""
+
+    def __init__(self, res: "R.Result", n_labels: int, log=()):
+        self.blocks = [_Block([c.a for c in res.constraints]), _Block([c.b for c in res.constraints]),
+                       _Block([c.c for c in res.constraints])]
+        self.l2w = np.array([res.signal_map.get(i, -1) for i in range(n_labels)] or [0], dtype=np.int64)
+        self.log_blk = _Block([to for _, to in log])
+        self.log_from = np.array([f for f, _ in log] or [0], dtype=np.uint32)
+        o = RsOutput()
+        o.n_constraints = len(res.constraints)
+        o.a, o.b, o.c = [b.lc for b in self.blocks]
+        o.n_labels = n_labels
+        o.label_to_wire = self.l2w.ctypes.data_as(C.POINTER(C.c_int64))
+        o.n_wires = len(res.signal_map)
+        o.no_private_inputs_witness = res.no_private_inputs_witness
+        o.n_log = len(log)
+        o.log_from = self.log_from.ctypes.data_as(C.POINTER(C.c_uint32))
+        o.log_to = self.log_blk.lc
+        self.out = o
 
 
 # --------------------------------------------------------------------------- oracle library

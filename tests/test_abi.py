@@ -190,3 +190,78 @@ def test_cli_usage():
     assert os.path.exists(exe)
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+# ---- --json / --simplification_substitution writers against the reference docs' exact texts
+_M1 = str(R.PRIMES["bn128"] - 1)
+DOCS_JSON_TEXT = {  # constraints-json.md:55-60 (--O1) and :93-97 (--O2), typed in as data
+    "O1": '{\n"constraints": [\n[{"2":"%s"},{"4":"1"},{"1":"%s"}],\n[{},{},{"0":"1","2":"2","3":"1","4":"%s"}]\n]\n}'
+          % (_M1, _M1, _M1),
+    "O2": '{\n"constraints": [\n[{"2":"%s"},{"0":"1","2":"2","3":"1"},{"1":"%s"}]\n]\n}' % (_M1, _M1),
+}
+DOCS_SUBS_TEXT = {  # simplification-json.md:48-51 (--O1) and :77-81 (--O2)
+    "O1": '{\n"5" : {"2":"1"},\n"4" : {"1":"1"}\n}',
+    "O2": '{\n"5" : {"2":"1"},\n"4" : {"1":"1"},\n"6" : {"0":"1","2":"2","3":"1"}\n}',
+}
+
+
+def _docs_result(level):
+    import make_golden as G
+    sys_ = G.docs_system()
+    return sys_, R.simplification(sys_, G.flags_of(level), want_log=True)
+
+
+@pytest.mark.parametrize("level", ["O1", "O2"])
+def test_json_writers_docs_text(level):
+    """rs_write_constraints_json / rs_write_substitution_json (product) on the oracle's result for the
+    docs circuit reproduce the reference docs' file texts byte for byte; so does the Python restatement
+    the GPU tests compare with."""
+    import sys
+    sys.path.insert(0, GOLD)
+    sys_, res = _docs_result(level)
+    log = rsio.pyref_log(res.log)
+    assert rsio.constraints_json_text(res.constraints, res.signal_map) == DOCS_JSON_TEXT[level]
+    assert rsio.substitutions_json_text(log) == DOCS_SUBS_TEXT[level]
+    h = rsio.OutputHolder(res, sys_.max_signal, log)
+    with tempfile.TemporaryDirectory() as tmp:
+        cj, sj = os.path.join(tmp, "c.json"), os.path.join(tmp, "s.json")
+        abi.check(abi.lib().rs_write_constraints_json(cj.encode(), C.byref(h.out)))
+        abi.check(abi.lib().rs_write_substitution_json(sj.encode(), C.byref(h.out)))
+        assert open(cj).read() == DOCS_JSON_TEXT[level]
+        assert open(sj).read() == DOCS_SUBS_TEXT[level]
+
+
+@pytest.mark.parametrize("seed,prime,level", [(61, "bls12381", "O2"), (62, "goldilocks", "O1"), (63, 257, "O2")])
+def test_json_writers_random(seed, prime, level):
+    """Decimal conversion (limb carries, zero values, multi-digit keys sorted as numbers) on random
+    systems: product writers == the Python restatement of json_writer.rs."""
+    p = prime if isinstance(prime, int) else R.PRIMES[prime]
+    sys_ = rsio.gen_system(seed, p, n_sig=400, n_rows=300, big_cluster=380 if seed % 2 else 0)
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_golden as G
+    res = R.simplification(sys_, G.flags_of(level), want_log=True)
+    log = rsio.pyref_log(res.log)
+    h = rsio.OutputHolder(res, sys_.max_signal, log)
+    with tempfile.TemporaryDirectory() as tmp:
+        cj, sj = os.path.join(tmp, "c.json"), os.path.join(tmp, "s.json")
+        abi.check(abi.lib().rs_write_constraints_json(cj.encode(), C.byref(h.out)))
+        abi.check(abi.lib().rs_write_substitution_json(sj.encode(), C.byref(h.out)))
+        assert open(cj).read() == rsio.constraints_json_text(res.constraints, res.signal_map)
+        assert open(sj).read() == rsio.substitutions_json_text(log)
+
+
+def test_json_decimal_edges():
+    """Values across limb boundaries (2^64 - 1, 2^64, 10^19 multiples, p - 1 of a 256-bit prime)."""
+    p = R.PRIMES["secq256r1"]
+    vals = [1, 9, 10, (1 << 64) - 1, 1 << 64, 10 ** 19, 10 ** 19 - 1, 10 ** 38, (1 << 192) + 7, p - 1]
+    log = [(i + 1, {0: v, 3 * i + 1000: 0}) for i, v in enumerate(vals)]
+    res = R.Result([], {0: 0}, 0)
+    h = rsio.OutputHolder(res, 1, log)
+    with tempfile.TemporaryDirectory() as tmp:
+        sj = os.path.join(tmp, "s.json")
+        abi.check(abi.lib().rs_write_substitution_json(sj.encode(), C.byref(h.out)))
+        assert open(sj).read() == rsio.substitutions_json_text(log)
+        cj = os.path.join(tmp, "c.json")
+        abi.check(abi.lib().rs_write_constraints_json(cj.encode(), C.byref(h.out)))
+        assert open(cj).read() == '{\n"constraints": [\n]\n}'
