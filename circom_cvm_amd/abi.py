@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "librs_simplify.so")
+# RS_LIB: an alternative build of the same library (e.g. the RS_KCLOCKS diagnostic variant)
+LIB_PATH = os.environ.get("RS_LIB") or os.path.join(PKG, "librs_simplify.so")
 
 U64_MAX = (1 << 64) - 1
 PRIME_IDS = {"bn128": 0, "bls12381": 1, "goldilocks": 2, "grumpkin": 3, "pallas": 4,

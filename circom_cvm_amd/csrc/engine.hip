@@ -828,7 +828,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.row_off = E->A.get<uint64_t>("el.row_off", n_slots);
     a.row_len = E->A.get<uint32_t>("el.row_len", n_slots);
 
-    a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", 16 * n_big) : nullptr;
+    a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", kProfWords * n_big) : nullptr;
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
     HC(hipMemsetAsync(a.bytes, 0, 24, E->st));
@@ -842,7 +842,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     at.big_touch_off += n_head;
     at.big_touch_n += n_head;
     at.big_alive += n_head;
-    if (at.prof) at.prof += 16 * n_head;
+    if (at.prof) at.prof += kProfWords * n_head;
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_head) {
@@ -984,30 +984,32 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       }
     }
     if (a.prof) {
-      std::vector<unsigned long long> pf(16 * n_big);
+      std::vector<unsigned long long> pf(kProfWords * n_big);
       HC(hipMemcpy(pf.data(), a.prof, 8 * pf.size(), hipMemcpyDeviceToHost));
       std::vector<uint64_t> ix(n_big);
       for (uint64_t i = 0; i < n_big; ++i) ix[i] = i;
       std::sort(ix.begin(), ix.end(), [&](uint64_t x, uint64_t y) {
-        return pf[16 * x + 4] + pf[16 * x + 5] + pf[16 * x + 6] + pf[16 * x + 7] > pf[16 * y + 4] + pf[16 * y + 5] + pf[16 * y + 6] + pf[16 * y + 7];
+        return pf[kProfWords * x + 4] + pf[kProfWords * x + 5] + pf[kProfWords * x + 6] + pf[kProfWords * x + 7] > pf[kProfWords * y + 4] + pf[kProfWords * y + 5] + pf[kProfWords * y + 6] + pf[kProfWords * y + 7];
       });
       double sum[4] = {0, 0, 0, 0};
       unsigned long long rows_all = 0, rows_main = 0, subs_all = 0, it_max = 0;
       for (uint64_t q = 0; q < n_big; ++q) {
-        for (int j = 0; j < 4; ++j) sum[j] += pf[16 * q + 4 + j] / 100.0;
-        rows_all += pf[16 * q]; subs_all += pf[16 * q + 1]; rows_main += pf[16 * q + 2];
-        it_max = std::max(it_max, pf[16 * q + 3]);
+        for (int j = 0; j < 4; ++j) sum[j] += pf[kProfWords * q + 4 + j] / 100.0;
+        rows_all += pf[kProfWords * q]; subs_all += pf[kProfWords * q + 1]; rows_main += pf[kProfWords * q + 2];
+        it_max = std::max(it_max, pf[kProfWords * q + 3]);
       }
       fprintf(stderr, "[rs-debug] big clusters: %llu rows %llu subs %llu sequential rows %llu max iters %llu; "
               "summed us: %.0f / %.0f / %.0f / %.0f\n", (unsigned long long)n_big, rows_all, subs_all, rows_main, it_max,
               sum[0], sum[1], sum[2], sum[3]);
       fprintf(stderr, "[rs-debug] big clusters: %llu (times in us: count+uniques / main / normalize / compose)\n", (unsigned long long)n_big);
       for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 8); ++q) {
-        unsigned long long *p = &pf[16 * ix[q]];
-        fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu iters=%llu  %.1f / %.1f / %.1f / %.1f  merges=%llu mwork=%llu "
-                "rowstart|rhs_sum=%llu newsub|rhs_max=%llu touched=%llu | pivot %.1f hold+stage %.1f merge %.1f us\n", p[0], p[1], p[2], p[3],
-                p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0, p[8], p[9], p[10], p[11], p[12],
-                p[13] / 100.0, p[14] / 100.0, p[15] / 100.0);
+        unsigned long long *p = &pf[kProfWords * ix[q]];
+        fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu  prep %.1f / main %.1f / normalize %.1f / compose %.1f us"
+                "  [kclocks: merges packed %llu (lanes %.1f) reg %llu lds %llu | row starts %.1f pivot %.1f holder %.1f "
+                "merge %.1f (packed: loads %.1f search+product %.1f hand-off %.1f combine %.1f) new-sub %.1f us]\n",
+                p[0], p[1], p[2], p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0,
+                p[8], p[8] ? (double)p[12] / p[8] : 0.0, p[9], p[10], p[3] / 100.0, p[13] / 100.0, p[14] / 100.0,
+                p[15] / 100.0, p[16] / 100.0, p[17] / 100.0, p[18] / 100.0, p[19] / 100.0, p[11] / 100.0);
       }
     }
     eo.n_sub.resize(eo.n_clusters);

@@ -13,6 +13,7 @@
 namespace rs {
 
 #define RS_NONE 0xffffffffu
+constexpr uint64_t kProfWords = 24;  // RS_PROF words per workgroup cluster
 
 struct DRows {
   uint64_t *off;
@@ -998,7 +999,7 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
       A.big_touch_n[ci] = n_touch;
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
-        unsigned long long *P = A.prof + 16 * ci;
+        unsigned long long *P = A.prof + kProfWords * ci;
         P[0] = n; P[4] = wall_clock64() - t_0;
       }
     }
@@ -1074,6 +1075,35 @@ __device__ inline uint32_t wave_excl_scan(uint32_t *a, uint32_t n) {
   __syncthreads();
   return total;
 }
+// Per-signal state of a work-list entry, loaded once when the entry enters the list: a row's
+// merges never change it (deletions happen only when the row ends in a new substitution).
+constexpr uint32_t kStForb = 0xffffffffu, kStTake = 0xfffffffeu;  // else: the holder slot (deleted)
+__device__ __forceinline__ uint32_t d_sig_state(const uint8_t *forb, const uint8_t *del, const int32_t *holder, uint32_t s) {
+  const uint8_t f = forb[s], d = del[s];
+  const int32_t h = holder[s];
+  return f ? kStForb : (d ? (uint32_t)h : kStTake);
+}
+// LDS hand-off between the lanes of one wave (in-order LDS: no workgroup barrier needed)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// lower_bound over a sorted LDS list of n <= 64 keys, branch-free (straight-line code the scheduler
+// can interleave with independent work); a[] must be readable up to index 63.  hit: a[pos] == key.
+__device__ __forceinline__ uint32_t lds_lb64(const uint32_t *a, uint32_t n, uint32_t key, bool &hit) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t step = 32; step >= 1; step >>= 1) {
+    const uint32_t q = pos + step;
+    const uint32_t v = a[q - 1];
+    pos = ((q <= n) & (v < key)) ? q : pos;  // non-short-circuit: the load stays unconditional
+  }
+  const uint32_t v = a[pos < 63 ? pos : 63];
+  const bool lt = (pos < n) & (v < key);  // only when all 64 keys are below key
+  hit = (pos < n) & (v == key);
+  return pos + (lt ? 1u : 0u);
+}
 __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t *a, uint32_t n, uint32_t key) {
   uint32_t lo = 0, hi = n;
   while (lo < hi) {
@@ -1088,6 +1118,7 @@ constexpr uint32_t kBigCap = 512;  // LDS work-list capacity of k_big_main
 __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
   __shared__ uint32_t wk[2][kBigCap];
+  __shared__ uint32_t ws[2][kBigCap];  // per work entry: its signal's state (kStForb / kStTake / holder slot)
   __shared__ Fe wv[2][kBigCap];
   __shared__ uint32_t rk[kBigCap];
   __shared__ Fe rv[kBigCap];
@@ -1105,10 +1136,15 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     unsigned long long merges = 0, mwork = 0, rows = 0, by = 0;  // by: algorithmic bytes (lane 0)
     unsigned long long tp_piv = 0, tp_hold = 0, tp_merge = 0, tp_x, tp_row = 0, tp_new = 0, tp_r0;  // debug clocks
     unsigned long long tp_q[4] = {0, 0, 0, 0};
+    unsigned long long n_packed = 0, n_reg = 0, n_lds = 0, w_packed = 0;  // RS_KCLOCKS path counts
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));
     const bool prof = A.prof != nullptr;
+#ifdef RS_KCLOCKS  // per-phase debug clocks inside the loop (each read splits the schedule)
     auto clk = [prof]() -> unsigned long long { return prof ? wall_clock64() : 0ull; };
-    t_1 = clk();
+#else
+    auto clk = []() -> unsigned long long { return 0ull; };
+#endif
+    t_1 = prof ? wall_clock64() : 0ull;
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     __syncthreads();
     const uint32_t n_loop = A.big_alive[ci];
@@ -1139,8 +1175,14 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         __syncthreads();
         continue;
       }
-      for (uint32_t i = tid; i < len; i += nt) { wk[0][i] = k[i]; wv[0][i] = v[i]; }
+      for (uint32_t i = tid; i < len; i += nt) {
+        const uint32_t kk = k[i];
+        wk[0][i] = kk;
+        wv[0][i] = v[i];
+        ws[0][i] = d_sig_state(A.forb, A.del, A.holder_idx, kk);
+      }
       uint32_t cur = 0;
+      bool st_ok = true;  // ws[cur] holds the states of wk[cur]
       __syncthreads();
       tp_row += clk() - tp_r0;
       while (len > 0) {
@@ -1152,19 +1194,15 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         int32_t hs = -1;
         if (len <= 64) {  // one entry per lane: ballots and a butterfly instead of LDS atomics
           const uint32_t key = tid < len ? wk[cur][tid] : 0u;
-          bool tk = false, dl = false;
-          int32_t oc = 0, hsl = -1;
-          if (tid < len && !A.forb[key]) {
-            tk = true;
-            dl = A.del[key] != 0;
-            if (dl) {  // fetched speculatively with the pivot search
-              hsl = A.holder_idx[key];
-            } else if (p4) {
-              oc = A.occ[key];
-              if (oc < 0) { atomicOr(A.err, 16); oc = 0; }
-            }
-          }
+          const uint32_t stv = tid >= len ? kStForb : (st_ok ? ws[cur][tid] : d_sig_state(A.forb, A.del, A.holder_idx, key));
+          const bool tk = stv != kStForb, dl = stv < kStTake;
+          const int32_t hsl = dl ? (int32_t)stv : -1;
           const uint64_t tm = __ballot(tk), dm = __ballot(tk && dl);
+          int32_t oc = 0;
+          if (p4 && tm && !dm && tk) {  // no deleted key: min occurrences (the row's last step)
+            oc = A.occ[key];
+            if (oc < 0) { atomicOr(A.err, 16); oc = 0; }
+          }
           if (tm) {
             if (!p4) {
               oi = 63 - __clzll(tm);
@@ -1271,6 +1309,9 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         { unsigned long long t = clk(); tp_hold += t - tp_x; tp_x = t; }
         const Fe coef = fneg(F, wv[cur][oi]);
         const uint32_t nx = cur ^ 1;
+#ifdef RS_KCLOCKS
+        if (len + rl <= 64) { ++n_packed; w_packed += len + rl; } else if (len <= 64 && rl <= 64) ++n_reg; else ++n_lds;
+#endif
         if (len + rl <= 64) {
           // ---- packed register merge: lanes [0, len) hold the work, lanes [len, len + rl) the
           // RHS, so the whole step costs one product latency; positions by ballots
@@ -1280,35 +1321,41 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           uint32_t key = 0;
           Fe val = fe_zero();
           if (isw) { key = wk[cur][l]; val = wv[cur][l]; }
-          if (isr) { key = A.pk[roff + j]; val = A.pv[roff + j]; }
+          uint32_t stv = !isw ? kStForb : (st_ok ? ws[cur][l] : d_sig_state(A.forb, A.del, A.holder_idx, key));
+          if (isr) {
+            key = A.pk[roff + j];
+            val = A.pv[roff + j];
+            rk[j] = key;
+            stv = d_sig_state(A.forb, A.del, A.holder_idx, key);  // in flight under the product
+          }
           const unsigned long long tq0 = clk();
-          if (isw || isr) val = fmul(F, isw ? c2 : coef, val);
+          wave_sync();  // the RHS keys are in LDS (one wave: no workgroup barrier needed)
+          // one search per lane in the other list (work lanes in the RHS, RHS lanes in the work) on
+          // the keys alone, and the product on the value: two independent chains in one basic block,
+          // so the LDS reads of the search hide under the product's latency
+          const uint32_t *ok = isw ? rk : wk[cur];
+          const uint32_t on = isw ? rl : (isr ? len : 0u);
+          bool hit;
+          const uint32_t lb = lds_lb64(ok, on, key, hit);
+          val = fmul(F, isw ? c2 : coef, val);
           const unsigned long long tq1 = clk();
-          if (isr) { rk[j] = key; rv[j] = val; }
-          __syncthreads();
+          if (isr) rv[j] = val;
+          wave_sync();
           const unsigned long long tq2 = clk();
           tp_q[0] += tq0 - tp_x;  // loads
-          tp_q[1] += tq1 - tq0;   // product
+          tp_q[1] += tq1 - tq0;   // search + product
           tp_q[2] += tq2 - tq1;   // barrier
-          // one search per lane in the other list (work lanes in the RHS, RHS lanes in the work)
           bool keep = false;
-          uint32_t lb = 0;
-          if (isw || isr) {
-            const uint32_t *ok = isw ? rk : wk[cur];
-            const uint32_t on = isw ? rl : len;
-            lb = lds_lower_bound(ok, on, key);
-            const bool hit = lb < on && ok[lb] == key;
-            if (isw) {  // -c2*v (+ coef*rv when the RHS has the key)
-              if (l != oi) {
-                val = hit ? fsub(F, rv[lb], val) : fneg(F, val);
-                keep = !fe_is_zero(val);
-              }
-            } else {  // RHS-only keys: coef*rv
-              keep = !hit && !fe_is_zero(val);
+          if (isw) {  // -c2*v (+ coef*rv when the RHS has the key)
+            if (l != oi) {
+              val = hit ? fsub(F, rv[lb], val) : fneg(F, val);
+              keep = !fe_is_zero(val);
             }
+          } else if (isr) {  // RHS-only keys: coef*rv
+            keep = !hit && !fe_is_zero(val);
           }
           const unsigned long long tq3 = clk();
-          tp_q[3] += tq3 - tq2;  // lookups
+          tp_q[3] += tq3 - tq2;  // combine (the scatter is in tp_merge - sum)
           const uint64_t km = __ballot(keep);
           const uint64_t wmk = len >= 64 ? km : (km & ((1ull << len) - 1ull)), rmk = km >> len;
           auto below = [](uint64_t m, uint32_t k) -> uint32_t {
@@ -1318,8 +1365,10 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
             const uint32_t q = isw ? below(wmk, l) + below(rmk, lb) : below(rmk, j) + below(wmk, lb);
             wk[nx][q] = key;
             wv[nx][q] = val;
+            ws[nx][q] = stv;
           }
-          __syncthreads();
+          wave_sync();  // LDS-only hand-off inside the wave
+          st_ok = true;
           const uint32_t nlen = (uint32_t)__popcll(km);
           cur = nx;
           by += 36ull * (len + rl + nlen);
@@ -1367,6 +1416,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
           __syncthreads();
           const uint32_t nlen = (uint32_t)(__popcll(wmk) + __popcll(rmk));
           cur = nx;
+          st_ok = false;
           by += 36ull * (len + rl + nlen);
           tp_merge += clk() - tp_x;
           len = nlen;
@@ -1416,6 +1466,7 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
         }
         __syncthreads();
         cur = nx;
+        st_ok = false;
         by += 36ull * (len + rl + tw + tr);
         tp_merge += clk() - tp_x;
         len = tw + tr;
@@ -1427,10 +1478,15 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
       atomicAdd(A.bytes_main, by);
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
-        unsigned long long *P = A.prof + 16 * ci;
-        P[2] = rows; P[5] = clk() - t_1; P[8] = merges; P[9] = mwork;
-        P[13] = tp_piv; P[14] = tp_hold; P[15] = tp_merge; P[10] = tp_row; P[11] = tp_new;
-        P[8] = tp_q[0]; P[9] = tp_q[1]; P[3] = tp_q[2]; P[12] = tp_q[3];
+        unsigned long long *P = A.prof + kProfWords * ci;
+        // [2] rows, [5] wall; RS_KCLOCKS builds: [3] row starts, [8..10] packed / register / LDS
+        // merges, [11] new substitutions, [12] lanes used by packed merges, [13..15] pivot / holder /
+        // merge time (100 MHz ticks)
+        P[2] = rows; P[5] = wall_clock64() - t_1;
+        P[3] = tp_row; P[8] = n_packed; P[9] = n_reg; P[10] = n_lds; P[11] = tp_new; P[12] = w_packed;
+        P[13] = tp_piv; P[14] = tp_hold; P[15] = tp_merge;
+        P[16] = tp_q[0]; P[17] = tp_q[1]; P[18] = tp_q[2]; P[19] = tp_q[3];  // packed merge: loads / search+product / hand-off / combine+scatter
+        (void)merges; (void)mwork;
       }
     }
     __syncthreads();
@@ -1552,11 +1608,6 @@ __device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t s
   return true;
 }
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 constexpr uint32_t kComposeCap = 256;  // entries one wave composes in LDS
 
@@ -1797,7 +1848,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
     if (tid == 0) {
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
-        unsigned long long *P = A.prof + 16 * ci;
+        unsigned long long *P = A.prof + kProfWords * ci;
         P[1] = m; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3;
       }
     }
@@ -1827,7 +1878,73 @@ __device__ __forceinline__ uint32_t d_frame_weight(const FrameArgs &A, uint32_t 
   return s >= 0 ? A.h_len[s] : 1;
 }
 
-// Expands one linear combination through the frames into [k, v) (capacity from d_frame_weight + 1)
+// Frame 3 (the linear substitutions) as an n-way merge of sorted lists, n <= K: list i is the
+// right-hand side of tail entry i scaled by its coefficient when its signal is substituted, else the
+// entry itself.  One list is consumed per step (the smallest head key; duplicates across lists
+// meet consecutively and are summed on emit), zero sums are dropped -- the result of expanding,
+// sorting, summing and dropping zeros (fast_encoded_constraint_substitution + fix), in O(w * K)
+// instead of an insertion sort over the expanded list.  Output from k[0]; the tail [rb, rb + n)
+// must lie beyond every output position (the caller reserves n extra slots).
+template <int K>
+__device__ inline uint32_t d_frame3_merge(const FrameArgs &A, uint32_t *k, Fe *v, uint32_t rb, uint32_t n) {
+  const FieldP &F = A.F;
+  uint32_t hk[K], hr[K];
+  uint64_t hb[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    hk[i] = RS_NONE;
+    hr[i] = 0;
+    hb[i] = RS_NONE;  // RS_NONE base: the entry itself (not substituted)
+    if ((uint32_t)i < n) {
+      const uint32_t kk = k[rb + i];
+      const int32_t s = A.sub_of[kk];
+      if (s >= 0) {
+        hb[i] = A.h_off[s];
+        hr[i] = A.h_len[s];
+        hk[i] = hr[i] ? A.pk[hb[i]] : RS_NONE;
+      } else {
+        hk[i] = kk;
+        hr[i] = 1;
+      }
+    }
+  }
+  uint32_t w = 0, lk = RS_NONE;
+  Fe lv = fe_zero();
+  for (;;) {
+    uint32_t mk = RS_NONE, mi = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      if (hk[i] < mk) { mk = hk[i]; mi = (uint32_t)i; }
+    if (mk == RS_NONE) break;
+    uint64_t b = 0;
+    uint32_t rem = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      if ((uint32_t)i == mi) { b = hb[i]; rem = hr[i]; }
+    const Fe sc = v[rb + mi];
+    Fe c = sc;
+    uint32_t nk = RS_NONE;
+    if (b != RS_NONE) {
+      c = fmul(F, sc, A.pv[b]);
+      if (rem > 1) nk = A.pk[b + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      if ((uint32_t)i == mi) { hk[i] = nk; hr[i] = rem - 1; hb[i] = b == RS_NONE ? b : b + 1; }
+    if (mk == lk) {
+      lv = fadd(F, lv, c);
+    } else {
+      if (lk != RS_NONE && !fe_is_zero(lv)) { k[w] = lk; v[w] = lv; ++w; }
+      lk = mk;
+      lv = c;
+    }
+  }
+  if (lk != RS_NONE && !fe_is_zero(lv)) { k[w] = lk; v[w] = lv; ++w; }
+  return w;
+}
+
+// Expands one linear combination through the frames into [k, v).  The region holds
+// 1 + sum(d_frame_weight) + n entries (n = input length): the input is staged in its last n slots.
 __device__ inline uint32_t d_apply_frames(const FrameArgs &A, const uint32_t *ik, const Fe *iv, uint32_t n,
                                           uint32_t *k, Fe *v, uint32_t cap) {
   const FieldP &F = A.F;
@@ -1849,7 +1966,9 @@ __device__ inline uint32_t d_apply_frames(const FrameArgs &A, const uint32_t *ik
       if (A.ce_has[tk[i]]) { tv[i] = fmul(F, tv[i], A.ce_val[tk[i]]); tk[i] = 0; any = true; }
     if (any) n = d_sort_combine(F, tk, tv, n);
   }
-  // frame 3 expands: write from the front, reading from the (shrunk) tail copy
+  if (n <= 8) return d_frame3_merge<8>(A, k, v, base, n);
+  // frame 3 expands (rows of more than 8 entries): write from the front, reading from the
+  // (shrunk) tail copy, then sort
   uint32_t rb = cap - n;
   if (rb != base)
     for (uint32_t i = n; i-- > 0;) { k[rb + i] = tk[i]; v[rb + i] = tv[i]; }  // overlapping: copy backwards
@@ -1885,7 +2004,8 @@ struct NLArgs {
 
 __global__ void k_nl_count(NLArgs A) {
   for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
-    uint64_t ca = 1, cb = 1, cc = 1;
+    // expansion bound + 1, plus the staged input (d_apply_frames)
+    uint64_t ca = 1 + A.a.len[r], cb = 1 + A.b.len[r], cc = 1 + A.c.len[r];
     for (uint32_t i = 0; i < A.a.len[r]; ++i) ca += d_frame_weight(A.fr, A.a.key[A.a.off[r] + i]);
     for (uint32_t i = 0; i < A.b.len[r]; ++i) cb += d_frame_weight(A.fr, A.b.key[A.b.off[r] + i]);
     for (uint32_t i = 0; i < A.c.len[r]; ++i) cc += d_frame_weight(A.fr, A.c.key[A.c.off[r] + i]);
@@ -1942,7 +2062,7 @@ struct RoundArgs {
 
 __global__ void k_round_count(RoundArgs A) {
   for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
-    uint64_t ca = 1, cb = 1, cc = 1;
+    uint64_t ca = 1 + A.a.len[r], cb = 1 + A.b.len[r], cc = 1 + A.c.len[r];  // + the staged input
     bool hit = false;
     for (uint32_t i = 0; i < A.a.len[r]; ++i) { int32_t s = A.sub_of[A.a.key[A.a.off[r] + i]]; ca += s >= 0 ? A.h_len[s] : 1; hit |= s >= 0; }
     for (uint32_t i = 0; i < A.b.len[r]; ++i) { int32_t s = A.sub_of[A.b.key[A.b.off[r] + i]]; cb += s >= 0 ? A.h_len[s] : 1; hit |= s >= 0; }
