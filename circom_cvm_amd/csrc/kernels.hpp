@@ -2098,65 +2098,74 @@ __global__ void k_round_fill(RoundArgs A) {
     uint32_t capa = (uint32_t)A.cap_a[r], capb = (uint32_t)A.cap_b[r], capc = (uint32_t)A.cap_c[r];
     uint32_t mx = capa > capb ? capa : capb;
     uint32_t cc = (capc - mx) / 2;
-    // ---- first substitution (in round order) after which A or B is constant/empty
-    {
-      // applicable ranks from A u B, ascending; per-row scratch = [2*oc, 2*oc + 2*capc)
-      uint32_t *rk_ = A.tmpk + 2 * (oc - A.c_base);
-      uint32_t nr = 0;
-      for (int part = 0; part < 2; ++part) {
-        const DRows &P = part ? A.b : A.a;
-        for (uint32_t i = 0; i < P.len[r]; ++i) {
-          int32_t q = A.rank_of[P.key[P.off[r] + i]];
-          if (q >= 0) rk_[nr++] = (uint32_t)q;
-        }
-      }
-      d_heap_sort_u32(rk_, nr);
-      // incremental application on copies of A and B held in the output regions
-      uint32_t na = A.a.len[r], nb = A.b.len[r];
-      uint32_t *ak = A.oa.key + oa, *bk = A.ob.key + ob;
-      Fe *av = A.oa.val + oa, *bv = A.ob.val + ob;
-      for (uint32_t i = 0; i < na; ++i) { ak[i] = A.a.key[A.a.off[r] + i]; av[i] = A.a.val[A.a.off[r] + i]; }
-      for (uint32_t i = 0; i < nb; ++i) { bk[i] = A.b.key[A.b.off[r] + i]; bv[i] = A.b.val[A.b.off[r] + i]; }
-      if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = -2;  // already linear
-      for (uint32_t q = 0; q < nr && A.turn[r] == -1; ++q) {
-        if (q > 0 && rk_[q] == rk_[q - 1]) continue;
-        for (int part = 0; part < 2; ++part) {
-          uint32_t *pk_ = part ? bk : ak;
-          Fe *pv_ = part ? bv : av;
-          uint32_t &pn = part ? nb : na;
-          uint32_t pcap = part ? capb : capa;
-          // find the signal with this rank in the part
-          uint32_t fi = RS_NONE;
-          for (uint32_t i = 0; i < pn; ++i)
-            if (A.rank_of[pk_[i]] == (int32_t)rk_[q]) { fi = i; break; }
-          if (fi == RS_NONE) continue;
-          int32_t s = A.sub_of[pk_[fi]];
-          Fe val = pv_[fi];
-          const uint32_t *hk = A.pk + A.h_off[s];
-          const Fe *hv = A.pv + A.h_off[s];
-          uint32_t hl = A.h_len[s];
-          // merge (pn - 1 + hl <= pcap) via scratch tmp region after rk_
-          uint32_t *mk = A.tmpk + 2 * (oc - A.c_base) + capc;
-          Fe *mv = A.tmpv + 2 * (oc - A.c_base) + capc;
-          uint32_t i = 0, j = 0, w = 0;
-          while (i < pn || j < hl) {
-            if (i == fi) { ++i; continue; }
-            if (j >= hl || (i < pn && pk_[i] < hk[j])) { mk[w] = pk_[i]; mv[w] = pv_[i]; ++i; }
-            else if (i >= pn || hk[j] < pk_[i]) { mk[w] = hk[j]; mv[w] = fmul(F, val, hv[j]); ++j; }
-            else { mk[w] = pk_[i]; mv[w] = fadd(F, pv_[i], fmul(F, val, hv[j])); ++i; ++j; }
-            ++w;
-          }
-          w = d_drop_zeros(mk, mv, w);
-          (void)pcap;
-          for (uint32_t t = 0; t < w; ++t) { pk_[t] = mk[t]; pv_[t] = mv[t]; }
-          pn = w;
-        }
-        if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = (int32_t)rk_[q];
-      }
-    }
-    // ---- final content: fix(all substitutions applied)
+    // A row that turns linear stays linear (fix_constraint clears A and B; later substitutions only
+    // touch C), so it turns iff its final A or B -- all of the round's substitutions applied -- is
+    // constant or empty.  The final A and B come first; only the rows that turn (few) replay the
+    // substitutions one by one to find the rank at which they turn.
     uint32_t na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
     uint32_t nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
+    if (d_const_or_empty(A.oa.key + oa, na) || d_const_or_empty(A.ob.key + ob, nb)) {
+      // ---- first substitution (in round order) after which A or B is constant/empty
+      {
+        // applicable ranks from A u B, ascending; per-row scratch = [2*oc, 2*oc + 2*capc)
+        uint32_t *rk_ = A.tmpk + 2 * (oc - A.c_base);
+        uint32_t nr = 0;
+        for (int part = 0; part < 2; ++part) {
+          const DRows &P = part ? A.b : A.a;
+          for (uint32_t i = 0; i < P.len[r]; ++i) {
+            int32_t q = A.rank_of[P.key[P.off[r] + i]];
+            if (q >= 0) rk_[nr++] = (uint32_t)q;
+          }
+        }
+        d_heap_sort_u32(rk_, nr);
+        // incremental application on copies of A and B held in the output regions
+        uint32_t na = A.a.len[r], nb = A.b.len[r];
+        uint32_t *ak = A.oa.key + oa, *bk = A.ob.key + ob;
+        Fe *av = A.oa.val + oa, *bv = A.ob.val + ob;
+        for (uint32_t i = 0; i < na; ++i) { ak[i] = A.a.key[A.a.off[r] + i]; av[i] = A.a.val[A.a.off[r] + i]; }
+        for (uint32_t i = 0; i < nb; ++i) { bk[i] = A.b.key[A.b.off[r] + i]; bv[i] = A.b.val[A.b.off[r] + i]; }
+        if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = -2;  // already linear
+        for (uint32_t q = 0; q < nr && A.turn[r] == -1; ++q) {
+          if (q > 0 && rk_[q] == rk_[q - 1]) continue;
+          for (int part = 0; part < 2; ++part) {
+            uint32_t *pk_ = part ? bk : ak;
+            Fe *pv_ = part ? bv : av;
+            uint32_t &pn = part ? nb : na;
+            uint32_t pcap = part ? capb : capa;
+            // find the signal with this rank in the part
+            uint32_t fi = RS_NONE;
+            for (uint32_t i = 0; i < pn; ++i)
+              if (A.rank_of[pk_[i]] == (int32_t)rk_[q]) { fi = i; break; }
+            if (fi == RS_NONE) continue;
+            int32_t s = A.sub_of[pk_[fi]];
+            Fe val = pv_[fi];
+            const uint32_t *hk = A.pk + A.h_off[s];
+            const Fe *hv = A.pv + A.h_off[s];
+            uint32_t hl = A.h_len[s];
+            // merge (pn - 1 + hl <= pcap) via scratch tmp region after rk_
+            uint32_t *mk = A.tmpk + 2 * (oc - A.c_base) + capc;
+            Fe *mv = A.tmpv + 2 * (oc - A.c_base) + capc;
+            uint32_t i = 0, j = 0, w = 0;
+            while (i < pn || j < hl) {
+              if (i == fi) { ++i; continue; }
+              if (j >= hl || (i < pn && pk_[i] < hk[j])) { mk[w] = pk_[i]; mv[w] = pv_[i]; ++i; }
+              else if (i >= pn || hk[j] < pk_[i]) { mk[w] = hk[j]; mv[w] = fmul(F, val, hv[j]); ++j; }
+              else { mk[w] = pk_[i]; mv[w] = fadd(F, pv_[i], fmul(F, val, hv[j])); ++i; ++j; }
+              ++w;
+            }
+            w = d_drop_zeros(mk, mv, w);
+            (void)pcap;
+            for (uint32_t t = 0; t < w; ++t) { pk_[t] = mk[t]; pv_[t] = mv[t]; }
+            pn = w;
+          }
+          if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = (int32_t)rk_[q];
+        }
+      }
+      // the replay used the A / B regions as scratch: final A and B again
+      na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
+      nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
+    }
+    // ---- final content: fix(all substitutions applied)
     uint32_t nc = d_apply_frames(fr, A.c.key + A.c.off[r], A.c.val + A.c.off[r], A.c.len[r], A.oc.key + oc, A.oc.val + oc, cc);
     d_fix(F, A.oa.key + oa, A.oa.val + oa, na, A.ob.key + ob, A.ob.val + ob, nb, A.oc.key + oc, A.oc.val + oc, nc,
           A.oc.key + oc + cc, A.oc.val + oc + cc);
