@@ -33,15 +33,8 @@ __global__ void k_cl_count(DRows V, uint64_t *npairs, unsigned long long *stat /
     nnz += len;
     act += len ? 1 : 0;
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {  // one atomic per wave
-    nnz += __shfl_xor(nnz, d);
-    act += __shfl_xor(act, d);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (nnz) atomicAdd(&stat[0], nnz);
-    if (act) atomicAdd(&stat[1], act);
-  }
+  wave_atomic_add(&stat[0], nnz);  // launched on a capped grid: few waves, few atomics
+  wave_atomic_add(&stat[1], act);
 }
 __global__ void k_cl_fill(DRows V, const uint64_t *poff, uint64_t *pkey, uint32_t *pslot) {
   for (uint64_t r = gtid(); r < V.n; r += gstride()) {
@@ -241,16 +234,19 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
 // cluster-size classes for the elimination kernels: sorted by (size desc, index)
 __global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, uint64_t *skey, uint32_t *sidx,
                              unsigned long long *cnt /* [0] >= 1e6, [1] workgroup kernels, [2] LDS replay, [3] > LDS, [4] large LDS replay */) {
+  unsigned long long k[5] = {0, 0, 0, 0, 0};
   for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
     uint64_t sz = cl_off[c + 1] - cl_off[c];
     skey[c] = ((uint64_t)(0xffffffffu - (uint32_t)sz) << 32) | c;
     sidx[c] = (uint32_t)c;
-    if (sz >= 1000000) atomicAdd(&cnt[0], 1ull);
-    if (sz >= kWaveMin) atomicAdd(&cnt[1], 1ull);
-    if (sz > kClSmall && sz <= kClLds) atomicAdd(&cnt[2], 1ull);
-    if (sz > kClLds) atomicAdd(&cnt[3], 1ull);
-    if (sz > kClMid && sz <= kClLds) atomicAdd(&cnt[4], 1ull);
+    k[0] += sz >= 1000000;
+    k[1] += sz >= kWaveMin;
+    k[2] += sz > kClSmall && sz <= kClLds;
+    k[3] += sz > kClLds;
+    k[4] += sz > kClMid && sz <= kClLds;
   }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) wave_atomic_add(&cnt[i], k[i]);
 }
 // small list = sorted[0, h) ++ sorted[h + nb, n_cl)
 __global__ void k_cl_small_ids(const uint32_t *sorted, uint64_t n_cl, uint64_t h, uint64_t nb, uint32_t *small) {

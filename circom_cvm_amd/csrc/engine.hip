@@ -103,6 +103,13 @@ struct Arena {
   }
 };
 
+// grid-stride kernels that end in per-wave atomics: a capped grid keeps the atomics few
+template <class K, class... Args>
+static void launch_capped(hipStream_t st, K kernel, uint64_t n, uint64_t max_blocks, Args... args) {
+  uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>((n + 255) / 256, 1), max_blocks);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, st, args...);
+  HC(hipGetLastError());
+}
 template <class K, class... Args>
 static void launch(hipStream_t st, K kernel, uint64_t n, Args... args) {
   uint64_t blocks = (n + 255) / 256;
@@ -610,7 +617,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   uint64_t *npairs = A.get<uint64_t>("cl.np", n);
   unsigned long long *stat = A.get<unsigned long long>("cl.stat", 8);
   HC(hipMemsetAsync(stat, 0, 64, st));
-  launch(st, k_cl_count, n, V, npairs, stat);
+  launch_capped(st, k_cl_count, n, 1024, V, npairs, stat);
   uint64_t *poff = A.get<uint64_t>("cl.poff", n);
   const uint64_t P = excl_scan_u64(E, npairs, poff, n, "cl1");
   unsigned long long hs[2];
@@ -660,7 +667,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   uint64_t *sk = A.get<uint64_t>("cl.sk", n_cl), *sk2 = A.get<uint64_t>("cl.sk2", n_cl);
   uint32_t *si = A.get<uint32_t>("cl.si", n_cl), *sorted = A.get<uint32_t>("el.big", n_cl);
   unsigned long long *cnt = stat + 2;
-  launch(st, k_cl_sizekey, n_cl, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt);
+  launch_capped(st, k_cl_sizekey, n_cl, 1024, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt);
   sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
   unsigned long long hc[5];
   uint64_t first = 0;

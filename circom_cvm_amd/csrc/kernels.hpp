@@ -25,6 +25,13 @@ struct DRows {
 
 __device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
+// One atomic per wave for a counter every lane contributes to (all lanes of the wave must call it):
+// per-lane atomics on one address serialise in the L2 (a million of them cost milliseconds).
+__device__ __forceinline__ void wave_atomic_add(unsigned long long *p, unsigned long long x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(p, x);
+}
 
 // ---------------------------------------------------------------- small sequential helpers
 // insertion sort by key + combine duplicate keys (sum); zeros are kept (HashMap semantics).
@@ -526,6 +533,7 @@ __device__ inline bool d_normalize_compose(const ElimArgs &A, Alloc &al, uint64_
 __global__ __launch_bounds__(64) void k_eliminate(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
   Alloc al;
+  unsigned long long by_all = 0;  // algorithmic bytes of this lane's clusters
   for (uint64_t ci = gtid(); ci < n_ids; ci += gstride()) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
@@ -728,8 +736,9 @@ __global__ __launch_bounds__(64) void k_eliminate(ElimArgs A, const uint32_t *id
     uint64_t rows_e = 0, subs_e = 0;
     for (uint64_t idx = b; idx < e; ++idx) rows_e += A.rows.len[A.perm[idx]];
     for (uint32_t i = 0; i < m; ++i) subs_e += A.h_len[b + i];
-    atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * n));
+    by_all += 36ull * (rows_e + 3 * subs_e) + 8ull * n;
   }
+  wave_atomic_add(A.bytes, by_all);
 }
 
 
@@ -1727,6 +1736,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   Alloc al;
   al.chunk = 128;
+  unsigned long long by_el = 0, by_fin = 0;  // this lane's algorithmic bytes (one atomic per wave at the end)
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
@@ -1836,8 +1846,8 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
     uint32_t hmax = 0;
     for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
     for (uint32_t i = tid; i < m; i += nt) { subs_e += A.h_len[b + i]; hmax = max(hmax, A.h_len[b + i]); }
-    atomicAdd(A.bytes, (unsigned long long)(36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0)));
-    if (by) atomicAdd(A.bytes_fin, by);
+    by_el += 36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0);
+    by_fin += by;
     if (A.prof) {
       if (tid == 0) { s_hsum = 0; s_hmax = 0; }
       __syncthreads();
@@ -1854,6 +1864,8 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
     }
     __syncthreads();
   }
+  wave_atomic_add(A.bytes, by_el);
+  wave_atomic_add(A.bytes_fin, by_fin);
 }
 
 // ---------------------------------------------------------------- substitution frames
