@@ -681,8 +681,11 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   launch(st, k_cl_replay_lane, n_cl, (const uint64_t *)D.cl_off, n_cl, (const uint64_t *)q_off,
          (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm, (const uint32_t *)n_ordered,
          old_heur);
-  if (hc[4]) {  // (kClMid, kClLds]: the largest LDS footprint
-    hipLaunchKernelGGL((k_cl_replay_lds<kClLds, kClChunk>), dim3((unsigned)std::min<uint64_t>(hc[4], 4096)), dim3(256), 0, st,
+  if (hc[4]) {  // (kClMid, kClLds]: the largest LDS footprint, on the second stream (the few
+                // largest clusters' serial replays overlap everything else's)
+    HC(hipEventRecord(E->evx[6], st));
+    HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
+    hipLaunchKernelGGL((k_cl_replay_lds<kClLds, kClChunk>), dim3((unsigned)std::min<uint64_t>(hc[4], 4096)), dim3(256), 0, E->st2,
                        (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[4],
                        (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
                        (const uint32_t *)n_ordered, old_heur);
@@ -695,6 +698,10 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
                        (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
                        (const uint32_t *)n_ordered, old_heur);
     HC(hipGetLastError());
+  }
+  if (hc[4]) {  // join: the elimination reads every cluster's order
+    HC(hipEventRecord(E->evx[7], E->st2));
+    HC(hipStreamWaitEvent(st, E->evx[7], 0));
   }
   // elimination split: clusters of kWaveMin rows or more (a prefix of the size order) go to the
   // workgroup kernels (process_3 or process_4 per cluster), the rest one lane each
@@ -870,7 +877,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_prep, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));
-        hipLaunchKernelGGL(k_big_main, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
         hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
@@ -887,7 +894,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev5, E->st));
-        hipLaunchKernelGGL(k_big_main, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
+        hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev6, E->st));
         {  // tail clusters flagged in cls, then one inversion per 64 slots across clusters

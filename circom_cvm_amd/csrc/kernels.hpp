@@ -1122,9 +1122,13 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t *a, uint32_t 
   return lo;
 }
 
-constexpr uint32_t kBigCap = 512;  // LDS work-list capacity of k_big_main
 
+// CAP: LDS work-list capacity (longer lists take the lane-serial spill path).  512 for the head's
+// largest clusters; 256 for the tail, whose many clusters are throughput-bound: 34 KB of LDS lets
+// four single-wave workgroups share a CU, as many as the kernel's VGPR budget allows.
+template <uint32_t CAP>
 __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  constexpr uint32_t kBigCap = CAP;
   const FieldP &F = A.F;
   __shared__ uint32_t wk[2][kBigCap];
   __shared__ uint32_t ws[2][kBigCap];  // per work entry: its signal's state (kStForb / kStTake / holder slot)
