@@ -857,6 +857,20 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     at.big_touch_n += n_head;
     at.big_alive += n_head;
     if (at.prof) at.prof += kProfWords * n_head;
+    at.split = 0;
+    ElimArgs ah = a;  // the head: split composition (k_big_finish -> k_compose_level per level -> k_big_emit)
+    uint64_t *cf_next = nullptr;
+    if (n_head) {
+      const uint64_t cap_items = n_head * std::max<uint64_t>(E->stats.max_cluster, 1);
+      ah.split = 1;
+      ah.cf_items = E->A.get<uint64_t>("cf.items0", cap_items);
+      cf_next = E->A.get<uint64_t>("cf.items1", cap_items);
+      ah.cf_n = E->A.get<unsigned long long>("cf.cnt", 2);
+      ah.cf_deg = E->A.get<uint64_t>("cf.deg", n_head);
+      ah.cf_dl = E->A.get<uint64_t>("cf.dl", n_head);
+      ah.cf_done = E->A.get<uint32_t>("cf.done", n_head);
+      HC(hipMemsetAsync(ah.cf_n, 0, 16, E->st));
+    }
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_head) {
@@ -882,9 +896,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipEventRecord(E->evx[3], E->st2));
         hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
-        hipLaunchKernelGGL(k_big_finish<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_big_finish<8>, dim3(g), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
-        HC(hipEventRecord(E->evx[4], E->st2));
+        // the Kahn levels and the emission follow once the rest is enqueued (the level loop waits)
       }
       if (n_tail) {
         // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
@@ -914,7 +928,33 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
       }
       HC(hipEventRecord(E->evx[5], E->st));
-      if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
+      if (n_head) {
+        // the head's composition, one Kahn level of all its clusters per launch over the whole GPU
+        // (each cluster's DAG is shallow but wide: ~20 levels for thousands of substitutions)
+        uint64_t *cur = ah.cf_items, *nxt = cf_next;
+        unsigned long long *nc = ah.cf_n, *nn = ah.cf_n + 1;
+        uint32_t levels = 0;
+        for (uint32_t level = 0; level <= n_slots + 1; ++level) {
+          HC(hipMemsetAsync(nn, 0, 8, E->st2));
+          hipLaunchKernelGGL(k_compose_level<8>, dim3(256), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big,
+                             (const uint64_t *)cur, (const unsigned long long *)nc, nxt, nn, level);
+          HC(hipGetLastError());
+          std::swap(cur, nxt);
+          std::swap(nc, nn);
+          levels = level + 1;
+          if (level % 4 == 3) {  // stop once a frontier is empty (checked every few levels)
+            unsigned long long h = 0;
+            HC(hipMemcpyAsync(&h, nc, 8, hipMemcpyDeviceToHost, E->st2));
+            HC(hipStreamSynchronize(E->st2));
+            if (!h) break;
+          }
+        }
+        hipLaunchKernelGGL(k_big_emit<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
+        HC(hipEventRecord(E->evx[4], E->st2));
+        if (g_prof_env) fprintf(stderr, "[rs-prof] head composition: %u level launches\n", levels);
+        HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
+      }
       HC(hipEventRecord(E->ev3, E->st));
     }
     int err = 0;
@@ -1020,10 +1060,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         unsigned long long *p = &pf[kProfWords * ix[q]];
         fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu  prep %.1f / main %.1f / normalize %.1f / compose %.1f us"
                 "  [kclocks: merges packed %llu (lanes %.1f) reg %llu lds %llu | row starts %.1f pivot %.1f holder %.1f "
-                "merge %.1f (packed: loads %.1f search+product %.1f hand-off %.1f combine %.1f) new-sub %.1f us]\n",
+                "merge %.1f (packed: loads %.1f search+product %.1f hand-off %.1f combine %.1f) new-sub %.1f us] levels %llu\n",
                 p[0], p[1], p[2], p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0,
                 p[8], p[8] ? (double)p[12] / p[8] : 0.0, p[9], p[10], p[3] / 100.0, p[13] / 100.0, p[14] / 100.0,
-                p[15] / 100.0, p[16] / 100.0, p[17] / 100.0, p[18] / 100.0, p[19] / 100.0, p[11] / 100.0);
+                p[15] / 100.0, p[16] / 100.0, p[17] / 100.0, p[18] / 100.0, p[19] / 100.0, p[11] / 100.0, p[20]);
       }
     }
     eo.n_sub.resize(eo.n_clusters);

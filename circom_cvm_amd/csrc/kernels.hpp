@@ -319,6 +319,14 @@ struct ElimArgs {
   uint64_t *row_off;          // per slot: (offset, length) of those rows in loop order (k_big_prep)
   uint32_t *row_len;
   int wide;                   // the k_wide_* kernels prepared this launch's largest p4 clusters
+  // split composition (the head's clusters): k_big_finish only normalises and builds each cluster's
+  // dependency DAG, k_compose_level composes one Kahn level of every cluster at a time over the
+  // whole GPU, k_big_emit finishes
+  int split;
+  uint64_t *cf_items;         // the first frontier (cluster position << 32 | local slot)
+  unsigned long long *cf_n;   // its length
+  uint64_t *cf_deg, *cf_dl;   // per cluster: pool offsets of deg[m] (+ dcnt[m+1]) and of the dependents
+  uint32_t *cf_done;          // per cluster: substitutions that reached a frontier
 
 };
 
@@ -1539,7 +1547,9 @@ __global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *i
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c];
     const uint32_t m = A.n_sub[c];
-    const uint32_t C = max(64u, (m + blockDim.x - 1) / blockDim.x);  // one chunk per lane on big clusters
+    // chunks of 16 (or one per lane on the largest clusters): the products of a chunk are a
+    // dependent chain, so short chains keep the head's critical path short
+    const uint32_t C = max(16u, (m + blockDim.x - 1) / blockDim.x);
     for (uint32_t c0 = tid * C; c0 < m; c0 += C * blockDim.x) {
       const uint32_t c1 = min(m, c0 + C);
       Fe acc = A.h_coef[b + c0];
@@ -1764,9 +1774,16 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
     if (tid == 0) {
       s_scr = pool_alloc_global(A, 6ull * m + 8);
       if (s_scr == RS_NONE) s_ok = 0;
+      if (A.split) A.cf_done[ci] = 0;
     }
     __syncthreads();
     uint32_t levels = 0;
+    if (A.split && !(s_ok && m)) {  // nothing to compose: k_big_emit still finishes the cluster
+      if (tid == 0 && !s_ok) atomicOr(A.err, 8);
+      by_fin += by;
+      __syncthreads();
+      continue;
+    }
     if (s_ok && m) {
       uint32_t *deg = A.pk + s_scr, *dcnt = deg + m, *dfill = dcnt + m + 1, *fr0 = dfill + m, *fr1 = fr0 + m;
       for (uint32_t i = tid; i < m; i += nt) { deg[i] = 0; dcnt[i] = 0; dfill[i] = 0; }
@@ -1801,6 +1818,20 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
           }
         }
         __syncthreads();
+        if (A.split) {  // hand the DAG and the first frontier to k_compose_level
+          const uint32_t nf0 = s_nf;
+          if (tid == 0) {
+            A.cf_deg[ci] = (uint64_t)(deg - A.pk);
+            A.cf_dl[ci] = s_scr;
+            A.cf_done[ci] = nf0;
+            s_scr = atomicAdd(A.cf_n, (unsigned long long)nf0);
+          }
+          __syncthreads();
+          for (uint32_t f = tid; f < nf0; f += nt) A.cf_items[s_scr + f] = ((uint64_t)ci << 32) | fr0[f];
+          by_fin += by;
+          __syncthreads();
+          continue;  // block-uniform: k_big_emit finishes the cluster
+        }
         uint32_t nf = s_nf, done = nf;
         uint32_t *cur = fr0, *nxt = fr1;
         while (nf && s_ok) {
@@ -1863,13 +1894,86 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
         unsigned long long *P = A.prof + kProfWords * ci;
-        P[1] = m; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3;
+        P[1] = m; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3; P[20] = levels;
       }
     }
     __syncthreads();
   }
   wave_atomic_add(A.bytes, by_el);
   wave_atomic_add(A.bytes_fin, by_fin);
+}
+
+// One Kahn level of the split composition, over every head cluster at once and the whole GPU: each
+// wave takes a frontier substitution, composes it (its dependencies were final one launch ago;
+// level 0 holds the substitutions without deleted keys, which need no composition), then releases
+// its dependents -- the ones whose last dependency this was form the next frontier.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_compose_level(ElimArgs A, const uint32_t *ids, const uint64_t *cur,
+                                                          const unsigned long long *n_cur, uint64_t *nxt,
+                                                          unsigned long long *n_nxt, uint32_t level) {
+  __shared__ uint64_t cw_S[NW][kComposeCap];
+  __shared__ Fe cw_V[NW][kComposeCap];
+  __shared__ uint32_t cw_dex[NW][64];
+  __shared__ uint64_t cw_dof[NW][64];
+  __shared__ Fe cw_dmu[NW][64];
+  const uint32_t wv_ = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Alloc al;
+  al.chunk = 128;
+  unsigned long long by = 0;
+  const uint64_t n = *n_cur, total = (uint64_t)gridDim.x * NW;
+  for (uint64_t f = (uint64_t)blockIdx.x * NW + wv_; f < n; f += total) {
+    const uint64_t item = cur[f];
+    const uint32_t ci = (uint32_t)(item >> 32), q = (uint32_t)item;
+    const uint32_t c = ids[ci];
+    const uint64_t b = A.cl_off[c];
+    const uint32_t m = A.n_sub[c];
+    if (level > 0) {
+      const int rc = d_compose_wave(A, al, b + q, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
+      if (rc == 2 && lane == 0) atomicOr(A.err, 8);
+      if (rc == 1 && lane == 0 && !d_compose_serial(A, al, b + q, by)) atomicOr(A.err, 8);
+      wave_sync();
+    }
+    uint32_t *deg = A.pk + A.cf_deg[ci], *dcnt = deg + m;
+    const uint32_t *dl = A.pk + A.cf_dl[ci];
+    for (uint32_t t = dcnt[q] + lane; t < dcnt[q + 1]; t += 64) {
+      const uint32_t d = dl[t];
+      if (atomicSub(&deg[d], 1u) == 1u) {
+        nxt[atomicAdd(n_nxt, 1ull)] = ((uint64_t)ci << 32) | d;
+        atomicAdd(&A.cf_done[ci], 1u);
+      }
+    }
+  }
+  wave_atomic_add(A.bytes_fin, by);
+}
+
+// The end of k_big_finish for split clusters: every substitution composed?  Emit, reset the dense
+// scratch, count the algorithmic bytes.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_big_emit(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  unsigned long long by_el = 0;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b);
+    const uint32_t m = A.n_sub[c];
+    if (tid == 0 && m && A.cf_done[ci] != m) atomicOr(A.err, 32);
+    for (uint32_t i = tid; i < m; i += nt) {
+      uint32_t s = A.h_sig[b + i];
+      A.holder_idx[s] = -1;
+      A.del[s] = 0;
+      A.sub_of[s] = (int32_t)(b + i);
+      A.deleted[s] = 1;
+    }
+    const uint32_t *touch = A.pk + A.big_touch_off[ci];
+    for (uint32_t t = tid; t < A.big_touch_n[ci]; t += nt) A.occ[touch[t]] = -1;
+    uint64_t rows_e = 0, subs_e = 0;
+    for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
+    for (uint32_t i = tid; i < m; i += nt) subs_e += A.h_len[b + i];
+    by_el += 36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0);
+    if (tid == 0 && A.prof) A.prof[kProfWords * ci + 1] = m;
+  }
+  wave_atomic_add(A.bytes, by_el);
 }
 
 // ---------------------------------------------------------------- substitution frames
