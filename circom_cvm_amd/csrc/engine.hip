@@ -869,6 +869,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       ah.cf_deg = E->A.get<uint64_t>("cf.deg", n_head);
       ah.cf_dl = E->A.get<uint64_t>("cf.dl", n_head);
       ah.cf_done = E->A.get<uint32_t>("cf.done", n_head);
+      ah.cf_big = E->A.get<uint64_t>("cf.big", cap_items);
+      ah.cf_nbig = E->A.get<unsigned long long>("cf.nbig", 1);
       HC(hipMemsetAsync(ah.cf_n, 0, 16, E->st));
     }
     if (eo.n_clusters) {
@@ -936,8 +938,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         uint32_t levels = 0;
         for (uint32_t level = 0; level <= n_slots + 1; ++level) {
           HC(hipMemsetAsync(nn, 0, 8, E->st2));
+          HC(hipMemsetAsync(ah.cf_nbig, 0, 8, E->st2));
           hipLaunchKernelGGL(k_compose_level<8>, dim3(256), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big,
                              (const uint64_t *)cur, (const unsigned long long *)nc, nxt, nn, level);
+          hipLaunchKernelGGL(k_compose_big, dim3(256), dim3(64), 0, E->st2, ah, (const uint32_t *)d_big, nxt, nn);
           HC(hipGetLastError());
           std::swap(cur, nxt);
           std::swap(nc, nn);

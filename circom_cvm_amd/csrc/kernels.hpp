@@ -327,6 +327,8 @@ struct ElimArgs {
   unsigned long long *cf_n;   // its length
   uint64_t *cf_deg, *cf_dl;   // per cluster: pool offsets of deg[m] (+ dcnt[m+1]) and of the dependents
   uint32_t *cf_done;          // per cluster: substitutions that reached a frontier
+  uint64_t *cf_big;           // a level's compositions too long for k_compose_level's waves
+  unsigned long long *cf_nbig;
 
 };
 
@@ -1736,6 +1738,110 @@ __device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, 
   return 0;
 }
 
+// d_compose_wave for right-hand sides of up to LCAP entries composing to up to ECAP entries: the
+// RHS is read 64 entries at a time (running counts for the own entries and the dependencies), the
+// rest is the same gather / bitonic sort / sum.  A single wave with a large LDS budget: the long
+// compositions of the largest clusters, which d_compose_wave sends back.
+template <uint32_t ECAP, uint32_t LCAP>
+__device__ inline int d_compose_wave_big(const ElimArgs &A, Alloc &al, uint64_t sl, uint64_t *S, Fe *V,
+                                         uint32_t *dex, uint64_t *dof, Fe *dmu, unsigned long long &by) {
+  const FieldP &F = A.F;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t off = A.h_off[sl];
+  const uint32_t len = A.h_len[sl];
+  if (len > LCAP) return 1;
+  const uint64_t lt = lane ? ((1ull << lane) - 1ull) : 0ull;
+  uint32_t n_own = 0, D = 0, tot = 0;  // wave-uniform running counts
+  for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    uint32_t key = 0, dl = 0;
+    Fe val = fe_zero();
+    int32_t hs = -1;
+    uint64_t doff = 0;
+    if (i < len) {
+      key = A.pk[off + i];
+      val = A.pv[off + i];
+      hs = A.holder_idx[key];
+      if (hs >= 0) { dl = A.h_len[hs]; doff = A.h_off[hs]; }
+    }
+    const uint64_t dm = __ballot(hs >= 0), om = __ballot(i < len && hs < 0);
+    uint32_t x = dl;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t y = __shfl_up(x, d);
+      if ((int)lane >= d) x += y;
+    }
+    const uint32_t ctot = __shfl(x, 63);
+    if (n_own + (uint32_t)__popcll(om) + tot + ctot > ECAP) return 1;
+    if (hs >= 0) {
+      const uint32_t r = D + (uint32_t)__popcll(dm & lt);
+      dex[r] = tot + x - dl;
+      dof[r] = doff;
+      dmu[r] = val;
+    }
+    if (i < len && hs < 0) {
+      const uint32_t q = n_own + (uint32_t)__popcll(om & lt);
+      S[q] = ((uint64_t)key << 32) | q;
+      V[q] = val;
+    }
+    n_own += (uint32_t)__popcll(om);
+    D += (uint32_t)__popcll(dm);
+    tot += ctot;
+  }
+  const uint32_t E = n_own + tot;
+  wave_sync();
+  for (uint32_t e = lane; e < tot; e += 64) {  // c_t * R(t), one product per entry
+    uint32_t lo = 0, hi = D;
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (dex[mid] <= e) lo = mid; else hi = mid;
+    }
+    const uint64_t src = dof[lo] + (e - dex[lo]);
+    const uint32_t q = n_own + e;
+    S[q] = ((uint64_t)A.pk[src] << 32) | q;
+    V[q] = fmul(F, dmu[lo], A.pv[src]);
+  }
+  uint32_t np2 = 1;
+  while (np2 < E) np2 <<= 1;
+  for (uint32_t q = E + lane; q < np2; q += 64) S[q] = ~0ull;
+  wave_sync();
+  for (uint32_t k = 2; k <= np2; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = lane; t < np2 / 2; t += 64) {
+        const uint32_t i = (t / j) * 2 * j + (t % j), pr = i + j;
+        const uint64_t a = S[i], c = S[pr];
+        if ((a > c) == ((i & k) == 0)) { S[i] = c; S[pr] = a; }
+      }
+      wave_sync();
+    }
+  }
+  uint64_t o = 0;
+  if (lane == 0) o = pool_alloc(A, al, E ? E : 1);
+  o = __shfl(o, 0);
+  if (o == RS_NONE) return 2;
+  uint32_t run = 0;
+  for (uint32_t cb = 0; cb < E; cb += 64) {
+    const uint32_t p = cb + lane;
+    const uint32_t k0 = p < E ? (uint32_t)(S[p] >> 32) : 0u;
+    const bool head = p < E && (p == 0 || (uint32_t)(S[p - 1] >> 32) != k0);
+    const uint64_t hm = __ballot(head);
+    if (head) {
+      Fe v = V[(uint32_t)S[p]];
+      for (uint32_t q = p + 1; q < E && (uint32_t)(S[q] >> 32) == k0; ++q) v = fadd(F, v, V[(uint32_t)S[q]]);
+      const uint64_t w = o + run + (uint32_t)__popcll(hm & lt);
+      A.pk[w] = k0;
+      A.pv[w] = v;
+    }
+    run += (uint32_t)__popcll(hm);
+  }
+  if (lane == 0) {
+    A.h_off[sl] = o;
+    A.h_len[sl] = run;
+    by += 36ull * (len + tot + run);
+  }
+  return 0;
+}
+
 template <int NW>  // waves per workgroup
 __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
@@ -1930,9 +2036,51 @@ __global__ __launch_bounds__(64 * NW) void k_compose_level(ElimArgs A, const uin
     if (level > 0) {
       const int rc = d_compose_wave(A, al, b + q, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
       if (rc == 2 && lane == 0) atomicOr(A.err, 8);
-      if (rc == 1 && lane == 0 && !d_compose_serial(A, al, b + q, by)) atomicOr(A.err, 8);
+      if (rc == 1) {  // too long for this wave's LDS: k_compose_big composes it and releases its dependents
+        if (lane == 0) A.cf_big[atomicAdd(A.cf_nbig, 1ull)] = item;
+        continue;
+      }
       wave_sync();
     }
+    uint32_t *deg = A.pk + A.cf_deg[ci], *dcnt = deg + m;
+    const uint32_t *dl = A.pk + A.cf_dl[ci];
+    for (uint32_t t = dcnt[q] + lane; t < dcnt[q + 1]; t += 64) {
+      const uint32_t d = dl[t];
+      if (atomicSub(&deg[d], 1u) == 1u) {
+        nxt[atomicAdd(n_nxt, 1ull)] = ((uint64_t)ci << 32) | d;
+        atomicAdd(&A.cf_done[ci], 1u);
+      }
+    }
+  }
+  wave_atomic_add(A.bytes_fin, by);
+}
+
+// The level's long compositions (deferred by k_compose_level): one wave per workgroup with room for
+// 2,048 composed entries; longer ones are composed lane-serially.  Then their dependents are
+// released like k_compose_level's.
+__global__ __launch_bounds__(64) void k_compose_big(ElimArgs A, const uint32_t *ids, uint64_t *nxt,
+                                                   unsigned long long *n_nxt) {
+  constexpr uint32_t ECAP = 2048, LCAP = 512;
+  __shared__ uint64_t S[ECAP];
+  __shared__ Fe V[ECAP];
+  __shared__ uint32_t dex[LCAP];
+  __shared__ uint64_t dof[LCAP];
+  __shared__ Fe dmu[LCAP];
+  const uint32_t lane = threadIdx.x & 63;
+  Alloc al;
+  al.chunk = 256;
+  unsigned long long by = 0;
+  const uint64_t n = *A.cf_nbig;
+  for (uint64_t f = blockIdx.x; f < n; f += gridDim.x) {
+    const uint64_t item = A.cf_big[f];
+    const uint32_t ci = (uint32_t)(item >> 32), q = (uint32_t)item;
+    const uint32_t c = ids[ci];
+    const uint64_t b = A.cl_off[c];
+    const uint32_t m = A.n_sub[c];
+    const int rc = d_compose_wave_big<ECAP, LCAP>(A, al, b + q, S, V, dex, dof, dmu, by);
+    if (rc == 2 && lane == 0) atomicOr(A.err, 8);
+    if (rc == 1 && lane == 0 && !d_compose_serial(A, al, b + q, by)) atomicOr(A.err, 8);
+    wave_sync();
     uint32_t *deg = A.pk + A.cf_deg[ci], *dcnt = deg + m;
     const uint32_t *dl = A.pk + A.cf_dl[ci];
     for (uint32_t t = dcnt[q] + lane; t < dcnt[q + 1]; t += 64) {
