@@ -896,7 +896,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
-        hipLaunchKernelGGL(k_batch_inv, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
+        hipLaunchKernelGGL(k_normalize, dim3(16, g), dim3(256), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         hipLaunchKernelGGL(k_big_finish<8>, dim3(g), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());

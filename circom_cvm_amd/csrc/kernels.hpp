@@ -1542,21 +1542,22 @@ __device__ inline uint32_t blk_excl_scan(uint32_t *a, uint32_t n, uint32_t *s_pa
 // before normalisation: one block per cluster, each lane inverts chunks of 64 slots with one
 // inversion per chunk (Montgomery's trick), so no cluster waits on an inversion chain of its own.
 // ftmp[slot] <- h_coef[slot]^-1.
+// Batch inversion of the pivot coefficients (multi_inv, modular_arithmetic.rs:71-91; exact inverses,
+// so the chunking is free): chains of 16 products per lane, blockIdx.y = cluster, blockIdx.x
+// spreads a large cluster's chains over many workgroups (the head's clusters, thousands of
+// substitutions each: short chains are the short critical path).
 __global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   const FieldP &F = A.F;
-  const uint32_t tid = threadIdx.x;
-  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+  constexpr uint32_t C = 16;
+  for (uint64_t ci = blockIdx.y; ci < n_ids; ci += gridDim.y) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c];
     const uint32_t m = A.n_sub[c];
-    // chunks of 16 (or one per lane on the largest clusters): the products of a chunk are a
-    // dependent chain, so short chains keep the head's critical path short
-    const uint32_t C = max(16u, (m + blockDim.x - 1) / blockDim.x);
-    for (uint32_t c0 = tid * C; c0 < m; c0 += C * blockDim.x) {
-      const uint32_t c1 = min(m, c0 + C);
+    for (uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * C; c0 < m; c0 += (uint64_t)gridDim.x * blockDim.x * C) {
+      const uint32_t c1 = (uint32_t)min<uint64_t>(m, c0 + C);
       Fe acc = A.h_coef[b + c0];
       A.ftmp[b + c0] = acc;
-      for (uint32_t i = c0 + 1; i < c1; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
+      for (uint32_t i = (uint32_t)c0 + 1; i < c1; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
       Fe inv = finv(F, acc);
       for (uint32_t i = c1 - 1; i > c0; --i) {
         const Fe inv_i = fmul(F, A.ftmp[b + i - 1], inv);
@@ -1566,6 +1567,25 @@ __global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *i
       A.ftmp[b + c0] = inv;
     }
   }
+}
+// normalize_substitutions (:414-437) of the split clusters: every RHS times its pivot's inverse,
+// one lane per substitution over a 2-D grid like k_batch_inv's
+__global__ __launch_bounds__(256) void k_normalize(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const FieldP &F = A.F;
+  unsigned long long by = 0;
+  for (uint64_t ci = blockIdx.y; ci < n_ids; ci += gridDim.y) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c];
+    const uint32_t m = A.n_sub[c];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+      const Fe inv_i = A.ftmp[b + i];
+      Fe *vv = A.pv + A.h_off[b + i];
+      const uint32_t l = A.h_len[b + i];
+      for (uint32_t t = 0; t < l; ++t) vv[t] = fmul(F, vv[t], inv_i);
+      by += 64ull * (l + 1);
+    }
+  }
+  wave_atomic_add(A.bytes_fin, by);
 }
 
 // The same over the slot space of many clusters at once (the tail stream's clusters, cls == 1):
@@ -1865,8 +1885,9 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
     unsigned long long t_2 = wall_clock64();
     unsigned long long by = 0;  // algorithmic bytes of this lane
     if (tid == 0) s_ok = 1;
-    // ---- normalize_substitutions (:414-437): the inverses come from k_batch_inv
-    for (uint32_t i = tid; i < m; i += nt) {
+    // ---- normalize_substitutions (:414-437): the inverses come from k_batch_inv (split clusters:
+    // k_normalize did it over the whole GPU)
+    for (uint32_t i = tid; i < (A.split ? 0u : m); i += nt) {
       const Fe inv_i = A.ftmp[b + i];
       Fe *vv = A.pv + A.h_off[b + i];
       for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
