@@ -234,19 +234,45 @@ __global__ void k_const_pick(DRows R, const uint8_t *forb, int32_t *ce_last, uin
   }
 }
 // clear_signal (algebra.rs:1108-1124): s := c / (-k)   (an empty map when c == 0 -> value 0)
+// One inversion per 8 rows (Montgomery's trick over the rows that define their signal's value;
+// exact inverses, so the batching is invisible): the inversion is the costly part of a row.
 __global__ void k_const_value(FieldP F, DRows R, const uint8_t *forb, const int32_t *ce_last, Fe *ce_val,
                               uint8_t *ce_has) {
-  for (uint64_t r = gtid(); r < R.n; r += gstride()) {
-    const uint32_t *k = R.key + R.off[r];
-    const Fe *v = R.val + R.off[r];
-    uint32_t n = R.len[r];
-    if (n == 0) continue;
-    uint32_t s = k[n - 1];
-    if (forb[s] || ce_last[s] != (int32_t)r) continue;
-    Fe c = (n == 2 && k[0] == 0) ? v[0] : fe_zero();
-    Fe inv = finv(F, fneg(F, v[n - 1]));
-    ce_val[s] = fmul(F, c, inv);
-    ce_has[s] = 1;
+  constexpr uint32_t C = 8;
+  for (uint64_t r0 = gtid() * C; r0 < R.n; r0 += gstride() * C) {
+    const uint32_t m = (uint32_t)min<uint64_t>(C, R.n - r0);
+    Fe pre[C];  // prefix products of the pivots -k (1 for rows that define nothing)
+    Fe acc = F.one;
+#pragma unroll
+    for (uint32_t i = 0; i < C; ++i) {
+      if (i < m) {
+        const uint64_t r = r0 + i;
+        const uint32_t n = R.len[r];
+        if (n) {
+          const uint32_t *k = R.key + R.off[r];
+          const uint32_t s = k[n - 1];
+          if (!forb[s] && ce_last[s] == (int32_t)r) acc = fmul(F, acc, fneg(F, R.val[R.off[r] + n - 1]));
+        }
+      }
+      pre[i] = acc;
+    }
+    Fe inv = finv(F, acc);
+#pragma unroll
+    for (int i = C - 1; i >= 0; --i) {
+      if ((uint32_t)i >= m) continue;
+      const uint64_t r = r0 + i;
+      const uint32_t n = R.len[r];
+      if (!n) continue;
+      const uint32_t *k = R.key + R.off[r];
+      const Fe *v = R.val + R.off[r];
+      const uint32_t s = k[n - 1];
+      if (forb[s] || ce_last[s] != (int32_t)r) continue;
+      const Fe inv_i = i ? fmul(F, pre[i - 1], inv) : inv;  // 1 / (-k) of this row
+      inv = fmul(F, inv, fneg(F, v[n - 1]));
+      const Fe c = (n == 2 && k[0] == 0) ? v[0] : fe_zero();
+      ce_val[s] = fmul(F, c, inv_i);
+      ce_has[s] = 1;
+    }
   }
 }
 // eq frame then constant frame on the linear rows (each frame + fix, :493-527); capacity len+1.
