@@ -1790,7 +1790,17 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         ra.tmpk = A.get<uint32_t>("r.tmpk", 2 * (q3.c + 1));
         ra.tmpv = A.get<Fe>("r.tmpv", 2 * (q3.c + 1));
         MK.mark("count");
-        launch(st, k_round_fill, n_st, ra);
+        {  // compact the touched rows: the fill's lanes all have work
+          uint64_t *tfl = A.get<uint64_t>("r.tfl", n_st), *tfp = A.get<uint64_t>("r.tfp", n_st);
+          uint32_t *tids = A.get<uint32_t>("r.touch_ids", n_st);
+          launch(st, k_touch_flags, n_st, (const uint64_t *)cc, n_st, tfl);
+          ra.n_ids = excl_scan_u64(E, tfl, tfp, n_st, "tfl");
+          if (ra.n_ids) launch(st, k_scatter_ids, n_st, (const uint64_t *)tfl, (const uint64_t *)tfp, n_st, tids);
+          ra.ids = tids;
+          HC(hipMemsetAsync(ra.turn, 0xff, 4 * n_st, st));
+          HC(hipMemsetAsync(ra.touched, 0, n_st, st));
+        }
+        if (ra.n_ids) launch(st, k_round_fill, ra.n_ids, ra);
         MK.mark("fill");
         if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qt);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);

@@ -2193,59 +2193,68 @@ __device__ __forceinline__ uint32_t d_frame_weight(const FrameArgs &A, uint32_t 
   return s >= 0 ? A.h_len[s] : 1;
 }
 
-// Frame 3 (the linear substitutions) as an n-way merge of sorted lists, n <= K: list i is the
-// right-hand side of tail entry i scaled by its coefficient when its signal is substituted, else the
-// entry itself.  One list is consumed per step (the smallest head key; duplicates across lists
-// meet consecutively and are summed on emit), zero sums are dropped -- the result of expanding,
-// sorting, summing and dropping zeros (fast_encoded_constraint_substitution + fix), in O(w * K)
-// instead of an insertion sort over the expanded list.  Output from k[0]; the tail [rb, rb + n)
-// must lie beyond every output position (the caller reserves n extra slots).
+// Frame 3 (the linear substitutions) as a merge of sorted lists: list 0 is the tail entries whose
+// signal is not substituted (in place, skipping the others), lists 1..K the right-hand sides of the
+// substituted ones scaled by their coefficients.  One list is consumed per step (the smallest head
+// key; duplicates across lists meet consecutively and are summed on emit), zero sums are dropped --
+// the result of expanding, sorting, summing and dropping zeros (fast_encoded_constraint_substitution
+// + fix), in O(w * K) for rows of any length with at most K substituted entries (false otherwise:
+// the caller sorts).  Output from k[0]; the tail [rb, rb + n) must lie beyond every output position.
 template <int K>
-__device__ inline uint32_t d_frame3_merge(const FrameArgs &A, uint32_t *k, Fe *v, uint32_t rb, uint32_t n) {
+__device__ inline bool d_frame3_merge(const FrameArgs &A, uint32_t *k, Fe *v, uint32_t rb, uint32_t n, uint32_t &w_out) {
   const FieldP &F = A.F;
-  uint32_t hk[K], hr[K];
+  uint32_t si[K], hk[K], hr[K];
   uint64_t hb[K];
 #pragma unroll
-  for (int i = 0; i < K; ++i) {
-    hk[i] = RS_NONE;
-    hr[i] = 0;
-    hb[i] = RS_NONE;  // RS_NONE base: the entry itself (not substituted)
-    if ((uint32_t)i < n) {
-      const uint32_t kk = k[rb + i];
-      const int32_t s = A.sub_of[kk];
-      if (s >= 0) {
-        hb[i] = A.h_off[s];
-        hr[i] = A.h_len[s];
-        hk[i] = hr[i] ? A.pk[hb[i]] : RS_NONE;
-      } else {
-        hk[i] = kk;
-        hr[i] = 1;
-      }
-    }
+  for (int j = 0; j < K; ++j) { si[j] = RS_NONE; hk[j] = RS_NONE; hr[j] = 0; hb[j] = 0; }
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int32_t s = A.sub_of[k[rb + i]];
+    if (s < 0) continue;
+    if (ns == (uint32_t)K) return false;
+    const uint64_t off = A.h_off[s];
+    const uint32_t len = A.h_len[s];
+    const uint32_t k0 = len ? A.pk[off] : RS_NONE;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if ((uint32_t)j == ns) { si[j] = i; hb[j] = off; hr[j] = len; hk[j] = k0; }
+    ++ns;
   }
+  auto is_sub = [&](uint32_t i) -> bool {
+    bool r = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) r |= si[j] == i;
+    return r;
+  };
+  uint32_t c0 = 0;
+  while (c0 < n && is_sub(c0)) ++c0;
+  uint32_t key0 = c0 < n ? k[rb + c0] : RS_NONE;
   uint32_t w = 0, lk = RS_NONE;
   Fe lv = fe_zero();
   for (;;) {
-    uint32_t mk = RS_NONE, mi = 0;
+    uint32_t mk = key0, mi = K;  // K: list 0
 #pragma unroll
-    for (int i = 0; i < K; ++i)
-      if (hk[i] < mk) { mk = hk[i]; mi = (uint32_t)i; }
+    for (int j = 0; j < K; ++j)
+      if (hk[j] < mk) { mk = hk[j]; mi = (uint32_t)j; }
     if (mk == RS_NONE) break;
-    uint64_t b = 0;
-    uint32_t rem = 0;
+    Fe c;
+    if (mi == (uint32_t)K) {
+      c = v[rb + c0];
+      ++c0;
+      while (c0 < n && is_sub(c0)) ++c0;
+      key0 = c0 < n ? k[rb + c0] : RS_NONE;
+    } else {
+      uint64_t b = 0;
+      uint32_t rem = 0, ix = 0;
 #pragma unroll
-    for (int i = 0; i < K; ++i)
-      if ((uint32_t)i == mi) { b = hb[i]; rem = hr[i]; }
-    const Fe sc = v[rb + mi];
-    Fe c = sc;
-    uint32_t nk = RS_NONE;
-    if (b != RS_NONE) {
-      c = fmul(F, sc, A.pv[b]);
-      if (rem > 1) nk = A.pk[b + 1];
+      for (int j = 0; j < K; ++j)
+        if ((uint32_t)j == mi) { b = hb[j]; rem = hr[j]; ix = si[j]; }
+      c = fmul(F, v[rb + ix], A.pv[b]);
+      const uint32_t nk = rem > 1 ? A.pk[b + 1] : RS_NONE;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if ((uint32_t)j == mi) { hk[j] = nk; hr[j] = rem - 1; hb[j] = b + 1; }
     }
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-      if ((uint32_t)i == mi) { hk[i] = nk; hr[i] = rem - 1; hb[i] = b == RS_NONE ? b : b + 1; }
     if (mk == lk) {
       lv = fadd(F, lv, c);
     } else {
@@ -2255,7 +2264,8 @@ __device__ inline uint32_t d_frame3_merge(const FrameArgs &A, uint32_t *k, Fe *v
     }
   }
   if (lk != RS_NONE && !fe_is_zero(lv)) { k[w] = lk; v[w] = lv; ++w; }
-  return w;
+  w_out = w;
+  return true;
 }
 
 // Expands one linear combination through the frames into [k, v).  The region holds
@@ -2281,8 +2291,11 @@ __device__ inline uint32_t d_apply_frames(const FrameArgs &A, const uint32_t *ik
       if (A.ce_has[tk[i]]) { tv[i] = fmul(F, tv[i], A.ce_val[tk[i]]); tk[i] = 0; any = true; }
     if (any) n = d_sort_combine(F, tk, tv, n);
   }
-  if (n <= 8) return d_frame3_merge<8>(A, k, v, base, n);
-  // frame 3 expands (rows of more than 8 entries): write from the front, reading from the
+  {
+    uint32_t w;
+    if (d_frame3_merge<8>(A, k, v, base, n, w)) return w;
+  }
+  // frame 3 expands (more than 8 substituted entries): write from the front, reading from the
   // (shrunk) tail copy, then sort
   uint32_t rb = cap - n;
   if (rb != base)
@@ -2373,7 +2386,12 @@ struct RoundArgs {
   uint32_t *tmpk;          // per-row scratch: 2 * cap_c entries at 2 * (C offset - c_base)
   Fe *tmpv;
   uint64_t c_base;
+  const uint32_t *ids;     // the rows a substitution touches (cap_c != 0), compacted
+  uint64_t n_ids;
 };
+__global__ void k_touch_flags(const uint64_t *cap_c, uint64_t n, uint64_t *flag) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) flag[r] = cap_c[r] != 0;
+}
 
 __global__ void k_round_count(RoundArgs A) {
   for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
@@ -2392,12 +2410,12 @@ __global__ void k_round_count(RoundArgs A) {
 // is the (zero-free, sorted) map empty or constant-only?
 __device__ __forceinline__ bool d_const_or_empty(const uint32_t *k, uint32_t n) { return n == 0 || (n == 1 && k[0] == 0); }
 
+// One lane per touched row (the compacted list: untouched rows are neither read nor written here;
+// turn = -1 and touched = 0 were set for every row beforehand).
 __global__ void k_round_fill(RoundArgs A) {
   const FieldP &F = A.F;
-  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
-    A.turn[r] = -1;
-    A.touched[r] = 0;
-    if (A.cap_c[r] == 0) continue;
+  for (uint64_t i = gtid(); i < A.n_ids; i += gstride()) {
+    const uint64_t r = A.ids[i];
     A.touched[r] = 1;
     FrameArgs fr;
     fr.F = F;
