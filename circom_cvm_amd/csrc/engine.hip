@@ -16,6 +16,7 @@
 #include <thread>
 #include <string>
 #include <unordered_map>
+#include <functional>
 #include <vector>
 
 #include <cstring>
@@ -240,12 +241,16 @@ static U3 excl_scan_u3(rs_engine *E, const U3 *in, U3 *out, uint64_t n, const ch
 __global__ void k_pack3(const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n, U3 *out) {
   for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = U3{a[i], b[i], c[i]};
 }
+// entry i sets row ids[i] (ids == nullptr: row i); cap (optional): entries with no space
+// (cap.a == 0) leave their row's offsets alone
 __global__ void k_set_offsets_u3(const U3 *scan, uint64_t ba, uint64_t bb, uint64_t bc, uint64_t n, uint64_t *oa, uint64_t *ob,
-                                 uint64_t *oc) {
+                                 uint64_t *oc, const U3 *cap, const uint32_t *ids) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
-    oa[i] = ba + scan[i].a;
-    ob[i] = bb + scan[i].b;
-    oc[i] = bc + scan[i].c;
+    if (cap && cap[i].a == 0) continue;
+    const uint64_t r = ids ? ids[i] : i;
+    oa[r] = ba + scan[i].a;
+    ob[r] = bb + scan[i].b;
+    oc[r] = bc + scan[i].c;
   }
 }
 
@@ -771,8 +776,13 @@ static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D
 
 // Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
 // the arena hold the substitutions (h_*) and leftovers (l_*), sub_of/deleted are updated.
+// Work enqueued on the main stream while the head clusters are still being eliminated (given the
+// head's cluster ids and the elimination arguments; the tail's substitutions are complete by then).
+using HeadOverlap = std::function<void(const uint32_t *head_ids, uint64_t n_head, const ElimArgs &a)>;
+
 static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
-                                      int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted) {
+                                      int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted,
+                                      const HeadOverlap *overlap = nullptr) {
   double t0 = now_ms();
   DevClusters D = gpu_clusters(E, view, old_heur, d_forb, eo);
   double t1 = now_ms();
@@ -932,6 +942,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
       }
       HC(hipEventRecord(E->evx[5], E->st));
+      if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
       if (n_head) {
         // the head's composition, one Kahn level of all its clusters per launch over the whole GPU
         // (each cluster's DAG is shallow but wide: ~20 levels for thousands of substitutions)
@@ -1468,36 +1479,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   HC(hipStreamSynchronize(st));
   E->stats.eq_ms = now_ms() - T0;
 
-  // ======================= linear round 1 (:544-578)
-  ElimOut eo;
-  Pool P = get_pool(E, 1 << 20);
-  if (apply_linear) {
-    run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted);
-    if (E->log_on) log_linear_round(E, eo, P);
-    collect_leftovers(E, eo, P, lconst);
-    E->stats.rounds++;
-  } else {
-    // --O1: the linear rows join lconst unchanged (:575-577)
-    HostRows H;
-    fetch_keys(E, lin, H);
-    std::vector<uint64_t> hoff(lin.n);
-    if (lin.n) {
-      HC(hipMemcpyAsync(hoff.data(), lin.off, 8 * lin.n, hipMemcpyDeviceToHost, st));
-      HC(hipStreamSynchronize(st));
-    }
-    std::vector<uint32_t> keys;
-    std::vector<uint64_t> vals, optr;
-    fetch_pool_maps(E, hoff, H.len, lin.key, lin.val, keys, vals, optr);
-    for (uint64_t i = 0; i < lin.n; ++i) {
-      HostCon c;
-      c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
-      c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
-      lconst.push_back(std::move(c));
-    }
-  }
-
-  // ======================= obtain_and_simplify_non_linear (non_linear_utils.rs:6-31)
-  double Ts = now_ms();
+  // ======================= obtain_and_simplify_non_linear (non_linear_utils.rs:6-31): setup
   const uint64_t n_nl = E->na.n;
   DRows ia{}, ib{}, ic{};
   auto mk_in = [&](rs_engine::Blk &B, DRows &R, const char *nm) {
@@ -1544,10 +1526,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   fr.ce_has = ce_has;
   fr.ce_val = ce_val;
   fr.sub_of = sub_of;
-  fr.h_off = A.get<uint64_t>("el.h_off", 1);
-  fr.h_len = A.get<uint32_t>("el.h_len", 1);
-  fr.pk = P.pk;
-  fr.pv = P.pv;
   for (DRows *R : {&sa, &sb, &sc}) {
     R->n = n_nl;
   }
@@ -1557,32 +1535,117 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   sb.len = A.get<uint32_t>("st.b.len", n_nl);
   sc.off = A.get<uint64_t>("st.c.off", n_nl);
   sc.len = A.get<uint32_t>("st.c.len", n_nl);
+  uint64_t *ca = nullptr, *cb = nullptr, *cc = nullptr;
+  U3 *cap3 = nullptr, *sc3 = nullptr;
+  uint64_t *nl_late = nullptr, *nl_lpos = nullptr;
+  uint8_t *hmark = nullptr;
+  uint32_t *nl_lids = nullptr;
+  uint64_t n_late = 0;
   if (n_nl) {
-    uint64_t *ca = A.get<uint64_t>("nl.capa", n_nl), *cb = A.get<uint64_t>("nl.capb", n_nl), *cc = A.get<uint64_t>("nl.capc", n_nl);
+    ca = A.get<uint64_t>("nl.capa", n_nl); cb = A.get<uint64_t>("nl.capb", n_nl); cc = A.get<uint64_t>("nl.capc", n_nl);
+    cap3 = A.get<U3>("nl.c3", n_nl); sc3 = A.get<U3>("nl.s3", n_nl);
+  }
+  // one pass of the frames over the non-linear rows ids[0, n) (phase: see NLArgs); the fill's
+  // kernel time is read from (e0, e1) once the caller synchronises
+  auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1) {
     NLArgs a;
     a.fr = fr;
     a.a = ia; a.b = ib; a.c = ic;
     a.cap_a = ca; a.cap_b = cb; a.cap_c = cc;
     a.bytes = d_bytes;
-    launch(st, k_nl_count, n_nl, a);
-    U3 *cap3 = A.get<U3>("nl.c3", n_nl), *sc3 = A.get<U3>("nl.s3", n_nl);
-    launch(st, k_pack3, n_nl, (const uint64_t *)ca, (const uint64_t *)cb, (const uint64_t *)cc, n_nl, cap3);
-    const U3 t3 = excl_scan_u3(E, cap3, sc3, n_nl, "nl");
+    a.ids = ids;
+    a.n = n;
+    a.phase = phase;
+    a.hmark = hmark;
+    a.late = nl_late;
+    launch(st, k_nl_count, n, a);
+    if (phase == 1) {  // the skipped rows, listed for the second pass
+      n_late = excl_scan_u64(E, nl_late, nl_lpos, n_nl, "nll");
+      launch(st, k_scatter_ids, n_nl, (const uint64_t *)nl_late, (const uint64_t *)nl_lpos, n_nl, nl_lids);
+    }
+    launch(st, k_pack3, n, (const uint64_t *)ca, (const uint64_t *)cb, (const uint64_t *)cc, n, cap3);
+    const U3 t3 = excl_scan_u3(E, cap3, sc3, n, "nl");
+    if (g_prof_env) fprintf(stderr, "[rs-prof] nl phase %d: %llu rows, %llu heap entries\n", phase, (unsigned long long)n,
+                            (unsigned long long)(t3.a + t3.b + t3.c));
     heap_reserve(t3.a + t3.b + t3.c);
-    launch(st, k_set_offsets_u3, n_nl, (const U3 *)sc3, heap_top, heap_top + t3.a, heap_top + t3.a + t3.b, n_nl, sa.off, sb.off,
-           sc.off);
+    launch(st, k_set_offsets_u3, n, (const U3 *)sc3, heap_top, heap_top + t3.a, heap_top + t3.a + t3.b, n, sa.off, sb.off,
+           sc.off, phase == 1 ? (const U3 *)cap3 : nullptr, ids);
     heap_top += t3.a + t3.b + t3.c;
     sa.key = sb.key = sc.key = heap_k;
     sa.val = sb.val = sc.val = heap_v;
     a.oa = sa; a.ob = sb; a.oc = sc;
-    HC(hipEventRecord(E->ev0, st));
-    launch(st, k_nl_fill, n_nl, a);
-    HC(hipEventRecord(E->ev1, st));
-    HC(hipEventSynchronize(E->ev1));
-    float ms = 0;
-    HC(hipEventElapsedTime(&ms, E->ev0, E->ev1));
-    E->stats.apply_kernel_ms += ms;
+    HC(hipEventRecord(e0, st));
+    launch(st, k_nl_fill, n, a);
+    HC(hipEventRecord(e1, st));
     E->stats.apply_kernel_launches++;
+  };
+  auto nl_ms = [&](hipEvent_t e0, hipEvent_t e1) {
+    float ms = 0;
+    HC(hipEventSynchronize(e1));
+    HC(hipEventElapsedTime(&ms, e0, e1));
+    E->stats.apply_kernel_ms += ms;
+  };
+  // rows that touch none of the largest clusters go through the frames while those clusters are
+  // still being eliminated (single rank: a sharded run learns the substitutions at the exchange)
+  bool nl_split = false;
+  HeadOverlap overlap = [&](const uint32_t *ids, uint64_t n_head, const ElimArgs &ea) {
+    hmark = A.get<uint8_t>("nl.hmark", E->S);
+    nl_late = A.get<uint64_t>("nl.late", n_nl);
+    nl_lpos = A.get<uint64_t>("nl.lpos", n_nl);
+    nl_lids = A.get<uint32_t>("nl.lids", n_nl);
+    HC(hipMemsetAsync(hmark, 0, E->S, st));
+    hipLaunchKernelGGL(k_mark_head_keys, dim3(16, (unsigned)n_head), dim3(256), 0, st, ea.rows, (const uint32_t *)ea.perm,
+                       (const uint64_t *)ea.cl_off, ids, hmark);
+    HC(hipGetLastError());
+    fr.h_off = ea.h_off; fr.h_len = ea.h_len; fr.pk = ea.pk; fr.pv = ea.pv;
+    nl_phase(1, nullptr, n_nl, E->evx[6], E->evx[7]);
+    nl_split = true;
+  };
+
+  // ======================= linear round 1 (:544-578)
+  ElimOut eo;
+  Pool P = get_pool(E, 1 << 20);
+  if (apply_linear) {
+    run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted,
+                              n_nl && !E->comm ? &overlap : nullptr);
+    if (E->log_on) log_linear_round(E, eo, P);
+    collect_leftovers(E, eo, P, lconst);
+    E->stats.rounds++;
+  } else {
+    // --O1: the linear rows join lconst unchanged (:575-577)
+    HostRows H;
+    fetch_keys(E, lin, H);
+    std::vector<uint64_t> hoff(lin.n);
+    if (lin.n) {
+      HC(hipMemcpyAsync(hoff.data(), lin.off, 8 * lin.n, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+    }
+    std::vector<uint32_t> keys;
+    std::vector<uint64_t> vals, optr;
+    fetch_pool_maps(E, hoff, H.len, lin.key, lin.val, keys, vals, optr);
+    for (uint64_t i = 0; i < lin.n; ++i) {
+      HostCon c;
+      c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
+      c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
+      lconst.push_back(std::move(c));
+    }
+  }
+
+  // ======================= obtain_and_simplify_non_linear (non_linear_utils.rs:6-31)
+  double Ts = now_ms();
+  fr.h_off = A.get<uint64_t>("el.h_off", 1);
+  fr.h_len = A.get<uint32_t>("el.h_len", 1);
+  fr.pk = P.pk;
+  fr.pv = P.pv;
+  if (n_nl) {
+    if (nl_split) nl_ms(E->evx[6], E->evx[7]);
+    if (!nl_split) {
+      nl_phase(0, nullptr, n_nl, E->ev0, E->ev1);
+      nl_ms(E->ev0, E->ev1);
+    } else if (n_late) {
+      nl_phase(2, nl_lids, n_late, E->ev0, E->ev1);
+      nl_ms(E->ev0, E->ev1);
+    }
   }
   unsigned long long bytes = 0;
   HC(hipMemcpyAsync(&bytes, d_bytes, 8, hipMemcpyDeviceToHost, st));
@@ -1783,7 +1846,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         ob.off = A.get<uint64_t>("r.ob.off", n_st); ob.len = A.get<uint32_t>("r.ob.len", n_st);
         oc.off = A.get<uint64_t>("r.oc.off", n_st); oc.len = A.get<uint32_t>("r.oc.len", n_st);
         launch(st, k_set_offsets_u3, n_st, (const U3 *)sc3, heap_top, heap_top + q3.a, heap_top + q3.a + q3.b, n_st, oa.off,
-               ob.off, oc.off);
+               ob.off, oc.off, (const U3 *)nullptr, (const uint32_t *)nullptr);
         heap_top += qt;
         ra.c_base = heap_top - q3.c;  // row scratch = 2 * (its C offset - c_base)
         ra.oa = oa; ra.ob = ob; ra.oc = oc;

@@ -2328,27 +2328,75 @@ struct NLArgs {
   DRows oa, ob, oc;    // output rows (off/cap computed by the count pass)
   uint64_t *cap_a, *cap_b, *cap_c;
   unsigned long long *bytes;  // algorithmic bytes counter
+  // rows processed: ids[0, n) (ids == nullptr: rows 0..n-1); cap_* are indexed by position in that list.
+  // phase 1 (while the largest clusters are still being eliminated) skips the rows one of whose
+  // signals (after frames 1-2) occurs in those clusters, flagging them in `late`; the caller runs
+  // them once every substitution is known.
+  const uint32_t *ids;
+  uint64_t n;
+  int phase;
+  const uint8_t *hmark;  // signal -> occurs in a row of a head cluster
+  uint64_t *late;
 };
 
+// Marks the signals of the head clusters' rows (signal 0 is never substituted).
+__global__ void k_mark_head_keys(DRows rows, const uint32_t *perm, const uint64_t *cl_off, const uint32_t *ids,
+                                 uint8_t *hmark) {
+  const uint32_t c = ids[blockIdx.y];
+  const uint64_t b = cl_off[c], e = cl_off[c + 1];
+  for (uint64_t i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = perm[i];
+    const uint64_t o = rows.off[r];
+    for (uint32_t j = 0; j < rows.len[r]; ++j) {
+      const uint32_t k = rows.key[o + j];
+      if (k) hmark[k] = 1;
+    }
+  }
+}
+
+__device__ inline bool d_touches_head(const FrameArgs &F, const uint8_t *hmark, const DRows &R, uint64_t r) {
+  const uint64_t o = R.off[r];
+  for (uint32_t i = 0; i < R.len[r]; ++i) {
+    const uint32_t k = R.key[o + i];
+    const int32_t t = F.eq_rep ? F.eq_rep[k] : -1;
+    const uint32_t k1 = t >= 0 ? (uint32_t)t : k;
+    if (F.ce_has && F.ce_has[k1]) continue;
+    if (hmark[k1]) return true;
+  }
+  return false;
+}
+
 __global__ void k_nl_count(NLArgs A) {
-  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
+  for (uint64_t x = gtid(); x < A.n; x += gstride()) {
+    const uint64_t r = A.ids ? A.ids[x] : x;
+    if (A.phase == 1) {
+      const bool lt = d_touches_head(A.fr, A.hmark, A.a, r) || d_touches_head(A.fr, A.hmark, A.b, r) ||
+                      d_touches_head(A.fr, A.hmark, A.c, r);
+      A.late[r] = lt;
+      if (lt) {  // a later pass's row: no space now
+        A.cap_a[x] = A.cap_b[x] = A.cap_c[x] = 0;
+        continue;
+      }
+    }
     // expansion bound + 1, plus the staged input (d_apply_frames)
     uint64_t ca = 1 + A.a.len[r], cb = 1 + A.b.len[r], cc = 1 + A.c.len[r];
     for (uint32_t i = 0; i < A.a.len[r]; ++i) ca += d_frame_weight(A.fr, A.a.key[A.a.off[r] + i]);
     for (uint32_t i = 0; i < A.b.len[r]; ++i) cb += d_frame_weight(A.fr, A.b.key[A.b.off[r] + i]);
     for (uint32_t i = 0; i < A.c.len[r]; ++i) cc += d_frame_weight(A.fr, A.c.key[A.c.off[r] + i]);
-    A.cap_a[r] = ca;
-    A.cap_b[r] = cb;
-    A.cap_c[r] = 2 * cc + (ca > cb ? ca : cb);  // expansion + scratch for c - a0*b
+    A.cap_a[x] = ca;
+    A.cap_b[x] = cb;
+    A.cap_c[x] = 2 * cc + (ca > cb ? ca : cb);  // expansion + scratch for c - a0*b
   }
 }
 
 __global__ void k_nl_fill(NLArgs A) {
   unsigned long long bytes = 0;
-  for (uint64_t r = gtid(); r < A.a.n; r += gstride()) {
+  for (uint64_t x = gtid(); x < A.n; x += gstride()) {
+    const uint64_t r = A.ids ? A.ids[x] : x;
+    if (A.phase == 1 && A.late[r]) continue;
     uint64_t oa = A.oa.off[r], ob = A.ob.off[r], oc = A.oc.off[r];
-    uint32_t capa = (uint32_t)A.cap_a[r], capb = (uint32_t)A.cap_b[r];
-    uint32_t capc = (uint32_t)A.cap_c[r];
+    uint32_t capa = (uint32_t)A.cap_a[x], capb = (uint32_t)A.cap_b[x];
+    uint32_t capc = (uint32_t)A.cap_c[x];
     uint32_t mx = capa > capb ? capa : capb;
     uint32_t cc = (capc - mx) / 2;
     uint32_t na = d_apply_frames(A.fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
