@@ -145,7 +145,8 @@ struct rs_engine {
   int device = 0;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // the largest clusters' elimination chain runs here, beside the rest
-  hipEvent_t evx[8] = {};     // [0] join-in, [1..4] head chain, [5] after the lane kernel
+  hipEvent_t evx[10] = {};    // [0] join-in, [1..4] head chain, [5] after the lane kernel, [6..7] the
+                              // largest replays' fork / join, [8..9] the overlapped frames pass
   Arena A;
   bool loaded = false;
   bool have_result = false;
@@ -608,7 +609,15 @@ struct DevClusters {
   uint32_t *perm = nullptr, *big = nullptr, *small = nullptr, *cid = nullptr;
   uint64_t *cl_off = nullptr;
   uint64_t n_slots = 0, n_big = 0, n_small = 0, tot_nnz = 0;
+  // the largest clusters' row orders are still being replayed on the second stream (evx[7] marks
+  // the end); only the head -- ordered after the replay on that stream -- reads them until the join
+  bool join_pending = false;
 };
+// the number of largest clusters eliminated on the second stream (RS_HEAD overrides)
+static uint64_t head_limit() {
+  const char *hd = getenv("RS_HEAD");
+  return hd ? (uint64_t)atoi(hd) : 16;
+}
 static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, const uint8_t *d_forb, ElimOut &eo) {
   Arena &A = E->A;
   hipStream_t st = E->st;
@@ -704,9 +713,12 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
                        (const uint32_t *)n_ordered, old_heur);
     HC(hipGetLastError());
   }
-  if (hc[4]) {  // join: the elimination reads every cluster's order
+  if (hc[4]) {  // join: the elimination reads every cluster's order -- deferred when every cluster
+                // replayed there is a head cluster (single rank: the head is this rank's largest)
     HC(hipEventRecord(E->evx[7], E->st2));
-    HC(hipStreamWaitEvent(st, E->evx[7], 0));
+    const bool sharded = E->comm && E->comm->world > 1;
+    if (!sharded && hc[3] + hc[4] <= head_limit()) D.join_pending = true;
+    else HC(hipStreamWaitEvent(st, E->evx[7], 0));
   }
   // elimination split: clusters of kWaveMin rows or more (a prefix of the size order) go to the
   // workgroup kernels (process_3 or process_4 per cluster), the rest one lane each
@@ -858,8 +870,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     HC(hipMemsetAsync(a.bytes, 0, 24, E->st));
     // The largest clusters' prep -> main -> finish chain runs on a second stream: the elimination
     // time is the critical path of the largest cluster, and everything else overlaps it.
-    const char *hd = getenv("RS_HEAD");
-    const uint64_t n_head = std::min<uint64_t>(n_big, hd ? (uint64_t)atoi(hd) : 16), n_tail = n_big - n_head;
+    const uint64_t n_head = std::min<uint64_t>(n_big, head_limit()), n_tail = n_big - n_head;
     a.wide = 1;       // the head's largest process_4 clusters go through the k_wide_* grid
     ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
     at.wide = 0;
@@ -942,6 +953,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
       }
       HC(hipEventRecord(E->evx[5], E->st));
+      if (D.join_pending) {  // the main stream reads the head clusters' orders from here on
+        HC(hipStreamWaitEvent(E->st, E->evx[7], 0));
+        D.join_pending = false;
+      }
       if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
       if (n_head) {
         // the head's composition, one Kahn level of all its clusters per launch over the whole GPU
@@ -1598,7 +1613,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
                        (const uint64_t *)ea.cl_off, ids, hmark);
     HC(hipGetLastError());
     fr.h_off = ea.h_off; fr.h_len = ea.h_len; fr.pk = ea.pk; fr.pv = ea.pv;
-    nl_phase(1, nullptr, n_nl, E->evx[6], E->evx[7]);
+    nl_phase(1, nullptr, n_nl, E->evx[8], E->evx[9]);
     nl_split = true;
   };
 
@@ -1638,7 +1653,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   fr.pk = P.pk;
   fr.pv = P.pv;
   if (n_nl) {
-    if (nl_split) nl_ms(E->evx[6], E->evx[7]);
+    if (nl_split) nl_ms(E->evx[8], E->evx[9]);
     if (!nl_split) {
       nl_phase(0, nullptr, n_nl, E->ev0, E->ev1);
       nl_ms(E->ev0, E->ev1);
