@@ -886,13 +886,14 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       ah.split = 1;
       ah.cf_items = E->A.get<uint64_t>("cf.items0", cap_items);
       cf_next = E->A.get<uint64_t>("cf.items1", cap_items);
-      ah.cf_n = E->A.get<unsigned long long>("cf.cnt", 2);
+      ah.cf_n = E->A.get<unsigned long long>("cf.cnt", 3);  // frontier counts, rotating over the levels
       ah.cf_deg = E->A.get<uint64_t>("cf.deg", n_head);
       ah.cf_dl = E->A.get<uint64_t>("cf.dl", n_head);
       ah.cf_done = E->A.get<uint32_t>("cf.done", n_head);
       ah.cf_big = E->A.get<uint64_t>("cf.big", cap_items);
-      ah.cf_nbig = E->A.get<unsigned long long>("cf.nbig", 1);
-      HC(hipMemsetAsync(ah.cf_n, 0, 16, E->st));
+      ah.cf_nbig = E->A.get<unsigned long long>("cf.nbig", 2);  // deferred counts, alternating
+      HC(hipMemsetAsync(ah.cf_n, 0, 24, E->st));
+      HC(hipMemsetAsync(ah.cf_nbig, 0, 16, E->st));
     }
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
@@ -961,22 +962,26 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       if (n_head) {
         // the head's composition, one Kahn level of all its clusters per launch over the whole GPU
         // (each cluster's DAG is shallow but wide: ~20 levels for thousands of substitutions)
+        // Level L reads count L%3, appends to (L+1)%3 and zeroes (L+2)%3 -- the one level L-1 read and
+        // level L+1 appends to -- and likewise alternates the deferred list's count: no memsets.
         uint64_t *cur = ah.cf_items, *nxt = cf_next;
-        unsigned long long *nc = ah.cf_n, *nn = ah.cf_n + 1;
+        unsigned long long *nn = ah.cf_n + 1;
         uint32_t levels = 0;
         for (uint32_t level = 0; level <= n_slots + 1; ++level) {
-          HC(hipMemsetAsync(nn, 0, 8, E->st2));
-          HC(hipMemsetAsync(ah.cf_nbig, 0, 8, E->st2));
-          hipLaunchKernelGGL(k_compose_level<8>, dim3(256), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big,
-                             (const uint64_t *)cur, (const unsigned long long *)nc, nxt, nn, level);
-          hipLaunchKernelGGL(k_compose_big, dim3(256), dim3(64), 0, E->st2, ah, (const uint32_t *)d_big, nxt, nn);
+          ElimArgs al = ah;
+          al.cf_nbig = ah.cf_nbig + (level & 1);
+          unsigned long long *nc = ah.cf_n + level % 3, *zc = ah.cf_n + (level + 2) % 3;
+          nn = ah.cf_n + (level + 1) % 3;
+          hipLaunchKernelGGL(k_compose_level<8>, dim3(256), dim3(512), 0, E->st2, al, (const uint32_t *)d_big,
+                             (const uint64_t *)cur, (const unsigned long long *)nc, nxt, nn, level, zc,
+                             ah.cf_nbig + ((level + 1) & 1));
+          hipLaunchKernelGGL(k_compose_big, dim3(256), dim3(64), 0, E->st2, al, (const uint32_t *)d_big, nxt, nn);
           HC(hipGetLastError());
           std::swap(cur, nxt);
-          std::swap(nc, nn);
           levels = level + 1;
           if (level % 4 == 3) {  // stop once a frontier is empty (checked every few levels)
             unsigned long long h = 0;
-            HC(hipMemcpyAsync(&h, nc, 8, hipMemcpyDeviceToHost, E->st2));
+            HC(hipMemcpyAsync(&h, nn, 8, hipMemcpyDeviceToHost, E->st2));
             HC(hipStreamSynchronize(E->st2));
             if (!h) break;
           }

@@ -2063,7 +2063,8 @@ __global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void k_compose_level(ElimArgs A, const uint32_t *ids, const uint64_t *cur,
                                                           const unsigned long long *n_cur, uint64_t *nxt,
-                                                          unsigned long long *n_nxt, uint32_t level) {
+                                                          unsigned long long *n_nxt, uint32_t level,
+                                                          unsigned long long *zero_cnt, unsigned long long *zero_big) {
   __shared__ uint64_t cw_S[NW][kComposeCap];
   __shared__ Fe cw_V[NW][kComposeCap];
   __shared__ uint32_t cw_dex[NW][64];
@@ -2074,6 +2075,10 @@ __global__ __launch_bounds__(64 * NW) void k_compose_level(ElimArgs A, const uin
   al.chunk = 128;
   unsigned long long by = 0;
   const uint64_t n = *n_cur, total = (uint64_t)gridDim.x * NW;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the counters the next level starts from (see the host loop)
+    *zero_cnt = 0;
+    *zero_big = 0;
+  }
   for (uint64_t f = (uint64_t)blockIdx.x * NW + wv_; f < n; f += total) {
     const uint64_t item = cur[f];
     const uint32_t ci = (uint32_t)(item >> 32), q = (uint32_t)item;
