@@ -1,16 +1,26 @@
 """bench.py -- constraints simplified/sec (--O2) on the 10M-constraint synthetic circuit.
 
-One step = one full --O2 simplification (rs_engine_run): the Simplifier bundle already resident in
-HBM -> simplified constraints + label->wire map resident in HBM.  N ranks (one process per GPU,
-torch.distributed over RCCL) each own an independent shard of template instances (weak scaling;
-the shards share no signal, so no exchange step is needed -- see DESIGN.md "Multi-GPU").
+One step = one full --O2 simplification measured as SURVEY 8(d) defines T_simplify: the Simplifier
+bundle as CSR blocks in HOST memory -> the simplified constraints + label->wire map in HOST memory
+(rs_engine_simplify on a persistent engine: H2D of the input overlapped with the simplification,
+device validation, the whole of constraint_simplification.rs:442-730 on the GPU, D2H of the result
+into pinned buffers).  The input blocks live in page-locked memory from rs_host_alloc, the buffers a
+Rust shim marshals the Simplifier into.
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events around it on
-the library's own stream) and the CPU baseline (the canonical CPU oracle, oracle/refcpu.cpp, on a
-bounded sample of the same workload, rank 0 only)."""
+N = 1: the metric circuit on one GPU.  N > 1 (one process per GPU, torch.distributed over RCCL):
+`value` is the SAME circuit sharded over the N ranks (its clusters dealt to the ranks, the
+eliminated-signal map exchanged over RCCL; strong scaling); the independent-shard number (each rank
+its own circuit, no collective; weak scaling) is the extra object `weak_shards`.
+
+Rank 0 prints ONE JSON line with: the roofline of the dominant kernel (HIP events on the library's
+streams, in-kernel algorithmic bytes; head and tail of the ordered elimination split), the
+whole-path roofline B_alg / T_simplify, the HBM-resident rate as an extra key, the CPU baseline (the
+canonical CPU oracle oracle/refcpu.cpp on this box's cores, plus a 1-thread leg on a bounded sample)
+and `bit_exact`: the last timed step's output compared array for array with the oracle's."""
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -23,26 +33,33 @@ METRIC = "constraints simplified/sec (--O2) on 10M-constraint circuit; bit-exact
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(rows: int, seed: int, threads: int, prime: str):
-    """The canonical CPU oracle (oracle/refcpu.cpp) on the same synthetic circuit as rank 0 (or a
-    smaller bounded sample when --cpu-rows is lower), on `threads` host threads."""
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: this process's CPU share (the box exports
+    OMP_NUM_THREADS = its share; os.sched_getaffinity lists the whole machine there)."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
+
+
+def cpu_baseline(M, inp, threads: int, j1_rows: int, seed: int, prime: str):
+    """The canonical CPU oracle (oracle/refcpu.cpp) on the rank-0 workload on `threads` threads (its
+    output is the bit-exactness reference), and on 1 thread over a bounded sample (the same generator,
+    j1_rows rows)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import rsio
-    import circom_cvm_amd as M
-    inp = M.Input.synth(0, rows, seed, prime)
-    t0 = time.time()
-    _, ms = rsio.oracle_arrays(inp.c, rsio.flags("O2"), threads=threads)
-    wall = time.time() - t0
-    return {"value": round(inp.rows() / (ms / 1000.0), 1), "unit": "constraints/s", "cores": threads,
-            "kind": "port",
-            "sample": f"synth_mixed rows={inp.rows()} seed={seed} {prime} --O2 (the rank-0 workload), "
-                      f"oracle/refcpu.cpp simplification() on {threads} threads: {ms / 1000.0:.1f} s "
-                      f"({wall:.1f} s incl. output copy)"}
-
-
-def shard_seed(seed: int, rank: int) -> int:
-    """Rank r simplifies its own circuit shard: the synthetic generator seeded with seed + r."""
-    return seed + rank
+    arrays, ms = rsio.oracle_arrays(inp.c, rsio.flags("O2"), threads=threads)
+    res = {"value": round(inp.rows() / (ms / 1000.0), 1), "unit": "constraints/s", "cores": threads,
+           "kind": "port", "affinity_cpus": len(os.sched_getaffinity(0)),
+           "sample": f"the full rank-0 workload ({inp.rows()} rows), oracle/refcpu.cpp simplification() "
+                     f"on {threads} threads: {ms / 1000.0:.2f} s"}
+    if j1_rows > 0:
+        smp = M.Input.synth(0, j1_rows, seed, prime)
+        _, ms1 = rsio.oracle_arrays(smp.c, rsio.flags("O2"), threads=1)
+        res["j1"] = {"value": round(smp.rows() / (ms1 / 1000.0), 1), "unit": "constraints/s", "cores": 1,
+                     "sample": f"synth_mixed rows={smp.rows()} seed={seed} {prime} --O2 on 1 thread: "
+                               f"{ms1 / 1000.0:.2f} s"}
+        smp.free()
+    return res, arrays
 
 
 def reduce_over_ranks(dist, dt: float, n_rows: int, device):
@@ -66,52 +83,63 @@ def share_comm_id(dist, rank: int, make):
     return obj[0]
 
 
-def sharded_one_circuit(M, dist, args, world, rank, local, fl, barrier):
-    """The SAME 10M metric circuit on every rank, its clusters dealt to the ranks and the
-    eliminated-signal map exchanged over RCCL (SURVEY 8(e), strong scaling).  Returns the max over
-    ranks of ms/step and the exchange time, measured like the headline."""
-    uid = share_comm_id(dist, rank, M.comm_unique_id)
-    inp = M.Input.synth(0, args.rows, args.seed, args.prime)
-    eng = M.Engine(local)
-    eng.join_rccl(world, rank, uid)
-    eng.load(inp.c)
-    for _ in range(args.warmup):
-        eng.run(fl)
+def shard_seed(seed: int, rank: int) -> int:
+    """Weak-scaling mode: rank r simplifies its own circuit, the generator seeded with seed + r."""
+    return seed + rank
+
+
+KERNELS = (  # (name, stats fields: ms, bytes, launches)
+    ("k_big_main<512> (head)", "head_main_ms", "head_main_bytes", "head_launches"),
+    ("k_big_main<256> (tail)", "tail_main_ms", "tail_main_bytes", "tail_launches"),
+    ("k_nl_fill", "apply_kernel_ms", "apply_bytes", "apply_kernel_launches"),
+    ("k_round_fill", "round_fill_ms", "round_fill_bytes", "round_fill_launches"),
+)
+
+
+def pmc_traffic():
+    """HBM bytes per launch per kernel from the newest committed PMC summary (profiles/
+    round*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes of this bench)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_traffic.json")))
+    if not files:
+        return {}, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("bytes_per_launch", {}), os.path.relpath(files[-1], ROOT)
+
+
+def timed_steps(eng, inp_c, fl, steps, barrier):
+    """K host -> host steps between barriers; per-kernel device time/bytes summed over them."""
+    acc = {k: [0.0, 0, 0] for k, *_ in KERNELS}
+    tot = {"alg_bytes": 0, "total_ms": 0.0, "h2d_wait_ms": 0.0, "d2h_ms": 0.0, "host_total_ms": 0.0}
     barrier()
     t0 = time.perf_counter()
-    xms = 0.0
-    for _ in range(args.steps):
-        eng.run(fl)
-        xms += eng.stats().exchange_ms
+    out = None
+    for _ in range(steps):
+        out = eng.simplify(inp_c, fl)
+        st = eng.stats()
+        for k, fm, fb, fn in KERNELS:
+            acc[k][0] += getattr(st, fm)
+            acc[k][1] += getattr(st, fb)
+            acc[k][2] += getattr(st, fn)
+        for k in tot:
+            tot[k] += getattr(st, k)
     barrier()
-    dt = time.perf_counter() - t0
-    dt, _ = reduce_over_ranks(dist, dt, 0, "cuda")
-    xmax, _ = reduce_over_ranks(dist, xms, 0, "cuda")
-    n = inp.rows()
-    st = eng.stats()
-    eng.close()
-    return {"workload": f"synth_mixed rows={args.rows} prime={args.prime} seed={args.seed} --O2, ONE circuit "
-                        f"on {world} ranks (clusters dealt by size, RCCL exchange of the eliminated-signal map)",
-            "scaling": "strong", "constraints": n, "ms_per_step": round(dt * 1000.0 / args.steps, 3),
-            "value": round(n * args.steps / dt, 1), "unit": "constraints/s",
-            "exchange_ms_per_step": round(xmax / args.steps, 3), "exchange_bytes_per_rank": int(st.exchange_bytes)}
+    return time.perf_counter() - t0, acc, tot, out, eng.stats()
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=80)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--prime", default="bn128")
-    ap.add_argument("--cpu-rows", type=int, default=10_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: this process's CPU share")
+    ap.add_argument("--cpu-j1-rows", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--mode", choices=("shards", "both"), default="both",
-                    help="N>1: shards = the headline only (each rank its own circuit shard, weak "
-                         "scaling); both = the headline + ONE circuit sharded over all ranks with the "
-                         "RCCL exchange (strong scaling), as the extra object sharded_one_circuit")
+    ap.add_argument("--no-weak", action="store_true", help="N>1: skip the independent-shard extra run")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,15 +154,7 @@ def main():
         dist = dist_
 
     import circom_cvm_amd as M
-
-    # each rank: its own shard of instances (seed + rank), staged in HBM once
-    inp = M.Input.synth(0, args.rows, shard_seed(args.seed, rank), args.prime)
-    n_rows = inp.rows()
-    eng = M.Engine(local)
-    eng.load(inp.c)
-    fl = M.make_flags("O2", device=local)
-    for _ in range(args.warmup):
-        eng.run(fl)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
 
     def barrier():
         if dist is not None:
@@ -142,67 +162,112 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    fl = M.make_flags("O2", device=local)
+    # ---- the headline: the metric circuit (ONE circuit over all ranks when N > 1), host -> host
+    inp = M.Input.synth(0, args.rows, args.seed, args.prime)
+    n_rows = inp.rows()
+    pin = M.PinnedInput(inp.c)
+    eng = M.Engine(local)
+    if world > 1:
+        eng.join_rccl(world, rank, share_comm_id(dist, rank, M.comm_unique_id))
+    for _ in range(args.warmup):
+        eng.simplify(pin.c, fl)
+    dt, acc, tot, out, last = timed_steps(eng, pin.c, fl, args.steps, barrier)
+    dt, _ = reduce_over_ranks(dist, dt, n_rows, "cuda")
+    got = None
+    if rank == 0 and not args.no_cpu:
+        import rsio
+        got = rsio.output_arrays(out)  # copy of the last timed step's result (the view is reused)
+    # ---- extra: the same engine with the input resident in HBM (rs_engine_run only)
+    eng.load(pin.c)
     barrier()
-    # device time + algorithmic bytes per kernel over the timed region (HIP events recorded by the
-    # library on its own stream around each launch; bytes counted in-kernel, SURVEY 8(d) B_alg terms)
-    K = {"k_big_main": [0.0, 0, 0], "k_big_finish": [0.0, 0, 0], "k_nl_fill": [0.0, 0, 0]}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.run(fl)  # synchronous: returns after its stream has drained
-        st = eng.stats()
-        for k, ms, by, n in (("k_big_main", st.big_main_ms, st.big_main_bytes, st.big_launches),
-                             ("k_big_finish", st.big_finish_ms, st.big_finish_bytes, st.big_launches),
-                             ("k_nl_fill", st.apply_kernel_ms, st.apply_bytes, st.apply_kernel_launches)):
-            K[k][0] += ms
-            K[k][1] += by
-            K[k][2] += n
+        eng.run(fl)
     barrier()
-    dt = time.perf_counter() - t0
-    dt, total_rows = reduce_over_ranks(dist, dt, n_rows, "cuda")
-    last = eng.stats()
-    sharded = None
-    if dist is not None and args.mode == "both":
-        eng.close()  # free the headline engine's HBM before the second one
-        sharded = sharded_one_circuit(M, dist, args, world, rank, local, fl, barrier)
+    dt_hbm, _ = reduce_over_ranks(dist, time.perf_counter() - t0, n_rows, "cuda")
+    eng.close()
+    pin.free()
+    # ---- extra at N > 1: independent circuits per rank (weak scaling, no data-path collective)
+    weak = None
+    if world > 1 and not args.no_weak:
+        winp = M.Input.synth(0, args.rows, shard_seed(args.seed, rank), args.prime)
+        wpin = M.PinnedInput(winp.c)
+        weng = M.Engine(local)
+        for _ in range(args.warmup):
+            weng.simplify(wpin.c, fl)
+        wdt, _, _, _, _ = timed_steps(weng, wpin.c, fl, args.steps, barrier)
+        wdt, wrows = reduce_over_ranks(dist, wdt, winp.rows(), "cuda")
+        weng.close()
+        wpin.free()
+        winp.free()
+        weak = {"scaling": "weak", "value": round(wrows * args.steps / wdt, 1), "unit": "constraints/s",
+                "ms_per_step": round(wdt * 1000.0 / args.steps, 3),
+                "workload": f"each rank its own synth_mixed rows={args.rows} seed={args.seed}+rank circuit "
+                            f"(no data-path collective), host -> host"}
+
     if rank == 0:
-        ms_step = dt * 1000.0 / args.steps
-        value = total_rows * args.steps / dt
-        # dominant kernel: the largest device time over the timed region
-        k_name = max(K, key=lambda k: K[k][0])
-        k_ms, k_bytes, k_launch = K[k_name]
-        per_launch_s = (k_ms / 1000.0) / max(k_launch, 1)
-        per_launch_bytes = k_bytes / max(k_launch, 1)
-        achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-        traffic = None
-        tf = os.environ.get("RS_PMC_TRAFFIC_BYTES")  # from profiles/ PMC pass, per launch
-        if tf:
-            traffic = float(tf)
+        K = args.steps
+        ms_step = dt * 1000.0 / K
+        value = n_rows * K / dt
+        # the dominant kernel: the largest device time over the timed region
+        k_name = max(acc, key=lambda k: acc[k][0])
+        traffic_tab, traffic_src = pmc_traffic()
+
+        def kline(k):
+            ms, by, n = acc[k]
+            per_s = (ms / 1000.0) / max(n, 1)
+            per_b = by / max(n, 1)
+            ach = per_b / per_s / 1e9 if per_s > 0 else 0.0
+            return {"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
+                    "avg_launch_ms": round(per_s * 1000.0, 4), "alg_bytes_per_launch": int(per_b),
+                    "launches_per_step": n / K, "ms_per_step": round(ms / K, 3),
+                    "traffic": traffic_tab.get(k)}
+        dom = kline(k_name)
+        path_ach = tot["alg_bytes"] / K / (ms_step / 1000.0) / 1e9
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "constraints/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "steps": K, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "strong" if world > 1 else "weak", "vs_baseline": None,
             "dtype": "u64x4 (F_p, 256-bit Montgomery)", "data": "synthetic",
-            "config": {"workload": f"synth_mixed rows={args.rows}/rank prime={args.prime} "
-                                   f"seed={args.seed}+rank --O2 (metric circuit, SURVEY 8(d))",
-                       "constraints_per_rank": n_rows, "parallelism": f"shards{world}"},
-            "roofline": {"bound": "hbm", "kernel": k_name, "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "launches_per_step": k_launch / args.steps,
-                         "avg_launch_ms": round(per_launch_s * 1000.0, 4),
-                         "alg_bytes_per_launch": int(per_launch_bytes)},
-            "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in K.items()},
-            "phases_ms": {k: round(getattr(last, k), 2) for k in
-                          ("total_ms", "eq_ms", "cluster_ms", "elim_ms", "subst_ms", "final_ms")},
+            "config": {"workload": f"synth_mixed rows={args.rows} prime={args.prime} seed={args.seed} --O2 "
+                                   f"(metric circuit, SURVEY 8(d) config 5), host CSR -> host CSR + "
+                                   f"label_to_wire (T_simplify)" + (f", ONE circuit sharded over {world} ranks "
+                                                                    f"(RCCL exchange of the eliminated-signal map)"
+                                                                    if world > 1 else ""),
+                       "constraints": n_rows, "parallelism": f"clusters{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "kernel": k_name, "achieved": dom["achieved"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic"],
+                         "traffic_source": traffic_src, "avg_launch_ms": dom["avg_launch_ms"],
+                         "alg_bytes_per_launch": dom["alg_bytes_per_launch"],
+                         "launches_per_step": dom["launches_per_step"],
+                         "path": {"alg_bytes_per_step": int(tot["alg_bytes"] / K), "T_simplify_ms": round(ms_step, 3),
+                                  "achieved": round(path_ach, 2), "frac": round(path_ach / HBM_PEAK_GBS, 5)},
+                         "kernels": {k: kline(k) for k in acc}},
+            "phases_ms": {"device_run": round(tot["total_ms"] / K, 3), "h2d_wait": round(tot["h2d_wait_ms"] / K, 3),
+                          "d2h": round(tot["d2h_ms"] / K, 3), "host_total": round(tot["host_total_ms"] / K, 3)},
+            "last_step": {k: round(getattr(last, k), 2) for k in
+                          ("eq_ms", "cluster_ms", "elim_ms", "subst_ms", "final_ms", "rounds")},
+            "hbm_resident": {"value": round(n_rows * K / dt_hbm, 1), "unit": "constraints/s",
+                             "ms_per_step": round(dt_hbm * 1000.0 / K, 3),
+                             "what": "rs_engine_run: input already in HBM -> result in HBM (no PCIe)"},
         }
-        if sharded is not None:
-            line["sharded_one_circuit"] = sharded
+        if weak is not None:
+            line["weak_shards"] = weak
         if not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_rows, shard_seed(args.seed, 0), args.cpu_threads,
-                                                args.prime)
+            threads = args.cpu_threads or cpu_threads()
+            cb, ref = cpu_baseline(M, inp, threads, args.cpu_j1_rows, args.seed, args.prime)
+            line["cpu_baseline"] = cb
+            import rsio
+            diff = rsio.diff_output_arrays(got, ref)
+            line["bit_exact"] = diff is None
+            if diff is not None:
+                line["bit_exact_diff"] = diff
         else:
             line["cpu_baseline"] = None
+            line["bit_exact"] = None
         print(json.dumps(line), flush=True)
-    eng.close()
+    inp.free()
     if dist is not None:
         dist.destroy_process_group()
 

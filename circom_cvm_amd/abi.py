@@ -58,7 +58,12 @@ class RsStats(C.Structure):
                 ("big_main_bytes", C.c_uint64), ("big_finish_bytes", C.c_uint64), ("big_launches", C.c_uint64),
                 ("rounds", C.c_uint64), ("n_clusters", C.c_uint64),
                 ("n_substitutions", C.c_uint64), ("max_cluster", C.c_uint64),
-                ("exchange_ms", C.c_double), ("exchange_bytes", C.c_uint64), ("world", C.c_uint64)]
+                ("exchange_ms", C.c_double), ("exchange_bytes", C.c_uint64), ("world", C.c_uint64),
+                ("head_main_ms", C.c_double), ("head_main_bytes", C.c_uint64), ("head_launches", C.c_uint64),
+                ("tail_main_ms", C.c_double), ("tail_main_bytes", C.c_uint64), ("tail_launches", C.c_uint64),
+                ("round_fill_ms", C.c_double), ("round_fill_bytes", C.c_uint64),
+                ("round_fill_launches", C.c_uint64), ("alg_bytes", C.c_uint64), ("h2d_wait_ms", C.c_double),
+                ("d2h_ms", C.c_double), ("host_total_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -76,6 +81,10 @@ SYMBOLS = [
     ("rs_engine_fetch", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(RsOutput))]),
     ("rs_engine_stats", C.c_int, [C.c_void_p, C.POINTER(RsStats)]),
     ("rs_engine_destroy", None, [C.c_void_p]),
+    ("rs_engine_simplify", C.c_int, [C.c_void_p, C.POINTER(RsInput), C.POINTER(RsFlags),
+                                     C.POINTER(C.POINTER(RsOutput))]),
+    ("rs_host_alloc", C.c_void_p, [C.c_uint64]),
+    ("rs_host_free", None, [C.c_void_p]),
     ("rs_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("rs_engine_join_rccl", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     ("rs_group_create", C.c_void_p, [C.c_int]),
@@ -202,6 +211,13 @@ class Engine:
         check(lib().rs_engine_fetch(self._h, C.byref(out)))
         return Output(out)
 
+    def simplify(self, inp: RsInput, flags: RsFlags) -> RsOutput:
+        """rs_engine_simplify: host input -> host output (the SURVEY 8(d) T_simplify region).  The
+        returned struct views the engine's pinned buffers: valid until the next call on this engine."""
+        out = C.POINTER(RsOutput)()
+        check(lib().rs_engine_simplify(self._h, C.byref(inp), C.byref(flags), C.byref(out)))
+        return out.contents
+
     def close(self):
         if self._h:
             lib().rs_engine_destroy(self._h)
@@ -266,6 +282,49 @@ class Input:
         if self.ptr:
             lib().rs_input_free(self.ptr)
             self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class PinnedInput:
+    """A copy of an rs_input in page-locked host memory (rs_host_alloc), as a Rust shim marshalling
+    the Simplifier into library-provided buffers would hold it: rs_engine_simplify's H2D then runs at
+    PCIe speed."""
+
+    _BLOCKS = ("cons_eq", "eq", "linear", "nl_a", "nl_b", "nl_c")
+
+    def __init__(self, src: RsInput):
+        L = lib()
+        self._bufs = []
+        dst = RsInput()
+        C.memmove(C.byref(dst), C.byref(src), C.sizeof(RsInput))  # header + forbidden (borrowed from src)
+        for nm in self._BLOCKS:
+            b = getattr(src, nm)
+            n, nnz = int(b.n_rows), int(b.nnz)
+            ptr = self._copy(b.ptr, 8 * (n + 1) if n else 0, C.c_uint64)
+            col = self._copy(b.col, 4 * nnz, C.c_uint32)
+            val = self._copy(b.val, 32 * nnz, C.c_uint64)
+            setattr(dst, nm, RsLc(n, nnz, ptr, col, val))
+        self._src = src
+        self.c = dst
+
+    def _copy(self, src_ptr, nbytes, ctype):
+        p = lib().rs_host_alloc(max(nbytes, 8))
+        if not p:
+            raise RuntimeError("rs_host_alloc failed (no device?)")
+        self._bufs.append(p)
+        if nbytes:
+            C.memmove(p, src_ptr, nbytes)
+        return C.cast(p, C.POINTER(ctype))
+
+    def free(self):
+        for p in self._bufs:
+            lib().rs_host_free(p)
+        self._bufs = []
 
     def __del__(self):
         try:

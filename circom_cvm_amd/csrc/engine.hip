@@ -178,23 +178,131 @@ struct rs_engine {
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
+  // pipelined load (rs_engine_simplify): input groups 0 = cons_eq + eq, 1 = linear, 2 = non-linear
+  // land on the copy stream, each validated there; the run waits for a group where it first needs it
+  hipStream_t stc = nullptr;
+  hipEvent_t ev_grp[3] = {};
+  bool pending[3] = {false, false, false};
+  int *h_vflag = nullptr;  // pinned: per-group validation verdicts (D2H after each group's checks)
+  double h2d_wait_ms = 0;
+  // pinned result buffers of rs_engine_simplify (grow only) and the view handed out
+  struct Pin {
+    void *p = nullptr;
+    size_t cap = 0;
+  };
+  Pin pin[11];  // a/b/c: ptr, col, val; label_to_wire; spare
+  rs_output view{};
 };
 
 namespace rs {
 
+// H2D of one CSR block on the copy stream.  The row pointers are not trusted: the block's
+// validation (k_check_ptr) checks ptr[0] = 0, monotonicity and ptr[n] = nnz on the device before
+// anything reads a row.
 static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, const char *name) {
+  if (src.n_rows && !src.ptr) throw RsError(RS_E_INVALID, std::string(name) + ": rows without a ptr array");
+  if (src.nnz && (!src.col || !src.val)) throw RsError(RS_E_INVALID, std::string(name) + ": entries without col/val");
+  if (src.n_rows > 0xfffffff0ull || src.nnz > (1ull << 40)) throw RsError(RS_E_INVALID, std::string(name) + ": block too large");
   dst.n = src.n_rows;
-  dst.nnz = src.n_rows ? src.ptr[src.n_rows] : 0;
+  dst.nnz = src.n_rows ? src.nnz : 0;
   std::string nm(name);
   dst.ptr = E->A.get<uint64_t>(nm + ".ptr", dst.n + 1);
   dst.key = E->A.get<uint32_t>(nm + ".key", dst.nnz);
   dst.val = E->A.get<Fe>(nm + ".val", dst.nnz);
-  if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, E->st));
-  else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), E->st));
+  hipStream_t s = E->stc;
+  if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, s));
+  else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), s));
   if (dst.nnz) {
-    HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, E->st));
-    HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, E->st));
+    HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, s));
+    HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, s));
   }
+}
+
+// ---------------------------------------------------------------- pipelined load
+static const char *kGroupName[3] = {"cons_eq/eq", "linear", "non-linear"};
+
+// Validates the header fields of `in` and enqueues the H2D of every block on the copy stream in
+// the order the run consumes them -- group 0 (cons_eq, eq), 1 (linear), 2 (nl_a, nl_b, nl_c) --
+// each group followed by its device checks (k_check_ptr, then k_sort_validate, which also sorts
+// the rows) and the D2H of its two verdict words into pinned memory.
+static void load_enqueue(rs_engine *E, const rs_input *in) {
+  uint64_t p[4];
+  if (!prime_of(in, p)) throw RsError(RS_E_INVALID, "unknown prime");
+  if (in->max_signal == 0 || in->max_signal > 0xfffffff0ull) throw RsError(RS_E_INVALID, "bad max_signal");
+  if (in->n_forbidden && !in->forbidden) throw RsError(RS_E_INVALID, "forbidden list missing");
+  std::vector<uint32_t> forb(in->forbidden, in->forbidden + in->n_forbidden);
+  bool has0 = false;
+  for (uint32_t f : forb) {
+    if (f >= in->max_signal) throw RsError(RS_E_INVALID, "forbidden signal out of range");
+    has0 |= f == 0;
+  }
+  if (!has0) throw RsError(RS_E_INVALID, "signal 0 must be forbidden");
+  if (in->nl_a.n_rows != in->nl_b.n_rows || in->nl_a.n_rows != in->nl_c.n_rows)
+    throw RsError(RS_E_INVALID, "non-linear blocks differ in row count");
+  HC(hipStreamSynchronize(E->stc));  // the previous call's copies are complete
+  E->loaded = false;
+  E->have_result = false;
+  for (bool &pd : E->pending) pd = false;
+  memcpy(E->prime, p, 32);
+  E->prime_id = in->prime_id;
+  E->F = make_field(p);
+  E->S = in->max_signal;
+  E->n_pub_out = in->n_pub_out;
+  E->n_pub_in = in->n_pub_in;
+  E->n_priv_in = in->n_priv_in;
+  E->forbidden.swap(forb);
+  E->h2d_wait_ms = 0;
+  int *vf = E->A.get<int>("vflag", 6);  // [2g]: row pointers of group g, [2g + 1]: its rows
+  HC(hipMemsetAsync(vf, 0, 24, E->stc));
+  struct G {
+    const rs_lc *src;
+    rs_engine::Blk *dst;
+    const char *nm;
+  };
+  const G groups[3][3] = {{{&in->cons_eq, &E->ce, "in.ce"}, {&in->eq, &E->eq, "in.eq"}, {nullptr, nullptr, nullptr}},
+                          {{&in->linear, &E->lin, "in.lin"}, {nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}},
+                          {{&in->nl_a, &E->na, "in.na"}, {&in->nl_b, &E->nb, "in.nb"}, {&in->nl_c, &E->nc, "in.nc"}}};
+  for (int g = 0; g < 3; ++g) {
+    for (const G &x : groups[g])
+      if (x.src) upload_block(E, *x.src, *x.dst, x.nm);
+    for (const G &x : groups[g])
+      if (x.src) launch(E->stc, k_check_ptr, x.dst->n + 1, (const uint64_t *)x.dst->ptr, x.dst->n, x.dst->nnz, vf + 2 * g);
+    for (const G &x : groups[g])
+      if (x.src && x.dst->n)
+        launch(E->stc, k_sort_validate, x.dst->n, E->F, (const uint64_t *)x.dst->ptr, x.dst->key, x.dst->val, x.dst->n, E->S,
+               (const int *)(vf + 2 * g), vf + 2 * g + 1);
+    HC(hipMemcpyAsync(E->h_vflag + 2 * g, vf + 2 * g, 8, hipMemcpyDeviceToHost, E->stc));
+    HC(hipEventRecord(E->ev_grp[g], E->stc));
+    E->pending[g] = true;
+  }
+  E->loaded = true;
+}
+
+// Blocks until input group g has landed and passed its checks; the main stream is ordered after it.
+static void load_wait(rs_engine *E, int g) {
+  if (!E->pending[g]) return;
+  const double t0 = now_ms();
+  HC(hipEventSynchronize(E->ev_grp[g]));
+  E->pending[g] = false;
+  E->h2d_wait_ms += now_ms() - t0;
+  if (E->h_vflag[2 * g]) {
+    E->loaded = false;
+    throw RsError(RS_E_INVALID, std::string(kGroupName[g]) + " block: bad row pointers (ptr[0] != 0, decreasing, or ptr[n_rows] != nnz)");
+  }
+  if (E->h_vflag[2 * g + 1]) {
+    E->loaded = false;
+    throw RsError(RS_E_INVALID, std::string(kGroupName[g]) +
+                                    " block: invalid rows (duplicate key, zero or non-canonical value, signal >= max_signal)");
+  }
+  HC(hipStreamWaitEvent(E->st, E->ev_grp[g], 0));
+}
+static void load_wait_all(rs_engine *E) {
+  for (int g = 0; g < 3; ++g) load_wait(E, g);
+}
+// After a failed call: the copy stream may still be reading the caller's buffers.
+static void load_abort(rs_engine *E) {
+  if (E->stc) (void)hipStreamSynchronize(E->stc);
+  for (bool &pd : E->pending) pd = false;
 }
 
 // H2D copy whose host buffer may be released right after the call: wait for it.
@@ -615,8 +723,15 @@ struct DevClusters {
 };
 // the number of largest clusters eliminated on the second stream (RS_HEAD overrides)
 static uint64_t head_limit() {
-  const char *hd = getenv("RS_HEAD");
-  return hd ? (uint64_t)atoi(hd) : 16;
+  static const uint64_t v = [] {
+    const char *hd = getenv("RS_HEAD");
+    if (!hd || !*hd) return (uint64_t)16;
+    char *end = nullptr;
+    const unsigned long long x = strtoull(hd, &end, 10);
+    if (*end || hd[0] == '-') return (uint64_t)16;  // not a plain count: the default
+    return (uint64_t)std::min<unsigned long long>(x, 4096);
+  }();
+  return v;
 }
 static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, const uint8_t *d_forb, ElimOut &eo) {
   Arena &A = E->A;
@@ -857,7 +972,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.pool_top = P.top;
     a.pool_cap = P.cap;
     a.err = d_err;
-    a.bytes = E->A.get<unsigned long long>("el.bytes", 3);
+    // in-kernel algorithmic-byte counters: [0] k_eliminate / composition emits, [1] / [2] the head's
+    // k_big_main / normalisation + composition, [3] / [4] the tail's
+    a.bytes = E->A.get<unsigned long long>("el.bytes", 5);
     a.big_touch_off = E->A.get<uint64_t>("el.bt_off", std::max<uint64_t>(n_big, 1));
     a.big_touch_n = E->A.get<uint32_t>("el.bt_n", std::max<uint64_t>(n_big, 1));
     a.big_alive = E->A.get<uint32_t>("el.alive", std::max<uint64_t>(n_big, 1));
@@ -867,13 +984,15 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", kProfWords * n_big) : nullptr;
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
-    HC(hipMemsetAsync(a.bytes, 0, 24, E->st));
+    HC(hipMemsetAsync(a.bytes, 0, 40, E->st));
     // The largest clusters' prep -> main -> finish chain runs on a second stream: the elimination
     // time is the critical path of the largest cluster, and everything else overlaps it.
     const uint64_t n_head = std::min<uint64_t>(n_big, head_limit()), n_tail = n_big - n_head;
     a.wide = 1;       // the head's largest process_4 clusters go through the k_wide_* grid
     ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
     at.wide = 0;
+    at.bytes_main = a.bytes + 3;
+    at.bytes_fin = a.bytes + 4;
     at.big_touch_off += n_head;
     at.big_touch_n += n_head;
     at.big_alive += n_head;
@@ -1027,14 +1146,16 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipEventElapsedTime(&msm, E->ev4, E->evx[5]));
       E->stats.elim_big_ms += ms - msm;  // wall of the workgroup kernels (both streams)
       E->stats.elim_small_ms += msm;
-      unsigned long long b3[3] = {0, 0, 0};
-      HC(hipMemcpy(b3, a.bytes, 24, hipMemcpyDeviceToHost));
-      by = b3[0];
+      unsigned long long b5[5] = {0, 0, 0, 0, 0};
+      HC(hipMemcpy(b5, a.bytes, 40, hipMemcpyDeviceToHost));
+      by = b5[0];
       E->stats.elim_kernel_ms += ms;
       E->stats.elim_kernel_launches++;
       E->stats.elim_bytes += by;
-      E->stats.big_main_bytes += b3[1];
-      E->stats.big_finish_bytes += b3[2];
+      E->stats.big_main_bytes += b5[1] + b5[3];
+      E->stats.big_finish_bytes += b5[2] + b5[4];
+      E->stats.head_main_bytes += b5[1];
+      E->stats.tail_main_bytes += b5[3];
       if (n_tail) {
         float m0 = 0, m1 = 0, m2 = 0;
         HC(hipEventElapsedTime(&m0, E->ev2, E->ev5));
@@ -1044,6 +1165,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.big_main_ms += m1;
         E->stats.big_finish_ms += m2;
         E->stats.big_launches++;
+        E->stats.tail_main_ms += m1;
+        E->stats.tail_launches++;
       }
       if (g_prof_env) {
         float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
@@ -1072,6 +1195,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.big_main_ms += m1;
         E->stats.big_finish_ms += m2;
         E->stats.big_launches++;
+        E->stats.head_main_ms += m1;
+        E->stats.head_launches++;
       }
     }
     if (a.prof) {
@@ -1308,6 +1433,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   E->log_ptr.assign(1, 0);
 
   // ======================= eq_simplification (:198-251) + renaming of linear / cons_eq rows
+  load_wait(E, 0);
   int32_t *eq_rep = A.get<int32_t>("eq_rep", S);
   HC(hipMemsetAsync(eq_rep, 0xff, 4 * S, st));
   {
@@ -1426,6 +1552,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   }
 
   // working copies (Montgomery): cons_eq (C), linear (C, one spare slot per row)
+  load_wait(E, 1);
   DRows ce{}, lin{};
   ce.n = E->ce.n;
   ce.off = A.get<uint64_t>("ce.off", ce.n);
@@ -1511,9 +1638,17 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (R.n) launch(st, k_make_ragged, R.n, E->F, (const uint64_t *)B.ptr, (const uint32_t *)B.key, (const Fe *)B.val, R.n,
                     (uint64_t)0, R.off, R.len, R.key, R.val);
   };
-  mk_in(E->na, ia, "nla");
-  mk_in(E->nb, ib, "nlb");
-  mk_in(E->nc, ic, "nlc");
+  // the non-linear blocks are staged where the frames first need them: their upload (group 2)
+  // overlaps the clustering and elimination
+  bool nl_staged = false;
+  auto stage_nl = [&]() {
+    if (nl_staged) return;
+    load_wait(E, 2);
+    mk_in(E->na, ia, "nla");
+    mk_in(E->nb, ib, "nlb");
+    mk_in(E->nc, ic, "nlc");
+    nl_staged = true;
+  };
   // storage rows live in one growable heap of (key, value) entries, owned by the engine
   DRows sa{}, sb{}, sc{};
   uint64_t heap_top = 0;
@@ -1568,6 +1703,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   // one pass of the frames over the non-linear rows ids[0, n) (phase: see NLArgs); the fill's
   // kernel time is read from (e0, e1) once the caller synchronises
   auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1) {
+    stage_nl();
     NLArgs a;
     a.fr = fr;
     a.a = ia; a.b = ib; a.c = ic;
@@ -1883,7 +2019,22 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           HC(hipMemsetAsync(ra.turn, 0xff, 4 * n_st, st));
           HC(hipMemsetAsync(ra.touched, 0, n_st, st));
         }
-        if (ra.n_ids) launch(st, k_round_fill, ra.n_ids, ra);
+        ra.bytes = A.get<unsigned long long>("r.bytes", 1);
+        HC(hipMemsetAsync(ra.bytes, 0, 8, st));
+        if (ra.n_ids) {
+          HC(hipEventRecord(E->ev0, st));
+          launch(st, k_round_fill, ra.n_ids, ra);
+          HC(hipEventRecord(E->ev1, st));
+          float fm = 0;
+          unsigned long long fb = 0;
+          HC(hipMemcpyAsync(&fb, ra.bytes, 8, hipMemcpyDeviceToHost, st));
+          HC(hipEventSynchronize(E->ev1));
+          HC(hipStreamSynchronize(st));
+          HC(hipEventElapsedTime(&fm, E->ev0, E->ev1));
+          E->stats.round_fill_ms += fm;
+          E->stats.round_fill_bytes += fb;
+          E->stats.round_fill_launches++;
+        }
         MK.mark("fill");
         if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qt);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
@@ -2118,12 +2269,27 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
     E->out_host_tail = std::move(lconst);
   }
+  load_wait_all(E);  // a group the path never needed (e.g. no non-linear rows) is still checked
   int err = 0;
   HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
   if (err) throw RsError(RS_E_INVALID, "input rejected by the device checks (code " + std::to_string(err) + ")");
   E->stats.final_ms = now_ms() - Tf;
   E->stats.total_ms = now_ms() - T0;
+  E->stats.h2d_wait_ms = E->h2d_wait_ms;
+  {  // B_alg: the in-kernel counters + input / output entries and rows + the label map
+    const uint64_t z_in = E->ce.nnz + E->eq.nnz + E->lin.nnz + E->na.nnz + E->nb.nnz + E->nc.nnz;
+    const uint64_t r_in = E->ce.n + E->eq.n + E->lin.n + E->na.n;
+    uint64_t z_out = E->out_nnz[0] + E->out_nnz[1] + E->out_nnz[2], r_out = E->out_n_dev;
+    for (auto &c : E->out_host_tail) {
+      const uint64_t m = c.k[0].size() + c.k[1].size() + c.k[2].size();
+      z_out += m;
+      r_out += m ? 1 : 0;
+    }
+    const rs_stats &s = E->stats;
+    E->stats.alg_bytes = s.elim_bytes + s.big_main_bytes + s.big_finish_bytes + s.apply_bytes + s.round_fill_bytes +
+                         36 * (z_in + z_out) + 8 * (r_in + r_out) + 8 * S;
+  }
   E->have_result = true;
 }
 
@@ -2154,7 +2320,11 @@ int rs_engine_create(int device, rs_engine **eng) {
     E->device = device;
     HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));
+    for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HC(hipHostMalloc((void **)&E->h_vflag, 6 * sizeof(int), hipHostMallocDefault));
+    memset(E->h_vflag, 0, 6 * sizeof(int));
     HC(hipEventCreate(&E->ev0));
     HC(hipEventCreate(&E->ev1));
     HC(hipEventCreate(&E->ev2));
@@ -2177,7 +2347,15 @@ void rs_engine_destroy(rs_engine *E) {
   if (!E) return;
   (void)hipSetDevice(E->device);
   if (E->st) (void)hipStreamSynchronize(E->st);
+  if (E->st2) (void)hipStreamSynchronize(E->st2);
+  if (E->stc) (void)hipStreamSynchronize(E->stc);
   E->comm.reset();
+  for (auto &pb : E->pin)
+    if (pb.p) (void)hipHostFree(pb.p);
+  if (E->h_vflag) (void)hipHostFree(E->h_vflag);
+  for (auto &ev : E->ev_grp)
+    if (ev) (void)hipEventDestroy(ev);
+  if (E->stc) (void)hipStreamDestroy(E->stc);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
   if (E->ev2) (void)hipEventDestroy(E->ev2);
@@ -2197,48 +2375,17 @@ void rs_engine_destroy(rs_engine *E) {
 int rs_engine_load(rs_engine *E, const rs_input *in) {
   try {
     HC(hipSetDevice(E->device));
-    uint64_t p[4];
-    if (!prime_of(in, p)) { set_error("unknown prime"); return RS_E_INVALID; }
-    if (in->max_signal == 0 || in->max_signal > 0xfffffff0ull) { set_error("bad max_signal"); return RS_E_INVALID; }
-    memcpy(E->prime, p, 32);
-    E->prime_id = in->prime_id;
-    E->F = make_field(p);
-    E->S = in->max_signal;
-    E->n_pub_out = in->n_pub_out;
-    E->n_pub_in = in->n_pub_in;
-    E->n_priv_in = in->n_priv_in;
-    E->forbidden.assign(in->forbidden, in->forbidden + in->n_forbidden);
-    bool has0 = false;
-    for (uint32_t f : E->forbidden) {
-      if (f >= E->S) { set_error("forbidden signal out of range"); return RS_E_INVALID; }
-      has0 |= f == 0;
-    }
-    if (!has0) { set_error("signal 0 must be forbidden"); return RS_E_INVALID; }
-    if (in->nl_a.n_rows != in->nl_b.n_rows || in->nl_a.n_rows != in->nl_c.n_rows) {
-      set_error("non-linear blocks differ in row count");
-      return RS_E_INVALID;
-    }
-    upload_block(E, in->cons_eq, E->ce, "in.ce");
-    upload_block(E, in->eq, E->eq, "in.eq");
-    upload_block(E, in->linear, E->lin, "in.lin");
-    upload_block(E, in->nl_a, E->na, "in.na");
-    upload_block(E, in->nl_b, E->nb, "in.nb");
-    upload_block(E, in->nl_c, E->nc, "in.nc");
-    int *d_err = E->A.get<int>("err", 1);
-    HC(hipMemsetAsync(d_err, 0, 4, E->st));
-    for (rs_engine::Blk *B : {&E->ce, &E->eq, &E->lin, &E->na, &E->nb, &E->nc})
-      if (B->n) launch(E->st, k_sort_validate, B->n, E->F, (const uint64_t *)B->ptr, B->key, B->val, B->n, E->S, d_err);
-    int err = 0;
-    HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
-    HC(hipStreamSynchronize(E->st));
-    if (err) { set_error("invalid input rows (duplicate key, zero or non-canonical value, signal >= max_signal)"); return RS_E_INVALID; }
-    E->loaded = true;
-    E->have_result = false;
+    load_enqueue(E, in);
+    load_wait_all(E);
     return RS_OK;
   } catch (const RsError &e) {
+    load_abort(E);
+    E->loaded = false;
     set_error(e.what());
     return e.code;
   } catch (const std::exception &e) {
+    load_abort(E);
+    E->loaded = false;
     set_error(e.what());
     return RS_E_INTERNAL;
   }
@@ -2264,60 +2411,69 @@ int rs_engine_stats(rs_engine *E, rs_stats *s) {
   return RS_OK;
 }
 
-int rs_engine_fetch(rs_engine *E, rs_output **out) {
-  try {
-    if (!E->have_result) { set_error("no result"); return RS_E_INVALID; }
-    HC(hipSetDevice(E->device));
-    rs_output *o = (rs_output *)calloc(1, sizeof(rs_output));
-    uint64_t nd = E->out_n_dev, nh = E->out_host_tail.size();
-    // count non-empty host rows (lconst after fix may be empty: extract_with removes them)
-    std::vector<const HostCon *> hrows;
-    for (auto &c : E->out_host_tail)
-      if (!(c.k[0].empty() && c.k[1].empty() && c.k[2].empty())) hrows.push_back(&c);
-    nh = hrows.size();
-    o->n_constraints = nd + nh;
-    const char *nm[3] = {"out.a", "out.b", "out.c"};
-    rs_lc *dst[3] = {&o->a, &o->b, &o->c};
-    for (int q = 0; q < 3; ++q) {
-      uint64_t hn = 0;
-      for (auto *c : hrows) hn += c->k[q].size();
-      uint64_t tot = E->out_nnz[q] + hn;
-      rs_lc &L = *dst[q];
-      L.n_rows = nd + nh;
-      L.nnz = tot;
-      L.ptr = (uint64_t *)malloc(8 * (nd + nh + 1));
-      L.col = (uint32_t *)malloc(4 * (tot ? tot : 1));
-      L.val = (uint64_t *)malloc(32 * (tot ? tot : 1));
-      if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
-      else L.ptr[0] = 0;
-      if (E->out_nnz[q]) {
-        HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(std::string(nm[q]) + ".col", 1), 4 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
-        HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(std::string(nm[q]) + ".val", 1), 32 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
-      }
-      HC(hipStreamSynchronize(E->st));
-      uint64_t e = E->out_nnz[q];
-      for (uint64_t i = 0; i < nh; ++i) {
-        const HostCon &c = *hrows[i];
-        for (size_t t = 0; t < c.k[q].size(); ++t) {
-          L.col[e] = c.k[q][t];
-          memcpy(L.val + 4 * e, &c.v[q][4 * t], 32);
-          ++e;
-        }
-        L.ptr[nd + i + 1] = e;
-      }
+namespace rs {
+// The result in host memory.  buf(slot, bytes) supplies the destination of each array -- slots
+// 0-2 ptr of a/b/c, 3-5 col, 6-8 val, 9 label_to_wire -- (malloc for rs_engine_fetch, the engine's
+// pinned buffers for rs_engine_simplify).  Every D2H is enqueued first and waited for once; the
+// host-side lconst rows are then appended after the device rows.  The substitution log is copied
+// (own = true) or pointed at (the engine's vectors, rs_engine_simplify's view).
+static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(int, size_t)> &buf, bool own_log) {
+  const uint64_t nd = E->out_n_dev;
+  // non-empty host rows (lconst after fix may be empty: extract_with removes them)
+  std::vector<const HostCon *> hrows;
+  for (auto &c : E->out_host_tail)
+    if (!(c.k[0].empty() && c.k[1].empty() && c.k[2].empty())) hrows.push_back(&c);
+  const uint64_t nh = hrows.size();
+  o->n_constraints = nd + nh;
+  const char *nm[3] = {"out.a", "out.b", "out.c"};
+  rs_lc *dst[3] = {&o->a, &o->b, &o->c};
+  for (int q = 0; q < 3; ++q) {
+    uint64_t hn = 0;
+    for (auto *c : hrows) hn += c->k[q].size();
+    const uint64_t tot = E->out_nnz[q] + hn;
+    rs_lc &L = *dst[q];
+    L.n_rows = nd + nh;
+    L.nnz = tot;
+    L.ptr = (uint64_t *)buf(q, 8 * (nd + nh + 1));
+    L.col = (uint32_t *)buf(3 + q, 4 * (tot ? tot : 1));
+    L.val = (uint64_t *)buf(6 + q, 32 * (tot ? tot : 1));
+    if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
+    else L.ptr[0] = 0;
+    if (E->out_nnz[q]) {
+      HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(std::string(nm[q]) + ".col", 1), 4 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+      HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(std::string(nm[q]) + ".val", 1), 32 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
     }
-    o->n_labels = E->S;
-    o->label_to_wire = (int64_t *)malloc(8 * E->S);
-    HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int64_t>("fin.l2w", 1), 8 * E->S, hipMemcpyDeviceToHost, E->st));
-    HC(hipStreamSynchronize(E->st));
-    o->n_wires = E->n_wires;
-    o->no_private_inputs_witness = E->npiw;
-    if (E->log_on) {
-      const uint64_t n = E->log_from.size(), nnz = E->log_key.size();
-      o->n_log = n;
+  }
+  o->n_labels = E->S;
+  o->label_to_wire = (int64_t *)buf(9, 8 * E->S);
+  HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int64_t>("fin.l2w", 1), 8 * E->S, hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+  for (int q = 0; q < 3; ++q) {
+    rs_lc &L = *dst[q];
+    uint64_t e = E->out_nnz[q];
+    for (uint64_t i = 0; i < nh; ++i) {
+      const HostCon &c = *hrows[i];
+      const size_t m = c.k[q].size();
+      if (m) {
+        memcpy(L.col + e, c.k[q].data(), 4 * m);
+        memcpy(L.val + 4 * e, c.v[q].data(), 32 * m);
+      }
+      e += m;
+      L.ptr[nd + i + 1] = e;
+    }
+  }
+  o->n_wires = E->n_wires;
+  o->no_private_inputs_witness = E->npiw;
+  o->n_log = 0;
+  o->log_from = nullptr;
+  o->log_to = rs_lc{};
+  if (E->log_on) {
+    const uint64_t n = E->log_from.size(), nnz = E->log_key.size();
+    o->n_log = n;
+    o->log_to.n_rows = n;
+    o->log_to.nnz = nnz;
+    if (own_log) {
       o->log_from = (uint32_t *)malloc(4 * (n ? n : 1));
-      o->log_to.n_rows = n;
-      o->log_to.nnz = nnz;
       o->log_to.ptr = (uint64_t *)malloc(8 * (n + 1));
       o->log_to.col = (uint32_t *)malloc(4 * (nnz ? nnz : 1));
       o->log_to.val = (uint64_t *)malloc(32 * (nnz ? nnz : 1));
@@ -2327,6 +2483,39 @@ int rs_engine_fetch(rs_engine *E, rs_output **out) {
         memcpy(o->log_to.col, E->log_key.data(), 4 * nnz);
         memcpy(o->log_to.val, E->log_val.data(), 32 * nnz);
       }
+    } else {
+      o->log_from = E->log_from.data();
+      o->log_to.ptr = E->log_ptr.data();
+      o->log_to.col = E->log_key.data();
+      o->log_to.val = E->log_val.data();
+    }
+  }
+}
+
+static void *pin_get(rs_engine *E, int slot, size_t bytes) {
+  rs_engine::Pin &b = E->pin[slot];
+  if (b.cap < bytes) {
+    const size_t cap = std::max(bytes, b.cap + b.cap / 4);
+    if (b.p) HC(hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    HC(hipHostMalloc(&b.p, cap, hipHostMallocDefault));
+    b.cap = cap;
+  }
+  return b.p;
+}
+}  // namespace rs
+
+int rs_engine_fetch(rs_engine *E, rs_output **out) {
+  try {
+    if (!E->have_result) { set_error("no result"); return RS_E_INVALID; }
+    HC(hipSetDevice(E->device));
+    rs_output *o = (rs_output *)calloc(1, sizeof(rs_output));
+    try {
+      fetch_result(E, o, [](int, size_t bytes) { void *p = malloc(bytes ? bytes : 1); if (!p) throw std::bad_alloc(); return p; }, true);
+    } catch (...) {
+      rs_output_free(o);
+      throw;
     }
     *out = o;
     return RS_OK;
@@ -2337,6 +2526,42 @@ int rs_engine_fetch(rs_engine *E, rs_output **out) {
     set_error(e.what());
     return RS_E_INTERNAL;
   }
+}
+
+int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, const rs_output **out) {
+  try {
+    const double t0 = now_ms();
+    HC(hipSetDevice(E->device));
+    load_enqueue(E, in);
+    engine_run(E, fl);
+    const double t1 = now_ms();
+    E->view = rs_output{};
+    fetch_result(E, &E->view, [E](int slot, size_t bytes) { return pin_get(E, slot, bytes); }, false);
+    const double t2 = now_ms();
+    E->stats.d2h_ms = t2 - t1;
+    E->stats.host_total_ms = t2 - t0;
+    *out = &E->view;
+    return RS_OK;
+  } catch (const RsError &e) {
+    load_abort(E);
+    E->loaded = false;
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    load_abort(E);
+    E->loaded = false;
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+void *rs_host_alloc(uint64_t bytes) {
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+void rs_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
 }
 
 void rs_output_free(rs_output *o) {

@@ -97,21 +97,59 @@ __device__ inline void d_fix(const FieldP &F, uint32_t *ak, Fe *av, uint32_t &an
 }
 
 // ---------------------------------------------------------------- load / convert / validate
-// Sorts every row by key and validates it (distinct keys < S, canonical nonzero values).
+// Row pointers of an uploaded block: ptr[0] = 0, non-decreasing, ptr[n] = nnz.  Runs before any
+// kernel reads a row of the block (a decreasing ptr would make a row length wrap).
+__global__ void k_check_ptr(const uint64_t *ptr, uint64_t n, uint64_t nnz, int *flag) {
+  for (uint64_t r = gtid(); r <= n; r += gstride()) {
+    const uint64_t v = ptr[r];
+    bool bad = r == 0 ? v != 0 : v < ptr[r - 1];
+    if (r == n) bad |= v != nnz;
+    if (bad) atomicOr(flag, 1);
+  }
+}
+// heap sort of (key, value) pairs by key (rows too long for an insertion sort)
+__device__ inline void d_heap_sort_pairs(uint32_t *k, Fe *v, uint32_t n) {
+  auto sift = [&](uint32_t i, uint32_t m) {
+    for (;;) {
+      uint32_t c = 2 * i + 1;
+      if (c >= m) return;
+      if (c + 1 < m && k[c + 1] > k[c]) ++c;
+      if (k[i] >= k[c]) return;
+      uint32_t tk = k[i]; k[i] = k[c]; k[c] = tk;
+      Fe tv = v[i]; v[i] = v[c]; v[c] = tv;
+      i = c;
+    }
+  };
+  for (uint32_t i = n / 2; i-- > 0;) sift(i, n);
+  for (uint32_t m = n; m-- > 1;) {
+    uint32_t tk = k[0]; k[0] = k[m]; k[m] = tk;
+    Fe tv = v[0]; v[0] = v[m]; v[m] = tv;
+    sift(0, m);
+  }
+}
+// Sorts every row by key and validates it (distinct keys < S, canonical nonzero values).  Skipped
+// when the block's row pointers failed k_check_ptr (`ptr_bad`, stream-ordered before this kernel).
 __global__ void k_sort_validate(FieldP F, const uint64_t *ptr, uint32_t *key, Fe *val, uint64_t n,
-                                uint64_t S, int *err) {
+                                uint64_t S, const int *ptr_bad, int *err) {
+  if (*ptr_bad) return;
   for (uint64_t r = gtid(); r < n; r += gstride()) {
     uint64_t b = ptr[r], e = ptr[r + 1];
     uint32_t *k = key + b;
     Fe *v = val + b;
     uint32_t m = (uint32_t)(e - b);
-    for (uint32_t i = 1; i < m; ++i) {
-      uint32_t kk = k[i];
-      Fe vv = v[i];
-      uint32_t j = i;
-      while (j > 0 && k[j - 1] > kk) { k[j] = k[j - 1]; v[j] = v[j - 1]; --j; }
-      k[j] = kk;
-      v[j] = vv;
+    bool sorted = true;
+    for (uint32_t i = 1; i < m && sorted; ++i) sorted = k[i - 1] < k[i];
+    if (!sorted && m <= 32) {
+      for (uint32_t i = 1; i < m; ++i) {
+        uint32_t kk = k[i];
+        Fe vv = v[i];
+        uint32_t j = i;
+        while (j > 0 && k[j - 1] > kk) { k[j] = k[j - 1]; v[j] = v[j - 1]; --j; }
+        k[j] = kk;
+        v[j] = vv;
+      }
+    } else if (!sorted) {
+      d_heap_sort_pairs(k, v, m);
     }
     for (uint32_t i = 0; i < m; ++i) {
       if (k[i] >= S || (i > 0 && k[i] == k[i - 1]) || fe_is_zero(v[i]) || geq4(v[i].l, F.p)) atomicOr(err, 1);
@@ -2441,6 +2479,7 @@ struct RoundArgs {
   uint64_t c_base;
   const uint32_t *ids;     // the rows a substitution touches (cap_c != 0), compacted
   uint64_t n_ids;
+  unsigned long long *bytes;  // algorithmic bytes: 36 per entry read (row + right-hand sides) or written
 };
 __global__ void k_touch_flags(const uint64_t *cap_c, uint64_t n, uint64_t *flag) {
   for (uint64_t r = gtid(); r < n; r += gstride()) flag[r] = cap_c[r] != 0;
@@ -2467,6 +2506,7 @@ __device__ __forceinline__ bool d_const_or_empty(const uint32_t *k, uint32_t n) 
 // turn = -1 and touched = 0 were set for every row beforehand).
 __global__ void k_round_fill(RoundArgs A) {
   const FieldP &F = A.F;
+  unsigned long long bytes = 0;
   for (uint64_t i = gtid(); i < A.n_ids; i += gstride()) {
     const uint64_t r = A.ids[i];
     A.touched[r] = 1;
@@ -2558,7 +2598,11 @@ __global__ void k_round_fill(RoundArgs A) {
     A.oa.len[r] = na;
     A.ob.len[r] = nb;
     A.oc.len[r] = nc;
+    // read: the row and, per entry, its right-hand side (the capacity bound minus the staging slots)
+    bytes += 36ull * ((capa - 1) + (capb - 1) + (cc - 1) - A.a.len[r] - A.b.len[r] - A.c.len[r]) +
+             36ull * (na + nb + nc);
   }
+  wave_atomic_add(A.bytes, bytes);
 }
 
 // ---------------------------------------------------------------- final assembly

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 3
+#define RS_ABI_VERSION 4
 
 enum rs_status {
   RS_OK = 0,
@@ -159,6 +159,24 @@ typedef struct rs_stats {
   double exchange_ms;          /* sharded runs: the eliminated-signal-map exchange (all rounds) */
   uint64_t exchange_bytes;     /* bytes each rank received + contributed in those collectives  */
   uint64_t world;              /* ranks the elimination was sharded over (1 = single GPU)       */
+  /* ABI 4: the ordered elimination loop split into the head (the largest clusters, one launch
+   * on the second stream, the critical path) and the tail (every other workgroup cluster), each
+   * with its own HIP-event time and in-kernel algorithmic bytes; the storage-row kernel of
+   * rounds >= 2; the host -> host legs of rs_engine_simplify. */
+  double head_main_ms;         /* k_big_main<512> (head)                                     */
+  uint64_t head_main_bytes;
+  uint64_t head_launches;
+  double tail_main_ms;         /* k_big_main<256> (tail)                                     */
+  uint64_t tail_main_bytes;
+  uint64_t tail_launches;
+  double round_fill_ms;        /* k_round_fill (apply_substitution_to_map, rounds >= 2)      */
+  uint64_t round_fill_bytes;
+  uint64_t round_fill_launches;
+  uint64_t alg_bytes;          /* B_alg of the run: every in-kernel counter +
+                                  36 (Z_in + Z_out) + 8 (R_in + R_out) + 8 max_signal       */
+  double h2d_wait_ms;          /* host time the run spent waiting for input groups to land  */
+  double d2h_ms;               /* D2H of the result into the engine's pinned buffers        */
+  double host_total_ms;        /* rs_engine_simplify: host input -> host output             */
 } rs_stats;
 
 typedef struct rs_engine rs_engine;
@@ -177,6 +195,24 @@ int rs_engine_run(rs_engine *eng, const rs_flags *fl);    /* the timed region   
 int rs_engine_fetch(rs_engine *eng, rs_output **out);     /* D2H of the last result             */
 int rs_engine_stats(rs_engine *eng, rs_stats *st);
 void rs_engine_destroy(rs_engine *eng);
+
+/*
+ * Host -> host on a persistent engine: the whole of simplification() (constraint_simplification.rs
+ * :442-730) from the host CSR blocks to the host result, the SURVEY 8(d) T_simplify region.
+ * The H2D copy of `in` runs on a copy stream in three groups (cons_eq + eq, linear, non-linear),
+ * each validated on the device as it lands, and the simplification consumes a group as soon as it
+ * is there, so the upload of the later groups overlaps the eq / clustering / elimination phases.
+ * The result is copied into pinned buffers the engine owns; *out points at them and stays valid
+ * until the next call on `eng` or rs_engine_destroy (do not rs_output_free it).  `in` is read
+ * only during the call.  Host buffers from rs_host_alloc move at full PCIe speed; pageable ones
+ * work too (HIP stages them), slower.
+ */
+int rs_engine_simplify(rs_engine *eng, const rs_input *in, const rs_flags *fl, const rs_output **out);
+
+/* Page-locked host memory (hipHostMalloc) for the CSR blocks a caller marshals the Simplifier into,
+ * so rs_engine_simplify's H2D runs at PCIe speed.  NULL without a device. */
+void *rs_host_alloc(uint64_t bytes);
+void rs_host_free(void *p);
 
 /*
  * Multi-GPU: ONE circuit sharded over W ranks.  Every rank loads the same input;
