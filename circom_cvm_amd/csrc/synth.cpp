@@ -12,8 +12,11 @@
 //  kind 1  linear (config 2): every row x_new = a*x_prev + b*x_other + c; 50% of rows in
 //          clusters of 8, 40% in clusters of 2048, 10% in one big cluster; 1/64 of the rows
 //          touch a public input.
-//  kind 2  chain  (config 4 stand-in): long dependent chains of limb-carry rows with quadratic
-//          rows whose A collapses after substitution, i.e. deep rounds >= 2.
+//  kind 2  chain  (config 4 stand-in, ECDSAVerify): deep process_4 chains whose composition fills
+//          right-hand sides of ~2,000 terms, constant cascades that run 8 rounds, chained
+//          4-limb big-integer products (see gen_chain).
+//  kind 3  poseidon (config 3 stand-in): Poseidon(16) (t = 17) 16-ary Merkle paths of depth 20.
+//  kind 4  sha (config 1 stand-in): sha256 compression gadgets (XOR3, Ch, Maj, BinSum, Num2Bits).
 //
 // Coefficients: 60% from {1, p-1, 2^k}, 40% uniform in [1, p) (splitmix64 stream).
 #include <algorithm>
@@ -270,54 +273,387 @@ static void gen_linear(Gen &g, uint64_t R, uint32_t n_pub) {
   }
 }
 
+// A quadratic row A * B = C of single-signal operands (circom's `out <== x * y`).
+static void quad(Gen &g, uint32_t x, uint32_t y, uint32_t out) {
+  const uint64_t one[4] = {1, 0, 0, 0};
+  Terms a, b, c;
+  add_v(a, x, one);
+  add_v(b, y, one);
+  add_v(c, out, one);
+  g.row(g.na, a);
+  g.row(g.nb, b);
+  g.row(g.nc, c);
+  g.n_q++;
+}
+// b * (b - 1) = 0 (bit / range check)
+static void bit_row(Gen &g, uint32_t x) {
+  const uint64_t one[4] = {1, 0, 0, 0};
+  uint64_t m1[4];
+  g.neg_one(m1);
+  Terms a, b, c;
+  add_v(a, x, one);
+  add_v(b, x, one);
+  add_v(b, 0, m1);
+  g.row(g.na, a);
+  g.row(g.nb, b);
+  g.row(g.nc, c);
+  g.n_q++;
+}
+
+// kind 2 (BASELINE configs[3], circom-ecdsa ECDSAVerify stand-in): three ingredients.
+//  (a) deep chains: L-row linear clusters (process_4) x_i = f(x_{i-1}, y_i, y_{i-1}); y_i and
+//      x_i / y_i each occur in two rows, so the uniques phase only consumes the two end rows and the
+//      ordered loop deletes x_i row by row: create_nonoverlapping_substitutions_4
+//      (simplification_utils.rs:465-479) then composes x_i into a right-hand side over y_1..y_i --
+//      O(L) entries, O(L^2) fill-in.  Every y_i is range checked (kept); every 64th x_i feeds a
+//      quadratic row, which the frames expand to ~i entries;
+//  (b) constant cascades t_k = t_{k-1}^2 from a constant t_0: row k turns linear only after round k
+//      has eliminated t_{k-1} (apply_substitution_to_map, constraint_simplification.rs:345-396), so a
+//      depth-D cascade runs D + 1 rounds;
+//  (c) bulk: 4-limb big-integer products (16 limb products, 7 carry columns, carry range checks),
+//      chained: the columns' outputs are the next product's limbs.
 static void gen_chain(Gen &g, uint64_t R, uint32_t n_pub) {
-  // limb decompositions with carries: x_{i+1} = x_i + 2^64 * c_i - l_i, quadratic range rows
-  // l_i * (l_i - 1) style, and selector rows A = {x_k} that collapse when x_k becomes constant.
-  Terms t, a, b, c;
-  uint64_t one[4] = {1, 0, 0, 0};
+  const uint64_t one[4] = {1, 0, 0, 0};
+  uint64_t m1[4];
+  g.neg_one(m1);
   uint64_t made = 0;
-  while (made < R) {
-    uint64_t depth = std::min<uint64_t>(4096, R - made);
-    uint32_t x = g.fresh();
+  Terms t, a, b, c;
+  // (a) deep chains
+  const uint64_t L = 2048;
+  const uint64_t n_deep = std::max<uint64_t>(1, R / 100000);
+  for (uint64_t q = 0; q < n_deep && made < R; ++q) {
+    uint32_t yp = g.fresh(), xp = g.fresh();  // y before x: x has the larger id (max-id tie break)
+    for (uint64_t i = 1; i <= L; ++i) {
+      const uint32_t y = g.fresh(), x = g.fresh();
+      t.clear();
+      add(g, t, x);
+      add(g, t, xp);
+      add(g, t, y);
+      add(g, t, yp);
+      if (g.rng.uni() < 0.3) add(g, t, 0);
+      g.linear_row(t);
+      bit_row(g, y);
+      made += 2;
+      if (i % 64 == 0) {
+        quad(g, x, x, g.fresh());
+        made++;
+      }
+      yp = y;
+      xp = x;
+    }
+  }
+  // (b) constant cascades of depth 2..7 (rounds 3..8)
+  for (int d = 2; d <= 7 && made < R; ++d) {
+    uint32_t tp = g.fresh();
     t.clear();
-    add_v(t, x, one);
+    add_v(t, tp, one);
     add(g, t, 0);
     g.row(g.ce, t);
     g.n_ce++;
     made++;
-    for (uint64_t i = 0; i + 1 < depth && made < R; ++i) {
-      uint32_t l = g.fresh(), cy = g.fresh(), nx = g.fresh();
+    for (int k = 1; k <= d; ++k) {
+      const uint32_t tk = g.fresh();
+      quad(g, tp, tp, tk);
+      made++;
+      tp = tk;
+    }
+  }
+  // (c) chained 4-limb products
+  uint32_t A[4], B[4];
+  auto fresh_limbs = [&](uint32_t *v) {
+    for (int i = 0; i < 4; ++i) v[i] = g.fresh();
+  };
+  fresh_limbs(A);
+  fresh_limbs(B);
+  uint64_t two64[4] = {0, 1, 0, 0};
+  uint64_t mtwo64[4];
+  g.neg(two64, mtwo64);
+  uint32_t pub_used = 0;
+  while (made < R) {
+    uint32_t P[4][4];
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        P[i][j] = g.fresh();
+        quad(g, A[i], B[j], P[i][j]);
+        made++;
+      }
+    uint32_t carry = 0, out[7];
+    for (int col = 0; col < 7; ++col) {
+      const uint32_t cy = g.fresh();
+      out[col] = g.fresh();
       t.clear();
-      add(g, t, nx);
-      add(g, t, x);
-      add(g, t, l);
-      add(g, t, cy);
+      for (int i = 0; i < 4; ++i)
+        if (col - i >= 0 && col - i < 4) add_v(t, P[i][col - i], one);
+      if (carry) add_v(t, carry, one);
+      add_v(t, cy, mtwo64);
+      add_v(t, out[col], m1);
+      if (pub_used < n_pub && g.rng.uni() < 1.0 / 8192) add(g, t, 2 + (pub_used++));
       g.linear_row(t);
-      made++;
-      a.clear(); b.clear(); c.clear();
-      add_v(a, l, one);
-      add_v(b, l, one);
-      add(g, b, 0);
-      g.row(g.na, a);
-      g.row(g.nb, b);
-      g.row(g.nc, c);
-      g.n_q++;
-      made++;
-      if (g.rng.uni() < 0.05) {
+      bit_row(g, cy);
+      made += 2;
+      carry = cy;
+    }
+    // the next product multiplies the low limbs of this one by fresh limbs (a chain of products)
+    for (int i = 0; i < 4; ++i) A[i] = out[i];
+    if (g.rng.uni() < 0.25) fresh_limbs(A);
+    fresh_limbs(B);
+  }
+}
+
+// kind 3 (BASELINE configs[2], Poseidon(16) Merkle tree stand-in; circomlib's constants are not
+// available offline): 16-ary Merkle paths, each level = 16 one-hot selector bits (e(e-1) = 0,
+// sum e = 1), 16 mux rows in_j = sib_j + e_j (cur - sib_j), then one Poseidon permutation of width
+// t = 17 (R_F = 8 full rounds, R_P = 68 partial): per round an Ark row a_i = s_i + c_i per lane, the
+// x^5 S-box as three quadratic rows (every lane in full rounds, lane 0 in partial rounds), and the
+// MDS mix as linear rows -- dense 17-term rows in full rounds, the sparse S/V form of circomlib's
+// PoseidonEx in partial rounds.  The partial rounds' lanes 1..16 pass through linear rows only, so
+// each permutation's partial rounds form one ~2,300-row process_4 cluster whose merges of 17-term
+// rows with 256-bit random coefficients are what stress treat_constraint_4
+// (simplification_utils.rs:312-349); the S-box rows then receive right-hand sides of up to ~85 terms.
+static void gen_poseidon(Gen &g, uint64_t R, uint32_t n_pub) {
+  constexpr int T = 17, RF = 8, RP = 68, NR = RF + RP;
+  typedef std::array<uint64_t, 4> E4;
+  std::vector<E4> M(T * T), S(T), V(T), C(NR * T);  // fixed per circuit, like circomlib's tables
+  for (auto *vec : {&M, &S, &V, &C})
+    for (auto &x : *vec) g.rand_elem(x.data());
+  const uint64_t one[4] = {1, 0, 0, 0};
+  uint64_t m1[4];
+  g.neg_one(m1);
+  Terms t, a, b, c;
+  uint64_t made = 0;
+  uint32_t pub_used = 0;
+  uint32_t st[T], y[T];
+  while (made < R) {
+    uint32_t cur = g.fresh();  // the leaf
+    for (int lvl = 0; lvl < 20 && made < R; ++lvl) {
+      uint32_t e[16], in[16];
+      for (int j = 0; j < 16; ++j) {
+        e[j] = g.fresh();
+        bit_row(g, e[j]);
+      }
+      t.clear();
+      for (int j = 0; j < 16; ++j) add_v(t, e[j], one);
+      add_v(t, 0, m1);
+      g.linear_row(t);
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t sib = g.fresh();
+        in[j] = g.fresh();
         a.clear(); b.clear(); c.clear();
-        add_v(a, x, one);
-        add_v(b, cy, one);
-        add_v(c, g.fresh(), one);
+        add_v(a, e[j], one);
+        add_v(b, cur, one);
+        add_v(b, sib, m1);
+        add_v(c, in[j], one);
+        add_v(c, sib, m1);
         g.row(g.na, a);
         g.row(g.nb, b);
         g.row(g.nc, c);
         g.n_q++;
-        made++;
       }
-      x = nx;
+      made += 33;
+      // capacity lane: a constant (initialState = 0)
+      st[0] = g.fresh();
+      t.clear();
+      add_v(t, st[0], one);
+      g.row(g.ce, t);
+      g.n_ce++;
+      made++;
+      for (int j = 0; j < 16; ++j) st[j + 1] = in[j];
+      for (int r = 0; r < NR; ++r) {
+        const bool full = r < RF / 2 || r >= RF / 2 + RP;
+        for (int i = 0; i < T; ++i) {  // Ark
+          const uint32_t ai = g.fresh();
+          uint64_t nc_[4];
+          g.neg(C[r * T + i].data(), nc_);
+          t.clear();
+          add_v(t, ai, one);
+          add_v(t, st[i], m1);
+          add_v(t, 0, nc_);
+          g.linear_row(t);
+          made++;
+          if (full || i == 0) {  // S-box x^5
+            const uint32_t x2 = g.fresh(), x4 = g.fresh(), yo = g.fresh();
+            quad(g, ai, ai, x2);
+            quad(g, x2, x2, x4);
+            quad(g, x4, ai, yo);
+            made += 3;
+            y[i] = yo;
+          } else {
+            y[i] = ai;
+          }
+        }
+        uint32_t m[T];
+        for (int i = 0; i < T; ++i) {  // Mix
+          m[i] = g.fresh();
+          t.clear();
+          add_v(t, m[i], one);
+          uint64_t nv[4];
+          if (full) {
+            for (int j = 0; j < T; ++j) {
+              g.neg(M[i * T + j].data(), nv);
+              add_v(t, y[j], nv);
+            }
+          } else if (i == 0) {
+            for (int j = 0; j < T; ++j) {
+              g.neg(S[j].data(), nv);
+              add_v(t, y[j], nv);
+            }
+          } else {
+            add_v(t, y[i], m1);
+            g.neg(V[i].data(), nv);
+            add_v(t, y[0], nv);
+          }
+          g.linear_row(t);
+          made++;
+        }
+        for (int i = 0; i < T; ++i) st[i] = m[i];
+      }
+      cur = st[1];
+    }
+    if (pub_used < n_pub) {  // the root is published: an equality with a public input
+      t.clear();
+      uint64_t cc[4], nc_[4];
+      g.coef(cc);
+      g.neg(cc, nc_);
+      add_v(t, cur, cc);
+      add_v(t, 2 + (pub_used++), nc_);
+      g.linear_row(t);
+      made++;
     }
   }
-  (void)n_pub;
+}
+
+// kind 4 (BASELINE configs[0], circomlib sha256_2 stand-in: circomlib is not available offline): per
+// compression round the bit-level gadgets of Sha256compression -- XOR3 (sigma functions, two
+// quadratic rows per bit: mid = b c, out = a (1 - 2b - 2c + 4 mid) + b + c - 2 mid), Ch (one
+// quadratic row per bit), Maj (two), and BinSum adders: one long linear row sum_k sum_i 2^i in_k[i] =
+// sum_i 2^i out[i] (+ carry bits), whose output bits are range checked (b (b - 1) = 0) -- plus the
+// message schedule's Num2Bits rows.  ~64 rounds + 48 schedule words per compression (~30k rows).
+static void gen_sha(Gen &g, uint64_t R, uint32_t n_pub) {
+  const uint64_t one[4] = {1, 0, 0, 0};
+  uint64_t m1[4], m2[4], four[4] = {4, 0, 0, 0};
+  g.neg_one(m1);
+  const uint64_t two[4] = {2, 0, 0, 0};
+  g.neg(two, m2);
+  Terms t, a, b, c;
+  uint64_t made = 0;
+  uint32_t pub_used = 0;
+  auto word = [&](uint32_t *w) {
+    for (int i = 0; i < 32; ++i) w[i] = g.fresh();
+  };
+  auto pow2 = [](int i, uint64_t v[4]) {
+    v[0] = v[1] = v[2] = v[3] = 0;
+    v[i / 64] = 1ULL << (i % 64);
+  };
+  // XOR3 of three bits -> new bit (two quadratic rows)
+  auto xor3 = [&](uint32_t x, uint32_t yb, uint32_t z) -> uint32_t {
+    const uint32_t mid = g.fresh(), out = g.fresh();
+    quad(g, yb, z, mid);
+    a.clear(); b.clear(); c.clear();
+    add_v(a, x, one);
+    add_v(b, 0, one);
+    add_v(b, yb, m2);
+    add_v(b, z, m2);
+    add_v(b, mid, four);
+    add_v(c, out, one);
+    add_v(c, yb, m1);
+    add_v(c, z, m1);
+    add_v(c, mid, two);
+    g.row(g.na, a);
+    g.row(g.nb, b);
+    g.row(g.nc, c);
+    g.n_q++;
+    made += 2;
+    return out;
+  };
+  // BinSum of n 32-bit words: one linear row + 32 + carry output bits with range checks
+  auto binsum = [&](const std::vector<const uint32_t *> &ops, uint32_t *out) {
+    const int nc = 32 + (ops.size() > 1 ? (int)std::ceil(std::log2((double)ops.size())) : 0);
+    t.clear();
+    uint64_t v[4], nv[4];
+    for (auto *w : ops)
+      for (int i = 0; i < 32; ++i) {
+        pow2(i, v);
+        add_v(t, w[i], v);
+      }
+    for (int i = 0; i < nc; ++i) {
+      const uint32_t ob = g.fresh();
+      if (i < 32) out[i] = ob;
+      pow2(i, v);
+      g.neg(v, nv);
+      add_v(t, ob, nv);
+      bit_row(g, ob);
+    }
+    g.linear_row(t);
+    made += 1 + nc;
+  };
+  while (made < R) {
+    // message: 16 words from 512 input bits (Num2Bits of 16 words: x = sum 2^i b_i, b range-checked)
+    std::vector<std::array<uint32_t, 32>> W(64);
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t x = g.fresh();
+      word(W[k].data());
+      t.clear();
+      uint64_t v[4];
+      for (int i = 0; i < 32; ++i) {
+        pow2(i, v);
+        add_v(t, W[k][i], v);
+        bit_row(g, W[k][i]);
+      }
+      add_v(t, x, m1);
+      if (pub_used < n_pub && k == 0) add_v(t, 2 + (pub_used++), one);
+      g.linear_row(t);
+      made += 33;
+    }
+    for (int k = 16; k < 64 && made < R; ++k) {  // schedule: W[k] = s1(W[k-2]) + W[k-7] + s0(W[k-15]) + W[k-16]
+      uint32_t s0[32], s1[32];
+      for (int i = 0; i < 32; ++i) {
+        s0[i] = xor3(W[k - 15][(i + 7) % 32], W[k - 15][(i + 18) % 32], W[k - 15][(i + 3) % 32]);
+        s1[i] = xor3(W[k - 2][(i + 17) % 32], W[k - 2][(i + 19) % 32], W[k - 2][(i + 10) % 32]);
+      }
+      binsum({s1, W[k - 7].data(), s0, W[k - 16].data()}, W[k].data());
+    }
+    uint32_t H[8][32];
+    for (auto &h : H) word(h);
+    for (int r = 0; r < 64 && made < R; ++r) {
+      uint32_t S1[32], ch[32], S0[32], mj[32], K[32], T1[32], T2[32], na_[32], ne_[32];
+      for (int i = 0; i < 32; ++i) {
+        S1[i] = xor3(H[4][(i + 6) % 32], H[4][(i + 11) % 32], H[4][(i + 25) % 32]);
+        S0[i] = xor3(H[0][(i + 2) % 32], H[0][(i + 13) % 32], H[0][(i + 22) % 32]);
+        // Ch = e f + (1 - e) g = e (f - g) + g
+        ch[i] = g.fresh();
+        a.clear(); b.clear(); c.clear();
+        add_v(a, H[4][i], one);
+        add_v(b, H[5][i], one);
+        add_v(b, H[6][i], m1);
+        add_v(c, ch[i], one);
+        add_v(c, H[6][i], m1);
+        g.row(g.na, a); g.row(g.nb, b); g.row(g.nc, c);
+        g.n_q++;
+        // Maj = a b + a c + b c - 2 a b c: mid = b c, out = a (b + c - 2 mid) + mid
+        const uint32_t mid = g.fresh();
+        mj[i] = g.fresh();
+        quad(g, H[1][i], H[2][i], mid);
+        a.clear(); b.clear(); c.clear();
+        add_v(a, H[0][i], one);
+        add_v(b, H[1][i], one);
+        add_v(b, H[2][i], one);
+        add_v(b, mid, m2);
+        add_v(c, mj[i], one);
+        add_v(c, mid, m1);
+        g.row(g.na, a); g.row(g.nb, b); g.row(g.nc, c);
+        g.n_q++;
+        made += 3;
+      }
+      word(K);  // the round constant's bits (constants in circomlib; free signals here)
+      binsum({H[7], S1, ch, K, W[r].data()}, T1);
+      binsum({S0, mj}, T2);
+      binsum({T1, T2}, na_);
+      binsum({H[3], T1}, ne_);
+      for (int w = 7; w > 0; --w) memcpy(H[w], H[w - 1], sizeof(H[w]));
+      memcpy(H[0], na_, sizeof(na_));
+      memcpy(H[4], ne_, sizeof(ne_));
+    }
+  }
 }
 
 }  // namespace rs
@@ -326,7 +662,7 @@ using namespace rs;
 
 extern "C" int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id,
                         rs_input **out) {
-  if (prime_id >= 8 || kind > 2) { set_error("rs_synth: bad kind/prime"); return RS_E_INVALID; }
+  if (prime_id >= 8 || kind > 4) { set_error("rs_synth: bad kind/prime"); return RS_E_INVALID; }
   Gen g;
   g.rng.s = seed;
   memcpy(g.p, kPrimes[prime_id], 32);
@@ -335,7 +671,9 @@ extern "C" int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t pr
   g.next_sig = 1 + n_out + n_pub + n_priv;
   if (kind == 0) gen_mixed(g, rows, n_pub, n_priv, 1 + n_out + n_pub);
   else if (kind == 1) gen_linear(g, rows, n_pub);
-  else gen_chain(g, rows, n_pub);
+  else if (kind == 2) gen_chain(g, rows, n_pub);
+  else if (kind == 3) gen_poseidon(g, rows, n_pub);
+  else gen_sha(g, rows, n_pub);
   rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
   in->prime_id = prime_id;
   memcpy(in->prime, g.p, 32);

@@ -257,7 +257,9 @@ int rs_write_constraints_json(const char *path, const rs_output *out);
 int rs_write_substitution_json(const char *path, const rs_output *out);
 
 /* Seeded synthetic --O0 systems for benchmarks/tests (see DESIGN.md "Workloads").
- * kind: 0 = mixed (metric circuit), 1 = purely linear, 2 = chain (deep substitution chains). */
+ * kind: 0 = mixed (metric circuit, BASELINE configs[4]), 1 = purely linear (configs[1]), 2 = chain
+ * (configs[3] ECDSA stand-in: deep composition, 8 rounds), 3 = Poseidon(16) Merkle (configs[2]),
+ * 4 = sha256-like bit gadgets (configs[0]). */
 int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id, rs_input **in);
 
 #ifdef __cplusplus
