@@ -1,35 +1,80 @@
-"""Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE),
-corrected as MI355X_MICROARCH.md 'HBM' prescribes for gfx950 (FETCH_SIZE reports half the bytes of
-wide streaming reads: doubled).  rocprofv3 reports both counters in KiB.
-usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel substring>  -> prints bytes"""
+"""Per-launch HBM traffic of the bench's kernels from separate rocprofv3 --pmc passes (FETCH_SIZE,
+WRITE_SIZE), corrected as MI355X_MICROARCH.md 'HBM' prescribes for gfx950: FETCH_SIZE reports half
+the bytes of wide streaming reads, so it is doubled; WRITE_SIZE is taken as is.  rocprofv3 reports
+both counters in KiB.
+
+usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> -o profiles/roundN_pmc_traffic.json
+           [--wrreq <dir of a TCC_EA0_WRREQ / TCC_EA0_WRREQ_64B pass>]
+The JSON's `bytes_per_launch` keys are bench.py's KERNELS names; bench.py reads the newest
+profiles/round*_pmc_traffic.json into roofline.traffic."""
+import argparse
 import csv
 import glob
+import json
 import os
 import sys
 
+# bench.py KERNELS name -> substring of the rocprofv3 kernel name
+GROUPS = {
+    "k_big_main<512> (head)": "k_big_main<512u>",
+    "k_big_main<256> (tail)": "k_big_main<256u>",
+    "k_nl_fill": "rs::k_nl_fill(",
+    "k_round_fill": "rs::k_round_fill(",
+}
 
-def per_dispatch(d, counter, kernel):
-    vals = []
+
+def per_dispatch(d, counter):
+    """{kernel name: [value per dispatch]} for one counter of one pass."""
+    out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                    vals.append(float(row["Counter_Value"]))
-    return vals
+                if row.get("Counter_Name") != counter:
+                    continue
+                out.setdefault(row.get("Kernel_Name", ""), []).append(float(row["Counter_Value"]))
+    return out
+
+
+def group_avg(tab, pat):
+    vals = [v for name, vs in tab.items() if pat in name for v in vs]
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
 def main():
-    fdir, wdir, kernel = sys.argv[1:4]
-    fe = per_dispatch(fdir, "FETCH_SIZE", kernel)
-    wr = per_dispatch(wdir, "WRITE_SIZE", kernel)
-    if not fe or not wr:
-        print("null")
-        return
-    fetch = 2.0 * sum(fe) / len(fe) * 1024.0
-    write = sum(wr) / len(wr) * 1024.0
-    print(f"{fetch + write:.0f}")
-    sys.stderr.write(f"{kernel}: {len(fe)} dispatches, FETCH_SIZE(x2) {fetch / 1e6:.1f} MB + "
-                     f"WRITE_SIZE {write / 1e6:.1f} MB per launch\n")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--wrreq", default=None)
+    args = ap.parse_args()
+    fe = per_dispatch(args.fetch_dir, "FETCH_SIZE")
+    wr = per_dispatch(args.write_dir, "WRITE_SIZE")
+    req = per_dispatch(args.wrreq, "TCC_EA0_WRREQ_sum") if args.wrreq else {}
+    req64 = per_dispatch(args.wrreq, "TCC_EA0_WRREQ_64B_sum") if args.wrreq else {}
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of "
+                     "`bench.py --steps 1 --warmup 0 --no-cpu`; FETCH_SIZE x2 (gfx950), KiB -> bytes",
+           "bytes_per_launch": {}, "detail": {}}
+    for name, pat in GROUPS.items():
+        f, nf = group_avg(fe, pat)
+        w, nw = group_avg(wr, pat)
+        if f is None or w is None:
+            continue
+        fetch = 2.0 * f * 1024.0
+        write = w * 1024.0
+        res["bytes_per_launch"][name] = int(fetch + write)
+        det = {"fetch_bytes_x2": int(fetch), "write_bytes": int(write), "dispatches": [nf, nw]}
+        r, _ = group_avg(req, pat)
+        r64, _ = group_avg(req64, pat)
+        if r is not None and r64 is not None:
+            det["wrreq"] = int(r)
+            det["wrreq_64B"] = int(r64)
+            det["wrreq_32B"] = int(r - r64)
+        res["detail"][name] = det
+        sys.stderr.write(f"{name}: FETCH_SIZE(x2) {fetch / 1e6:.1f} MB + WRITE_SIZE {write / 1e6:.1f} MB per launch"
+                         + (f"; write requests {det.get('wrreq')} ({det.get('wrreq_64B')} of 64 B)" if "wrreq" in det else "")
+                         + "\n")
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
 
 
 if __name__ == "__main__":
