@@ -95,6 +95,7 @@ SYMBOLS = [
     ("rs_read_r1cs_o0", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(RsInput))]),
     ("rs_input_free", None, [C.POINTER(RsInput)]),
     ("rs_write_r1cs", C.c_int, [C.c_char_p, C.POINTER(RsInput), C.POINTER(RsOutput)]),
+    ("rs_write_r1cs_gates", C.c_int, [C.c_char_p, C.POINTER(RsInput), C.POINTER(RsOutput), C.c_char_p]),
     ("rs_write_sym", C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(RsOutput)]),
     ("rs_write_constraints_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),
     ("rs_write_substitution_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),

@@ -54,7 +54,7 @@ int main(int argc, char **argv) {
   int rc = rs_simplify(in, &fl, &o);
   auto t1 = std::chrono::steady_clock::now();
   if (rc) { fprintf(stderr, "error %d: %s\n", rc, rs_last_error()); rs_input_free(in); return 1; }
-  if (rs_write_r1cs((out + ".r1cs").c_str(), in, o)) { fprintf(stderr, "error: %s\n", rs_last_error()); return 1; }
+  if (rs_write_r1cs_gates((out + ".r1cs").c_str(), in, o, in_r1cs)) { fprintf(stderr, "error: %s\n", rs_last_error()); return 1; }
   if (in_sym && rs_write_sym(in_sym, (out + ".sym").c_str(), o)) { fprintf(stderr, "error: %s\n", rs_last_error()); return 1; }
   if (json && rs_write_constraints_json((out + "_constraints.json").c_str(), o)) { fprintf(stderr, "error: %s\n", rs_last_error()); return 1; }
   if (fl.emit_substitution_log && rs_write_substitution_json((out + "_substitutions.json").c_str(), o)) {

@@ -29,18 +29,6 @@
 
 namespace rs {
 
-const uint64_t kPrimes[8][4] = {
-    {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL, 0x30644e72e131a029ULL},
-    {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL, 0x73eda753299d7d48ULL},
-    {0xffffffff00000001ULL, 0, 0, 0},
-    {0x3c208c16d87cfd47ULL, 0x97816a916871ca8dULL, 0xb85045b68181585dULL, 0x30644e72e131a029ULL},
-    {0x992d30ed00000001ULL, 0x224698fc094cf91bULL, 0x0000000000000000ULL, 0x4000000000000000ULL},
-    {0x8c46eb2100000001ULL, 0x224698fc0994a8ddULL, 0x0000000000000000ULL, 0x4000000000000000ULL},
-    {0xffffffffffffffffULL, 0x00000000ffffffffULL, 0x0000000000000000ULL, 0xffffffff00000001ULL},
-    {0x0a11800000000001ULL, 0x59aa76fed0000001ULL, 0x60b44d1e5c37b001ULL, 0x12ab655e9a2ca556ULL}};
-
-static thread_local std::string g_err;
-void set_error(const std::string &m) { g_err = m; }
 
 struct RsError : std::runtime_error {
   int code;
@@ -184,6 +172,8 @@ struct rs_engine {
   hipEvent_t ev_grp[3] = {};
   bool pending[3] = {false, false, false};
   int *h_vflag = nullptr;  // pinned: per-group validation verdicts (D2H after each group's checks)
+  unsigned long long *h_lvl = nullptr;  // pinned: frontier counts of the head's composition levels
+  hipEvent_t ev_lvl[4] = {};
   double h2d_wait_ms = 0;
   // pinned result buffers of rs_engine_simplify (grow only) and the view handed out
   struct Pin {
@@ -1098,11 +1088,17 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           HC(hipGetLastError());
           std::swap(cur, nxt);
           levels = level + 1;
-          if (level % 4 == 3) {  // stop once a frontier is empty (checked every few levels)
-            unsigned long long h = 0;
-            HC(hipMemcpyAsync(&h, nn, 8, hipMemcpyDeviceToHost, E->st2));
-            HC(hipStreamSynchronize(E->st2));
-            if (!h) break;
+          if (level % 4 == 3) {
+            // stop once a frontier is empty: every 4 levels the frontier count goes to a pinned
+            // slot, and the host checks the slot of two batches back -- it never waits for the
+            // level it just enqueued (launches past an empty frontier return at once)
+            const uint32_t b = level / 4;
+            HC(hipMemcpyAsync(E->h_lvl + b % 4, nn, 8, hipMemcpyDeviceToHost, E->st2));
+            HC(hipEventRecord(E->ev_lvl[b % 4], E->st2));
+            if (b >= 2) {
+              HC(hipEventSynchronize(E->ev_lvl[(b - 2) % 4]));
+              if (!E->h_lvl[(b - 2) % 4]) break;
+            }
           }
         }
         hipLaunchKernelGGL(k_big_emit<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
@@ -2298,7 +2294,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
 // ==================================================================== C API
 extern "C" {
 
-const char *rs_last_error(void) { return g_err.c_str(); }
 int rs_abi_version(void) { return RS_ABI_VERSION; }
 
 int rs_engine_create(int device, rs_engine **eng) {
@@ -2325,6 +2320,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipHostMalloc((void **)&E->h_vflag, 6 * sizeof(int), hipHostMallocDefault));
     memset(E->h_vflag, 0, 6 * sizeof(int));
+    HC(hipHostMalloc((void **)&E->h_lvl, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+    for (auto &ev : E->ev_lvl) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipEventCreate(&E->ev0));
     HC(hipEventCreate(&E->ev1));
     HC(hipEventCreate(&E->ev2));
@@ -2353,6 +2350,9 @@ void rs_engine_destroy(rs_engine *E) {
   for (auto &pb : E->pin)
     if (pb.p) (void)hipHostFree(pb.p);
   if (E->h_vflag) (void)hipHostFree(E->h_vflag);
+  if (E->h_lvl) (void)hipHostFree(E->h_lvl);
+  for (auto &ev : E->ev_lvl)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : E->ev_grp)
     if (ev) (void)hipEventDestroy(ev);
   if (E->stc) (void)hipStreamDestroy(E->stc);

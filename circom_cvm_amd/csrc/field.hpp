@@ -29,7 +29,6 @@ struct FieldP {
   Fe r2;        // R^2 mod p  (R = 2^261)
   Fe one;       // R mod p
   Fe pm2;       // p - 2 (Fermat exponent)
-  Fe r3;        // R^3 mod p (Montgomery-form inverse from a plain binary GCD)
 };
 
 __host__ __device__ __forceinline__ bool fe_is_zero(const Fe &a) {
@@ -218,20 +217,11 @@ __host__ __device__ inline Fe finv_fermat(const FieldP &F, const Fe &a) {
   }
   return r;
 }
-__host__ __device__ __forceinline__ void shr1c(uint64_t *x, uint64_t top) {  // x = (top:x) >> 1
-  x[0] = (x[0] >> 1) | (x[1] << 63);
-  x[1] = (x[1] >> 1) | (x[2] << 63);
-  x[2] = (x[2] >> 1) | (x[3] << 63);
-  x[3] = (x[3] >> 1) | (top << 63);
-}
-__host__ __device__ __forceinline__ bool is_one4(const uint64_t *x) { return x[0] == 1 && (x[1] | x[2] | x[3]) == 0; }
-// Inverse in Montgomery form: binary extended Euclid on the residue aR (shifts, adds and
-// subtractions only), (aR)^-1 = a^-1 R^-1, then one product by R^3 gives a^-1 R.  The same value
-// as num-bigint's mod_inverse (the inverse is unique); about 30x lower latency than Fermat's
-// ~384 dependent products (tools/micro/fmul_bench.hip).
-// a^-1 = a^(p-2) (Fermat), left to right: 254 squarings (fsqr) and a product per set bit; the control
-// flow follows the exponent only, so a wave never diverges.  3.2x lower latency for one wave than
-// the binary extended GCD it replaced (tools/micro/finv_bench.hip); 0 -> 0.
+// Inverse in Montgomery form: (aR)^-1 R^2 = (aR)^(p-2) as Montgomery powers, i.e. a^-1 = a^(p-2)
+// (Fermat), left to right: ~254 squarings (fsqr) and a product per set bit of p-2.  The control flow
+// follows the exponent only, so a wave never diverges.  The same value as num-bigint's mod_inverse
+// (the inverse is unique); 3.2x lower latency for one wave than the binary extended GCD this
+// replaced (tools/micro/finv_bench.hip).  0 -> 0.
 __host__ __device__ inline Fe finv(const FieldP &F, const Fe &a) {
   int top = 3;
   while (top > 0 && F.pm2.l[top] == 0) --top;
@@ -268,7 +258,6 @@ inline FieldP make_field(const uint64_t prime[4]) {
   for (int j = 0; j < 4; ++j) F.r2.l[j] = x[j];
   uint64_t two[4] = {2, 0, 0, 0};
   sub4(F.pm2.l, F.p, two);
-  F.r3 = fmul(F, F.r2, F.r2);
   return F;
 }
 

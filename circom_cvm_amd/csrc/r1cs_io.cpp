@@ -61,6 +61,74 @@ static inline uint64_t le_order_key(uint32_t k) {
   return key;
 }
 
+// Bounds-checked reader over one section [off, off + size) of an .r1cs buffer: every read fails
+// (with the error set) instead of running past the section or the file.
+struct Cursor {
+  const std::vector<uint8_t> &b;
+  uint64_t pos, end;
+  Cursor(const std::vector<uint8_t> &buf, uint64_t off, uint64_t size) : b(buf), pos(off), end(off + size) {}
+  uint64_t left() const { return end - pos; }
+  bool bytes(void *dst, uint64_t n) {
+    if (n > left()) { set_error("truncated r1cs section"); return false; }
+    memcpy(dst, &b[pos], n);
+    pos += n;
+    return true;
+  }
+  bool skip(uint64_t n) {
+    if (n > left()) { set_error("truncated r1cs section"); return false; }
+    pos += n;
+    return true;
+  }
+  bool u32(uint32_t &v) { return bytes(&v, 4); }
+  bool u64(uint64_t &v) { return bytes(&v, 8); }
+};
+
+// Section table of an .r1cs file (r1cs_writer.rs:147-204): the first section of each type 1-5.
+struct R1csSections {
+  bool have[6] = {};
+  uint64_t off[6] = {}, size[6] = {};
+};
+static bool scan_sections(const std::vector<uint8_t> &buf, R1csSections &S) {
+  uint32_t nsec = rd<uint32_t>(&buf[8]);
+  uint64_t off = 12;
+  for (uint32_t s = 0; s < nsec; ++s) {
+    if (off + 12 > buf.size()) { set_error("truncated r1cs section table"); return false; }
+    const uint32_t t = rd<uint32_t>(&buf[off]);
+    const uint64_t sz = rd<uint64_t>(&buf[off + 4]);
+    off += 12;
+    if (sz > buf.size() - off) { set_error("r1cs section runs past the end of the file"); return false; }
+    if (t >= 1 && t <= 5 && !S.have[t]) { S.have[t] = true; S.off[t] = off; S.size[t] = sz; }
+    off += sz;
+  }
+  return true;
+}
+// Custom gates applied (section 5, r1cs_writer.rs:408-450): u32 count, then per application a u32
+// gate index, a u32 signal count and u64 signals.  Collects the signals (sorted, distinct) and/or
+// the raw applications.
+static bool read_gate_applications(const std::vector<uint8_t> &buf, const R1csSections &S, uint64_t n_labels,
+                                   std::vector<uint32_t> *sigs, std::vector<std::pair<uint32_t, std::vector<uint64_t>>> *apps) {
+  Cursor c(buf, S.off[5], S.size[5]);
+  uint32_t na = 0;
+  if (!c.u32(na)) return false;
+  for (uint32_t a = 0; a < na; ++a) {
+    uint32_t gi = 0, ns = 0;
+    if (!c.u32(gi) || !c.u32(ns)) return false;
+    if ((uint64_t)ns * 8 > c.left()) { set_error("truncated custom-gate application"); return false; }
+    std::vector<uint64_t> v(ns);
+    for (uint32_t i = 0; i < ns; ++i) {
+      c.u64(v[i]);
+      if (v[i] >= n_labels) { set_error("custom-gate signal >= n_labels"); return false; }
+      if (sigs) sigs->push_back((uint32_t)v[i]);
+    }
+    if (apps) apps->push_back({gi, std::move(v)});
+  }
+  if (sigs) {
+    std::sort(sigs->begin(), sigs->end());
+    sigs->erase(std::unique(sigs->begin(), sigs->end()), sigs->end());
+  }
+  return true;
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -121,65 +189,68 @@ int rs_read_r1cs_o0(const char *path, rs_input **out) {
     set_error(std::string("cannot read r1cs file ") + path);
     return RS_E_INVALID;
   }
-  uint32_t nsec = rd<uint32_t>(&buf[8]);
-  size_t off = 12;
-  size_t hdr_off = 0, cons_off = 0;
-  bool have_hdr = false, have_cons = false;
-  for (uint32_t s = 0; s < nsec; ++s) {
-    if (off + 12 > buf.size()) { set_error("truncated r1cs"); return RS_E_INVALID; }
-    uint32_t t = rd<uint32_t>(&buf[off]);
-    uint64_t sz = rd<uint64_t>(&buf[off + 4]);
-    off += 12;
-    if (t == 1 && !have_hdr) { hdr_off = off; have_hdr = true; }
-    if (t == 2 && !have_cons) { cons_off = off; have_cons = true; }
-    if (t == 4 || t == 5) {
-      set_error("custom-gate sections are out of scope for this back end");
-      return RS_E_INVALID;
-    }
-    off += sz;
-  }
-  if (!have_hdr || !have_cons) { set_error("r1cs without header/constraints"); return RS_E_INVALID; }
-  uint32_t fs = rd<uint32_t>(&buf[hdr_off]);
+  R1csSections S;
+  if (!scan_sections(buf, S)) return RS_E_INVALID;
+  if (!S.have[1] || !S.have[2]) { set_error("r1cs without header/constraints"); return RS_E_INVALID; }
+  Cursor hc(buf, S.off[1], S.size[1]);
+  uint32_t fs = 0;
+  if (!hc.u32(fs)) return RS_E_INVALID;
   if (fs == 0 || fs > 32 || fs % 8) { set_error("unsupported field size"); return RS_E_INVALID; }
   uint64_t p[4] = {0, 0, 0, 0};
-  memcpy(p, &buf[hdr_off + 4], fs);
-  size_t h = hdr_off + 4 + fs;
-  uint32_t n_out = rd<uint32_t>(&buf[h + 4]);
-  uint32_t n_pub = rd<uint32_t>(&buf[h + 8]);
-  uint32_t n_prv = rd<uint32_t>(&buf[h + 12]);
-  uint64_t n_labels = rd<uint64_t>(&buf[h + 16]);
-  uint32_t n_cons = rd<uint32_t>(&buf[h + 24]);
+  uint32_t n_wires = 0, n_out = 0, n_pub = 0, n_prv = 0, n_cons = 0;
+  uint64_t n_labels = 0;
+  if (!hc.bytes(p, fs) || !hc.u32(n_wires) || !hc.u32(n_out) || !hc.u32(n_pub) || !hc.u32(n_prv) ||
+      !hc.u64(n_labels) || !hc.u32(n_cons))
+    return RS_E_INVALID;
+  if (n_labels == 0 || n_labels > 0xfffffff0ull || 1 + (uint64_t)n_out + n_pub > n_labels) {
+    set_error("r1cs header: bad label count");
+    return RS_E_INVALID;
+  }
+  // custom-gate signals (section 5, written by dag/src/r1cs_porting.rs:74-107) are forbidden:
+  // map_tree inserts every signal of a custom-gate node (dag/src/map_to_constraint_list.rs:22-24)
+  std::vector<uint32_t> gate_sigs;
+  if (S.have[5] && !read_gate_applications(buf, S, n_labels, &gate_sigs, nullptr)) return RS_E_INVALID;
+  if (S.have[4]) {  // custom gates used (r1cs_writer.rs:358-405): checked for shape only
+    Cursor gc(buf, S.off[4], S.size[4]);
+    uint32_t ng = 0;
+    if (!gc.u32(ng)) return RS_E_INVALID;
+    for (uint32_t g = 0; g < ng; ++g) {
+      uint8_t ch = 1;
+      while (ch != 0)
+        if (!gc.bytes(&ch, 1)) return RS_E_INVALID;
+      uint32_t np = 0;
+      if (!gc.u32(np) || !gc.skip((uint64_t)np * fs)) return RS_E_INVALID;
+    }
+  }
 
-  rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
-  in->prime_id = RS_PRIME_CUSTOM;
-  for (int i = 0; i < 8; ++i)
-    if (memcmp(kPrimes[i], p, 32) == 0) in->prime_id = i;
-  memcpy(in->prime, p, 32);
-  in->max_signal = n_labels;
-  in->n_pub_out = n_out;
-  in->n_pub_in = n_pub;
-  in->n_priv_in = n_prv;
-  // forbidden_if_main = {0} u outputs u public inputs (dag/src/lib.rs:174, 179-204)
-  in->n_forbidden = 1 + (uint64_t)n_out + n_pub;
-  in->forbidden = (uint32_t *)malloc(sizeof(uint32_t) * in->n_forbidden);
-  for (uint64_t i = 0; i < in->n_forbidden; ++i) in->forbidden[i] = (uint32_t)i;
+  // forbidden_if_main = {0} u outputs u public inputs (dag/src/lib.rs:174, 179-204) u custom-gate
+  // signals, sorted and distinct
+  std::vector<uint32_t> forb;
+  forb.reserve(1 + (uint64_t)n_out + n_pub + gate_sigs.size());
+  for (uint64_t i = 0; i < 1 + (uint64_t)n_out + n_pub; ++i) forb.push_back((uint32_t)i);
+  forb.insert(forb.end(), gate_sigs.begin(), gate_sigs.end());
+  std::sort(forb.begin(), forb.end());
+  forb.erase(std::unique(forb.begin(), forb.end()), forb.end());
 
   Block ce, eq, lin, na, nb, nc;
-  size_t o = cons_off;
+  Cursor cc(buf, S.off[2], S.size[2]);
   std::vector<uint32_t> ks[3];
   std::vector<uint64_t> vs[3];
   for (uint32_t r = 0; r < n_cons; ++r) {
     for (int part = 0; part < 3; ++part) {
       ks[part].clear();
       vs[part].clear();
-      uint32_t n = rd<uint32_t>(&buf[o]);
-      o += 4;
+      uint32_t n = 0;
+      if (!cc.u32(n)) return RS_E_INVALID;
+      if ((uint64_t)n * (4 + fs) > cc.left()) { set_error("truncated r1cs constraint"); return RS_E_INVALID; }
       for (uint32_t e = 0; e < n; ++e) {
-        ks[part].push_back(rd<uint32_t>(&buf[o]));
+        uint32_t k = 0;
         uint64_t v[4] = {0, 0, 0, 0};
-        memcpy(v, &buf[o + 4], fs);
+        cc.u32(k);
+        cc.bytes(v, fs);
+        if (k >= n_labels) { set_error("r1cs constraint: signal >= n_labels"); return RS_E_INVALID; }
+        ks[part].push_back(k);
         vs[part].insert(vs[part].end(), v, v + 4);
-        o += 4 + fs;
       }
     }
     bool lin_row = ks[0].empty() && ks[1].empty();
@@ -203,6 +274,18 @@ int rs_read_r1cs_o0(const char *path, rs_input **out) {
       push(nc, 2);
     }
   }
+  rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
+  in->prime_id = RS_PRIME_CUSTOM;
+  for (int i = 0; i < 8; ++i)
+    if (memcmp(kPrimes[i], p, 32) == 0) in->prime_id = i;
+  memcpy(in->prime, p, 32);
+  in->max_signal = n_labels;
+  in->n_pub_out = n_out;
+  in->n_pub_in = n_pub;
+  in->n_priv_in = n_prv;
+  in->n_forbidden = forb.size();
+  in->forbidden = (uint32_t *)malloc(sizeof(uint32_t) * forb.size());
+  memcpy(in->forbidden, forb.data(), sizeof(uint32_t) * forb.size());
   to_lc(ce, in->cons_eq);
   to_lc(eq, in->eq);
   to_lc(lin, in->linear);
@@ -220,7 +303,12 @@ void rs_input_free(rs_input *in) {
   free(in);
 }
 
-int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out) {
+}  // extern "C"
+
+// r1cs_porting.rs:4-124.  `gates` (optional): the --O0 file's custom-gate sections, re-emitted as
+// the O2 writer does (:54-121): section 4 unchanged, section 5 with every signal mapped label -> wire.
+static int write_r1cs(const char *path, const rs_input *in, const rs_output *out, const std::vector<uint8_t> *o0,
+                      const R1csSections *gates) {
   uint64_t p[4];
   if (!prime_of(in, p)) { set_error("unknown prime"); return RS_E_INVALID; }
   int fs = field_size_bytes(p);
@@ -240,7 +328,8 @@ int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out) {
   };
   std::vector<std::pair<uint64_t, uint64_t>> ord;  // (order key, entry)
   const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
-  fwrite("r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
+  const bool with_gates = gates && (gates->have[4] || gates->have[5]);
+  fwrite(with_gates ? "r1cs\x01\x00\x00\x00\x05\x00\x00\x00" : "r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
   // constraints section (r1cs_porting.rs:20-35) -- written first, size back-patched
   std::vector<uint8_t> hdr;
   put32(hdr, 2);
@@ -306,10 +395,62 @@ int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out) {
   put64(hdr, 8 * out->n_wires);
   fwrite(hdr.data(), 1, hdr.size(), f);
   fwrite(w2l.data(), 8, w2l.size(), f);
+  if (with_gates) {
+    hdr.clear();
+    put32(hdr, 4);
+    if (gates->have[4]) {
+      put64(hdr, gates->size[4]);
+      hdr.insert(hdr.end(), o0->begin() + gates->off[4], o0->begin() + gates->off[4] + gates->size[4]);
+    } else {
+      put64(hdr, 4);
+      put32(hdr, 0);
+    }
+    std::vector<std::pair<uint32_t, std::vector<uint64_t>>> apps;
+    if (gates->have[5] && !read_gate_applications(*o0, *gates, out->n_labels, nullptr, &apps)) {
+      fclose(f);
+      return RS_E_INVALID;
+    }
+    std::vector<uint8_t> s5;
+    put32(s5, (uint32_t)apps.size());
+    for (auto &a : apps) {
+      put32(s5, a.first);
+      put32(s5, (uint32_t)a.second.size());
+      for (uint64_t s : a.second) {
+        const int64_t w = out->label_to_wire[s];
+        if (w < 0) {
+          fclose(f);
+          set_error("custom-gate signal without a wire (SignalMap::get(..).unwrap() panics)");
+          return RS_E_INTERNAL;
+        }
+        put64(s5, (uint64_t)w);
+      }
+    }
+    put32(hdr, 5);
+    put64(hdr, s5.size());
+    hdr.insert(hdr.end(), s5.begin(), s5.end());
+    fwrite(hdr.data(), 1, hdr.size(), f);
+  }
   bool ok = !ferror(f);
   fclose(f);
   if (!ok) { set_error("write error"); return RS_E_INVALID; }
   return RS_OK;
+}
+
+extern "C" {
+
+int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out) {
+  return write_r1cs(path, in, out, nullptr, nullptr);
+}
+
+int rs_write_r1cs_gates(const char *path, const rs_input *in, const rs_output *out, const char *o0_r1cs) {
+  std::vector<uint8_t> buf;
+  if (!read_file(o0_r1cs, buf) || buf.size() < 12 || memcmp(buf.data(), "r1cs", 4) != 0) {
+    set_error(std::string("cannot read r1cs file ") + o0_r1cs);
+    return RS_E_INVALID;
+  }
+  R1csSections S;
+  if (!scan_sections(buf, S)) return RS_E_INVALID;
+  return write_r1cs(path, in, out, &buf, &S);
 }
 
 int rs_write_constraints_json(const char *path, const rs_output *out) {

@@ -241,11 +241,18 @@ void rs_group_destroy(rs_group *g);
 int rs_simplify_multi(const rs_input *in, const rs_flags *fl, int n_devices, const int *devices, rs_output **out);
 
 /* --O0 .r1cs -> rs_input (host arrays owned by the library; free with rs_input_free).
- * Classifies rows exactly like dag/src/map_to_constraint_list.rs:12-44. */
+ * Classifies rows exactly like dag/src/map_to_constraint_list.rs:12-44.  The signals of the
+ * custom-gate applications (section 5, dag/src/r1cs_porting.rs:74-107) join `forbidden`, as
+ * map_tree inserts them (map_to_constraint_list.rs:22-24).  Every read is bounds-checked against
+ * its section and the file: a truncated or malformed file is RS_E_INVALID. */
 int rs_read_r1cs_o0(const char *path, rs_input **in);
 void rs_input_free(rs_input *in);
 /* Writes the simplified .r1cs (constraint_list/src/r1cs_porting.rs:4-124). */
 int rs_write_r1cs(const char *path, const rs_input *in, const rs_output *out);
+/* The same, plus the --O0 file's custom-gate sections as the O2 writer re-emits them
+ * (r1cs_porting.rs:54-121): section 4 unchanged, section 5 with its signals mapped label -> wire
+ * (5 sections in all).  Without sections 4/5 in `o0_r1cs` the output equals rs_write_r1cs's. */
+int rs_write_r1cs_gates(const char *path, const rs_input *in, const rs_output *out, const char *o0_r1cs);
 /* Rewrites an --O0 .sym with the witness column of `out` (constraint_list/src/sym_porting.rs). */
 int rs_write_sym(const char *o0_sym, const char *path, const rs_output *out);
 /* --json: <prefix>_constraints.json (constraint_list/src/json_porting.rs:36-48 port_constraints,

@@ -790,6 +790,9 @@ class System:
     n_priv_in: int
     forbidden: set
     rows: List[Con]                          # --O0 rows in DFS order
+    # custom gates of the --O0 export, or None: (section 4 bytes, [(gate index, [signals])]);
+    # the O2 writer re-emits them (constraint_list/src/r1cs_porting.rs:54-121)
+    gates: Optional[Tuple[bytes, List[Tuple[int, List[int]]]]] = None
 
 
 @dataclass
@@ -958,8 +961,10 @@ def _lc_block(m: Map, fs: int) -> bytes:
 
 
 def write_r1cs_bytes(p, constraints: List[Con], n_wires, n_pub_out, n_pub_in, n_priv_in,
-                     n_labels, wire_to_label: List[int]) -> bytes:
-    """constraint_list/src/r1cs_porting.rs:4-124 + r1cs_writer.rs (3 sections, no custom gates)."""
+                     n_labels, wire_to_label: List[int], gates=None) -> bytes:
+    """constraint_list/src/r1cs_porting.rs:4-124 + r1cs_writer.rs: 3 sections, or 5 with custom
+    gates -- `gates` = (section 4 bytes, [(gate index, [wires])]) written by
+    write_custom_gates_usages / write_custom_gates_applications (r1cs_writer.rs:358-450)."""
     fs = field_size_bytes(p)
     body = b"".join(_lc_block(c.a, fs) + _lc_block(c.b, fs) + _lc_block(c.c, fs)
                     for c in constraints)
@@ -970,7 +975,14 @@ def write_r1cs_bytes(p, constraints: List[Con], n_wires, n_pub_out, n_pub_in, n_
     sec_hdr = struct.pack("<I", 1) + struct.pack("<Q", len(hdr)) + hdr
     w2l = b"".join(struct.pack("<Q", x) for x in wire_to_label)
     sec_w2l = struct.pack("<I", 3) + struct.pack("<Q", len(w2l)) + w2l
-    return b"r1cs" + bytes([1, 0, 0, 0, 3, 0, 0, 0]) + sec_cons + sec_hdr + sec_w2l
+    if gates is None:
+        return b"r1cs" + bytes([1, 0, 0, 0, 3, 0, 0, 0]) + sec_cons + sec_hdr + sec_w2l
+    used, apps = gates
+    body5 = struct.pack("<I", len(apps)) + b"".join(
+        struct.pack("<II", gi, len(sig)) + b"".join(struct.pack("<Q", x) for x in sig) for gi, sig in apps)
+    sec4 = struct.pack("<IQ", 4, len(used)) + used
+    sec5 = struct.pack("<IQ", 5, len(body5)) + body5
+    return b"r1cs" + bytes([1, 0, 0, 0, 5, 0, 0, 0]) + sec_cons + sec_hdr + sec_w2l + sec4 + sec5
 
 
 def apply_correspondence(c: Con, sm: Dict[int, int]) -> Con:
@@ -986,8 +998,12 @@ def result_to_r1cs(sys_: System, res: Result) -> bytes:
     for k, v in res.signal_map.items():
         w2l[v] = k
     cons = [apply_correspondence(c, res.signal_map) for c in res.constraints]
+    gates = None
+    if sys_.gates is not None:  # r1cs_porting.rs:90-107: signals through the SignalMap (unwrap)
+        used, apps = sys_.gates
+        gates = (used, [(gi, [res.signal_map[x] for x in sig]) for gi, sig in apps])
     return write_r1cs_bytes(sys_.p, cons, wires, sys_.n_pub_out, sys_.n_pub_in, sys_.n_priv_in,
-                            sys_.max_signal, w2l)
+                            sys_.max_signal, w2l, gates)
 
 
 def result_to_sym(sym_lines: List[Tuple[int, int, int, str]], res: Result) -> str:
@@ -1032,7 +1048,23 @@ def read_r1cs_bytes(data: bytes) -> Tuple[System, dict]:
         rows.append(Con(*lcs))
     hdr = dict(fs=fs, n_wires=n_wires, n_labels=n_labels, n_cons=n_cons)
     forb = {0} | set(range(1, n_out + n_pub + 1))
-    return System(p, n_labels, n_out, n_pub, n_prv, forb, rows), hdr
+    gates = None
+    if 4 in secs or 5 in secs:
+        used = data[secs[4][0]: secs[4][0] + secs[4][1]] if 4 in secs else struct.pack("<I", 0)
+        apps = []
+        if 5 in secs:
+            o = secs[5][0]
+            (na,) = struct.unpack_from("<I", data, o)
+            o += 4
+            for _ in range(na):
+                gi, ns = struct.unpack_from("<II", data, o)
+                o += 8
+                sig = list(struct.unpack_from(f"<{ns}Q", data, o))
+                o += 8 * ns
+                apps.append((gi, sig))
+                forb |= set(sig)  # map_to_constraint_list.rs:22-24: custom-gate signals are forbidden
+        gates = (used, apps)
+    return System(p, n_labels, n_out, n_pub, n_prv, forb, rows, gates), hdr
 
 
 def to_json_constraints(constraints: List[Con], sm: Dict[int, int]) -> list:

@@ -3,7 +3,9 @@ exports exactly what the header declares, refuses to compute without a gfx950 GP
 and its host-side pieces -- .r1cs reader/classifier, .r1cs/.sym writers, synthetic generator -- agree
 with the oracle byte for byte.  No GPU compute is called here."""
 import ctypes as C
+import dataclasses
 import os
+import struct
 import re
 import subprocess
 import tempfile
@@ -183,6 +185,78 @@ def test_writer_key_order_random():
         finally:
             lib.refcpu_output_free(out)
         assert open(r1, "rb").read() == R.result_to_r1cs(sys_, res)
+
+
+def _gate_system(seed=57):
+    """A random system with one custom gate (section 4) applied twice (section 5) over signals that
+    occur in its rows: map_tree makes them forbidden (dag/src/map_to_constraint_list.rs:22-24)."""
+    sys_ = rsio.gen_system(seed, R.PRIMES["bn128"], n_sig=80, n_rows=150)
+    used = struct.pack("<I", 1) + b"CMul\x00" + struct.pack("<I", 1) + (7).to_bytes(32, "little")
+    apps = [(0, [10, 11, 12]), (0, [40, 41, 12])]
+    gsig = {x for _, sig in apps for x in sig}
+    return dataclasses.replace(sys_, forbidden=sys_.forbidden | gsig, gates=(used, apps))
+
+
+def test_custom_gate_sections_forbidden_and_rewritten():
+    """Sections 4/5 of an --O0 file: the reader adds the applied signals to `forbidden`; the writer
+    re-emits section 4 and section 5 mapped label -> wire (r1cs_porting.rs:54-121), byte for byte
+    what pyref's restatement writes for its own simplification of the same system."""
+    sys_ = _gate_system()
+    ident = R.Result(sys_.rows, {i: i for i in range(sys_.max_signal)}, sys_.n_priv_in)
+    with tempfile.TemporaryDirectory() as tmp:
+        o0 = _write(tmp, "in.r1cs", R.result_to_r1cs(sys_, ident))
+        back, _ = R.read_r1cs_bytes(open(o0, "rb").read())
+        assert back.forbidden == sys_.forbidden and back.gates == sys_.gates
+        inp = M.Input.read_r1cs(o0)
+        forb = np.ctypeslib.as_array(inp.c.forbidden, shape=(inp.c.n_forbidden,)).tolist()
+        assert forb == sorted(sys_.forbidden)
+        for level in ("O1", "O2"):
+            fl = rsio.flags(level)
+            want = R.simplification(sys_, rsio.py_flags(fl))
+            lib = rsio.oracle_lib()
+            out = C.POINTER(abi.RsOutput)()
+            ms, rounds = C.c_double(), C.c_uint64()
+            assert lib.refcpu_simplify(C.byref(inp.c), C.byref(fl), 1, C.byref(out), C.byref(ms), C.byref(rounds)) == 0
+            r1 = os.path.join(tmp, f"{level}.r1cs")
+            try:
+                abi.check(abi.lib().rs_write_r1cs_gates(r1.encode(), C.byref(inp.c), out, o0.encode()))
+            finally:
+                lib.refcpu_output_free(out)
+            got = open(r1, "rb").read()
+            assert got == R.result_to_r1cs(sys_, want)
+            assert got[8] == 5
+
+
+def test_reader_rejects_truncated_and_malformed_files():
+    """A truncated or malformed .r1cs is RS_E_INVALID, never an over-read (every read is checked
+    against its section and the file)."""
+    sys_ = _gate_system(58)
+    ident = R.Result(sys_.rows, {i: i for i in range(sys_.max_signal)}, sys_.n_priv_in)
+    data = R.result_to_r1cs(sys_, ident)
+    with tempfile.TemporaryDirectory() as tmp:
+        cuts = sorted(set([0, 4, 11, 12, 20, 23, 40, 100, len(data) // 3, len(data) // 2, len(data) - 9,
+                           len(data) - 1]))
+        for n in cuts:
+            path = _write(tmp, "t.r1cs", data[:n])
+            with pytest.raises(abi.RsError) as e:
+                M.Input.read_r1cs(path)
+            assert e.value.code == -1, n
+        # a section size beyond the file
+        bad = bytearray(data)
+        struct.pack_into("<Q", bad, 16, len(data) * 2)
+        with pytest.raises(abi.RsError):
+            M.Input.read_r1cs(_write(tmp, "s.r1cs", bytes(bad)))
+        # a constraint entry count beyond its section
+        bad = bytearray(data)
+        struct.pack_into("<I", bad, 24, 0x7fffffff)
+        with pytest.raises(abi.RsError):
+            M.Input.read_r1cs(_write(tmp, "c.r1cs", bytes(bad)))
+        # a signal id >= n_labels
+        bad = bytearray(data)
+        struct.pack_into("<I", bad, 28, 0xfffffff0)
+        with pytest.raises(abi.RsError):
+            M.Input.read_r1cs(_write(tmp, "k.r1cs", bytes(bad)))
+        assert M.Input.read_r1cs(_write(tmp, "ok.r1cs", data)).c.max_signal == sys_.max_signal
 
 
 def test_cli_usage():

@@ -202,3 +202,19 @@ def test_refcpu_threads_deterministic():
     h = rsio.InputHolder(sys_)
     outs = [rsio.oracle_run(h.inp, rsio.flags("O2"), t)[0] for t in (1, 2, 8)]
     assert outs[0] == outs[1] == outs[2]
+
+
+def test_asan_ubsan_check(tmp_path):
+    """the oracle and the product's host-side pieces (--O0 reader, writers, generator)
+    built with -fsanitize=address,undefined and driven over every generator kind, three flag levels,
+    1/3 oracle threads, and every truncation of an .r1cs (oracle/asan_check.cpp)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "oracle"), "asan"])
+    r = subprocess.run([os.path.join(root, "oracle", "_ref", "asan_check"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "asan_check: OK" in r.stdout
