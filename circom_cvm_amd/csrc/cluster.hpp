@@ -167,7 +167,8 @@ template <uint32_t CAP, uint32_t CHUNK>
 __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, const uint32_t *ids, uint64_t n_ids,
                                                        const uint64_t *q_off, const uint32_t *stream,
                                                        const uint32_t *srow, uint32_t *next, uint32_t *perm,
-                                                       const uint32_t *n_ordered, int old_heur) {
+                                                       const uint32_t *n_ordered, int old_heur,
+                                                       unsigned long long *prof = nullptr) {
   constexpr uint32_t kClChunk = CHUNK;
   __shared__ uint16_t C2[CAP], T[CAP];
   __shared__ uint32_t S[kClChunk];
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
       continue;
     }
     const uint64_t q0 = q_off[b], q1 = q_off[b + n];
+    const unsigned long long t_0 = prof ? wall_clock64() : 0ull;
     uint32_t *N = next + b;
     int32_t t = -1;  // lane 0: current row
     uint32_t tail = 0;
@@ -227,6 +229,107 @@ __global__ __launch_bounds__(256) void k_cl_replay_lds(const uint64_t *cl_off, c
     }
     __syncthreads();
     for (uint32_t i = tid; i < n; i += nt) perm[b + i] = srow[b + T[i]];
+    if (prof && tid == 0) {  // RS_PROF: (cluster, rows, pairs, 100 MHz ticks)
+      prof[4 * ci] = c;
+      prof[4 * ci + 1] = n;
+      prof[4 * ci + 2] = q1 - q0;
+      prof[4 * ci + 3] = wall_clock64() - t_0;
+    }
+    __syncthreads();
+  }
+}
+
+// One-wave replay (kClSmall < n <= CAP), the same arena merges as k_cl_replay_lds with the finds of a
+// row done in parallel: the stream is read 64 entries at a time (one per lane, the next window
+// prefetched), each row's entries in the window find their roots together (path halving; concurrent
+// halving writes only ever store ancestors), then the row's links run in entry order -- one LDS
+// read pair per entry instead of a whole dependent find chain.  Finds of a row see every link of
+// the earlier rows; a root linked earlier in the same row is recognised by C2[root] != root, a root
+// equal to the current row by r == t.
+template <uint32_t CAP>
+__global__ __launch_bounds__(64) void k_cl_replay_wave(const uint64_t *cl_off, const uint32_t *ids, uint64_t n_ids,
+                                                       const uint64_t *q_off, const uint32_t *stream,
+                                                       const uint32_t *srow, uint32_t *next, uint32_t *perm,
+                                                       const uint32_t *n_ordered, int old_heur,
+                                                       unsigned long long *prof = nullptr) {
+  __shared__ uint16_t C2[CAP], T[CAP];
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = cl_off[c];
+    const uint32_t n = (uint32_t)(cl_off[c + 1] - b);
+    if (d_cl_order_free(n, old_heur, n_ordered, c)) {
+      for (uint32_t i = lane; i < n; i += 64) perm[b + i] = srow[b + i];
+      continue;
+    }
+    const uint64_t q0 = q_off[b], q1 = q_off[b + n];
+    const unsigned long long t_0 = prof ? wall_clock64() : 0ull;
+    uint32_t *N = next + b;
+    int32_t t = -1;     // current row (uniform)
+    uint32_t tail = 0;  // its list tail (uniform)
+    uint32_t e_nx = q0 + lane < q1 ? stream[q0 + lane] : 0u;
+    for (uint64_t q = q0; q < q1; q += 64) {
+      const uint32_t e = e_nx;
+      const bool valid = q + lane < q1;
+      e_nx = q + 64 + lane < q1 ? stream[q + 64 + lane] : 0u;
+      const uint64_t starts = __ballot(valid && (e & kClRowBit));
+      const uint32_t cnt = (uint32_t)min<uint64_t>(64, q1 - q);
+      uint32_t a = 0;
+      while (a < cnt) {
+        const uint64_t later = a >= 63 ? 0ull : (starts & ~((2ull << a) - 1ull));
+        const uint32_t bnd = later ? (uint32_t)(__ffsll((long long)later) - 1) : cnt;
+        if ((starts >> a) & 1ull) {  // a new row
+          if (t >= 0 && lane == 0) T[t] = (uint16_t)tail;
+          ++t;
+          if (lane == 0) { C2[t] = (uint16_t)t; N[t] = RS_NONE; }
+          tail = (uint32_t)t;
+          wave_sync();
+        }
+        uint32_t r = e & ~kClRowBit;
+        const bool mine = lane >= a && lane < bnd && r != kClNoPrev;
+        if (mine) {
+          uint32_t p2 = C2[r];
+          while (p2 != r) {  // path halving
+            const uint32_t g = C2[p2];
+            C2[r] = (uint16_t)g;
+            r = p2 == g ? p2 : g;
+            p2 = C2[r];
+          }
+        }
+        wave_sync();
+        uint64_t mm = __ballot(mine);
+        while (mm) {
+          const int l = __ffsll((long long)mm) - 1;
+          mm &= mm - 1;
+          const uint32_t rr = (uint32_t)__shfl((int)r, l);
+          const uint32_t cr = C2[rr], tr = T[rr];
+          if (rr == (uint32_t)t || cr != rr) continue;  // already in this row's list
+          if (lane == 0) {
+            N[tail] = rr;
+            C2[rr] = (uint16_t)t;
+          }
+          tail = tr;
+          wave_sync();
+        }
+        a = bnd;
+      }
+    }
+    if (lane == 0 && t >= 0) T[t] = (uint16_t)tail;
+    __syncthreads();  // N (global) complete
+    for (uint32_t i = lane; i < n; i += 64) { const uint32_t x = N[i]; C2[i] = (uint16_t)(x == RS_NONE ? 0xffffu : x); }
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t x = n - 1, qq = 0;
+      while (x != 0xffffu) { T[qq++] = (uint16_t)x; x = C2[x]; }
+    }
+    __syncthreads();
+    for (uint32_t i = lane; i < n; i += 64) perm[b + i] = srow[b + T[i]];
+    if (prof && lane == 0) {  // RS_PROF: (cluster, rows, pairs, 100 MHz ticks)
+      prof[4 * ci] = c;
+      prof[4 * ci + 1] = n;
+      prof[4 * ci + 2] = q1 - q0;
+      prof[4 * ci + 3] = wall_clock64() - t_0;
+    }
     __syncthreads();
   }
 }

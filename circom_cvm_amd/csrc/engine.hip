@@ -800,19 +800,29 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   launch(st, k_cl_replay_lane, n_cl, (const uint64_t *)D.cl_off, n_cl, (const uint64_t *)q_off,
          (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm, (const uint32_t *)n_ordered,
          old_heur);
+  unsigned long long *rprof = nullptr;
   if (hc[4]) {  // (kClMid, kClLds]: the largest LDS footprint, on the second stream (the few
                 // largest clusters' serial replays overlap everything else's)
     HC(hipEventRecord(E->evx[6], st));
     HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
-    hipLaunchKernelGGL((k_cl_replay_lds<kClLds, kClChunk>), dim3((unsigned)std::min<uint64_t>(hc[4], 4096)), dim3(256), 0, E->st2,
+    if (g_prof_env) rprof = A.get<unsigned long long>("cl.rprof", 4 * hc[4]);
+    hipLaunchKernelGGL((k_cl_replay_wave<kClLds>), dim3((unsigned)std::min<uint64_t>(hc[4], 4096)), dim3(64), 0, E->st2,
                        (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[4],
                        (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
-                       (const uint32_t *)n_ordered, old_heur);
+                       (const uint32_t *)n_ordered, old_heur, rprof);
     HC(hipGetLastError());
+    if (rprof) {
+      std::vector<unsigned long long> rp(4 * hc[4]);
+      HC(hipMemcpyAsync(rp.data(), rprof, 8 * rp.size(), hipMemcpyDeviceToHost, E->st2));
+      HC(hipStreamSynchronize(E->st2));
+      for (uint64_t i = 0; i < hc[4]; ++i)
+        fprintf(stderr, "[rs-prof] replay #%llu: cluster %llu rows %llu pairs %llu %.1f us\n", (unsigned long long)i,
+                rp[4 * i], rp[4 * i + 1], rp[4 * i + 2], rp[4 * i + 3] / 100.0);
+    }
   }
   if (hc[2] > hc[4]) {  // (kClSmall, kClMid]
     const uint64_t nm = hc[2] - hc[4];
-    hipLaunchKernelGGL((k_cl_replay_lds<kClMid, 1024>), dim3((unsigned)std::min<uint64_t>(nm, 16384)), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_cl_replay_wave<kClMid>), dim3((unsigned)std::min<uint64_t>(nm, 16384)), dim3(64), 0, st,
                        (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3] + hc[4]), nm,
                        (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
                        (const uint32_t *)n_ordered, old_heur);
@@ -972,6 +982,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.row_len = E->A.get<uint32_t>("el.row_len", n_slots);
 
     a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", kProfWords * n_big) : nullptr;
+    if (a.prof) HC(hipMemsetAsync(a.prof, 0, 8 * kProfWords * n_big, E->st));
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
     HC(hipMemsetAsync(a.bytes, 0, 40, E->st));
@@ -1024,8 +1035,18 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_prep, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));
-        hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        HC(hipGetLastError());
+        {  // the ordered loop with LDS-resident signal state; clusters that do not fit its table
+           // follow on k_big_main<512> (fb_only)
+          ElimArgs al = a;
+          al.lds_fb = E->A.get<uint8_t>("el.lds_fb", n_head);
+          static const bool no_lds = getenv("RS_NO_LDS_HEAD") != nullptr;  // diagnostic
+          if (no_lds) HC(hipMemsetAsync(al.lds_fb, 1, n_head, E->st2));
+          else hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, al, (const uint32_t *)d_big, n_head);
+          HC(hipGetLastError());
+          al.fb_only = 1;
+          hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, al, (const uint32_t *)d_big, n_head);
+          HC(hipGetLastError());
+        }
         HC(hipEventRecord(E->evx[3], E->st2));
         hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -1035,6 +1056,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         // the Kahn levels and the emission follow once the rest is enqueued (the level loop waits)
       }
+      if (n_head && getenv("RS_HEAD_ALONE")) HC(hipStreamWaitEvent(E->st, E->evx[3], 0));  // diagnostic
       if (n_tail) {
         // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
         // per-lane pool chunks are bounded by the grid size
@@ -1198,6 +1220,16 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     if (a.prof) {
       std::vector<unsigned long long> pf(kProfWords * n_big);
       HC(hipMemcpy(pf.data(), a.prof, 8 * pf.size(), hipMemcpyDeviceToHost));
+      {  // head workgroups' start offsets (k_big_main_lds)
+        unsigned long long t0m = ~0ull;
+        for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 16); ++q)
+          if (pf[kProfWords * q + 22]) t0m = std::min(t0m, pf[kProfWords * q + 22]);
+        fprintf(stderr, "[rs-prof] head starts (us after the first):");
+        for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 16); ++q)
+          fprintf(stderr, " %llu:%.0f/%.0f", (unsigned long long)pf[kProfWords * q],
+                  pf[kProfWords * q + 22] ? (pf[kProfWords * q + 22] - t0m) / 100.0 : -1.0, pf[kProfWords * q + 5] / 100.0);
+        fprintf(stderr, "\n");
+      }
       std::vector<uint64_t> ix(n_big);
       for (uint64_t i = 0; i < n_big; ++i) ix[i] = i;
       std::sort(ix.begin(), ix.end(), [&](uint64_t x, uint64_t y) {
@@ -1218,10 +1250,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         unsigned long long *p = &pf[kProfWords * ix[q]];
         fprintf(stderr, "[rs-debug]   n=%llu m=%llu main_rows=%llu  prep %.1f / main %.1f / normalize %.1f / compose %.1f us"
                 "  [kclocks: merges packed %llu (lanes %.1f) reg %llu lds %llu | row starts %.1f pivot %.1f holder %.1f "
-                "merge %.1f (packed: loads %.1f search+product %.1f hand-off %.1f combine %.1f) new-sub %.1f us] levels %llu\n",
+                "merge %.1f (packed: loads %.1f search+product %.1f hand-off %.1f combine %.1f) new-sub %.1f us] levels %llu touched %llu\n",
                 p[0], p[1], p[2], p[4] / 100.0, p[5] / 100.0, p[6] / 100.0, p[7] / 100.0,
                 p[8], p[8] ? (double)p[12] / p[8] : 0.0, p[9], p[10], p[3] / 100.0, p[13] / 100.0, p[14] / 100.0,
-                p[15] / 100.0, p[16] / 100.0, p[17] / 100.0, p[18] / 100.0, p[19] / 100.0, p[11] / 100.0, p[20]);
+                p[15] / 100.0, p[16] / 100.0, p[17] / 100.0, p[18] / 100.0, p[19] / 100.0, p[11] / 100.0, p[20], p[21]);
       }
     }
     eo.n_sub.resize(eo.n_clusters);
@@ -2313,7 +2345,28 @@ int rs_engine_create(int device, rs_engine **eng) {
     }
     std::unique_ptr<rs_engine> E(new rs_engine());
     E->device = device;
-    HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
+    {
+      // The main stream leaves kHeadCUs compute units to the second stream: the head's ordered loop
+      // (k_big_main_lds, one workgroup of ~154 KB LDS per cluster) finds whole CUs free there
+      // instead of waiting for the tail kernels to drain a CU (RS_HEAD_CUS overrides; 0 = no mask).
+      uint32_t head_cus = 16;
+      if (const char *hc = getenv("RS_HEAD_CUS")) head_cus = (uint32_t)std::min<unsigned long>(strtoul(hc, nullptr, 10), 64ul);
+      const uint32_t n_cu = (uint32_t)prop.multiProcessorCount;
+      bool masked = false;
+      if (head_cus && n_cu >= 4 * head_cus) {
+        std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
+        for (uint32_t cu = 0; cu < n_cu - head_cus; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+        masked = hipExtStreamCreateWithCUMask(&E->st, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+        if (masked && g_prof_env) {
+          std::vector<uint32_t> got(mask.size(), 0u);
+          (void)hipExtStreamGetCUMask(E->st, (uint32_t)got.size(), got.data());
+          fprintf(stderr, "[rs-prof] main stream CU mask (%u CUs):", n_cu);
+          for (uint32_t w : got) fprintf(stderr, " %08x", w);
+          fprintf(stderr, "\n");
+        }
+      }
+      if (!masked) HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
+    }
     HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));

@@ -6,4 +6,4 @@ set -e
 cd "$(dirname "$0")/.."
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared --gpu-max-threads-per-block=256 -DRS_KCLOCKS \
   -o circom_cvm_amd/librs_simplify_kclk.so circom_cvm_amd/csrc/engine.hip circom_cvm_amd/csrc/r1cs_io.cpp \
-  circom_cvm_amd/csrc/synth.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+  circom_cvm_amd/csrc/synth.cpp circom_cvm_amd/csrc/host_common.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
