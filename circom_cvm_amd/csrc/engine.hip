@@ -133,7 +133,7 @@ struct rs_engine {
   int device = 0;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // the largest clusters' elimination chain runs here, beside the rest
-  hipEvent_t evx[10] = {};    // [0] join-in, [1..4] head chain, [5] after the lane kernel, [6..7] the
+  hipEvent_t evx[11] = {};    // [0] join-in, [1..4] head chain, [5] after the lane kernel, [6..7] the
                               // largest replays' fork / join, [8..9] the overlapped frames pass
   Arena A;
   bool loaded = false;
@@ -166,12 +166,17 @@ struct rs_engine {
   uint32_t *heap_k = nullptr;  // storage-row heap (grows, reused across runs)
   Fe *heap_v = nullptr;
   uint64_t heap_cap = 0;
-  // pipelined load (rs_engine_simplify): input groups 0 = cons_eq + eq, 1 = linear, 2 = non-linear
-  // land on the copy stream, each validated there; the run waits for a group where it first needs it
+  // pipelined load: input groups 0 = cons_eq + eq, 1 = linear row pointers + keys, 2 = linear
+  // values, 3 = non-linear land on the copy stream, each validated there; the run waits for a group
+  // where it first needs it.  rs_engine_simplify stages the linear keys before their values
+  // (`staged`): build_clusters can start on the keys while the values are still on the way, and the
+  // eq block's values stay on the host (`hin`, valid for the call) -- the device never needs them.
   hipStream_t stc = nullptr;
-  hipEvent_t ev_grp[3] = {};
-  bool pending[3] = {false, false, false};
-  int *h_vflag = nullptr;  // pinned: per-group validation verdicts (D2H after each group's checks)
+  hipEvent_t ev_grp[4] = {};
+  bool pending[4] = {false, false, false, false};
+  int *h_vflag = nullptr;  // pinned: per-group verdicts [2g] row pointers, [2g + 1] rows; [8] linear keys unsorted
+  bool staged = false;
+  const rs_input *hin = nullptr;
   unsigned long long *h_lvl = nullptr;  // pinned: frontier counts of the head's composition levels
   hipEvent_t ev_lvl[4] = {};
   double h2d_wait_ms = 0;
@@ -189,7 +194,9 @@ namespace rs {
 // H2D of one CSR block on the copy stream.  The row pointers are not trusted: the block's
 // validation (k_check_ptr) checks ptr[0] = 0, monotonicity and ptr[n] = nnz on the device before
 // anything reads a row.
-static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, const char *name) {
+// what of a block to send: everything, the row pointers + keys, or the values alone
+enum UpPart { kUpAll = 0, kUpKeys = 1, kUpVals = 2 };
+static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, const char *name, int part = kUpAll) {
   if (src.n_rows && !src.ptr) throw RsError(RS_E_INVALID, std::string(name) + ": rows without a ptr array");
   if (src.nnz && (!src.col || !src.val)) throw RsError(RS_E_INVALID, std::string(name) + ": entries without col/val");
   if (src.n_rows > 0xfffffff0ull || src.nnz > (1ull << 40)) throw RsError(RS_E_INVALID, std::string(name) + ": block too large");
@@ -200,22 +207,27 @@ static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, co
   dst.key = E->A.get<uint32_t>(nm + ".key", dst.nnz);
   dst.val = E->A.get<Fe>(nm + ".val", dst.nnz);
   hipStream_t s = E->stc;
-  if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, s));
-  else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), s));
-  if (dst.nnz) {
-    HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, s));
-    HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, s));
+  if (part != kUpVals) {
+    if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, s));
+    else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), s));
+    if (dst.nnz) HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, s));
   }
+  if (part != kUpKeys && dst.nnz) HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, s));
 }
 
 // ---------------------------------------------------------------- pipelined load
-static const char *kGroupName[3] = {"cons_eq/eq", "linear", "non-linear"};
+static const char *kGroupName[4] = {"cons_eq/eq", "linear", "linear", "non-linear"};
 
 // Validates the header fields of `in` and enqueues the H2D of every block on the copy stream in
-// the order the run consumes them -- group 0 (cons_eq, eq), 1 (linear), 2 (nl_a, nl_b, nl_c) --
-// each group followed by its device checks (k_check_ptr, then k_sort_validate, which also sorts
-// the rows) and the D2H of its two verdict words into pinned memory.
-static void load_enqueue(rs_engine *E, const rs_input *in) {
+// the order the run consumes them, each group followed by its device checks and the D2H of its
+// verdict words into pinned memory:
+//   0: cons_eq (k_check_ptr, k_sort_validate, which also sorts rows), eq (staged: row pointers and
+//      keys only, k_check_keys -- eq_simplification reads no value; the rows it keeps as they are
+//      take their values from the host input);
+//   1: linear (staged: row pointers + keys, k_check_keys also flags unsorted rows; else all of it);
+//   2: linear values (staged; k_sort_validate, which sorts rows the keys left unsorted);
+//   3: nl_a, nl_b, nl_c.
+static void load_enqueue(rs_engine *E, const rs_input *in, bool staged) {
   uint64_t p[4];
   if (!prime_of(in, p)) throw RsError(RS_E_INVALID, "unknown prime");
   if (in->max_signal == 0 || in->max_signal > 0xfffffff0ull) throw RsError(RS_E_INVALID, "bad max_signal");
@@ -242,29 +254,63 @@ static void load_enqueue(rs_engine *E, const rs_input *in) {
   E->n_priv_in = in->n_priv_in;
   E->forbidden.swap(forb);
   E->h2d_wait_ms = 0;
-  int *vf = E->A.get<int>("vflag", 6);  // [2g]: row pointers of group g, [2g + 1]: its rows
-  HC(hipMemsetAsync(vf, 0, 24, E->stc));
-  struct G {
-    const rs_lc *src;
-    rs_engine::Blk *dst;
-    const char *nm;
+  E->staged = staged;
+  E->hin = staged ? in : nullptr;
+  int *vf = E->A.get<int>("vflag", 10);
+  HC(hipMemsetAsync(vf, 0, 40, E->stc));
+  hipStream_t s = E->stc;
+  auto check = [&](const rs_engine::Blk &B, int g) {
+    launch(s, k_check_ptr, B.n + 1, (const uint64_t *)B.ptr, B.n, B.nnz, vf + 2 * g);
   };
-  const G groups[3][3] = {{{&in->cons_eq, &E->ce, "in.ce"}, {&in->eq, &E->eq, "in.eq"}, {nullptr, nullptr, nullptr}},
-                          {{&in->linear, &E->lin, "in.lin"}, {nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}},
-                          {{&in->nl_a, &E->na, "in.na"}, {&in->nl_b, &E->nb, "in.nb"}, {&in->nl_c, &E->nc, "in.nc"}}};
-  for (int g = 0; g < 3; ++g) {
-    for (const G &x : groups[g])
-      if (x.src) upload_block(E, *x.src, *x.dst, x.nm);
-    for (const G &x : groups[g])
-      if (x.src) launch(E->stc, k_check_ptr, x.dst->n + 1, (const uint64_t *)x.dst->ptr, x.dst->n, x.dst->nnz, vf + 2 * g);
-    for (const G &x : groups[g])
-      if (x.src && x.dst->n)
-        launch(E->stc, k_sort_validate, x.dst->n, E->F, (const uint64_t *)x.dst->ptr, x.dst->key, x.dst->val, x.dst->n, E->S,
-               (const int *)(vf + 2 * g), vf + 2 * g + 1);
-    HC(hipMemcpyAsync(E->h_vflag + 2 * g, vf + 2 * g, 8, hipMemcpyDeviceToHost, E->stc));
-    HC(hipEventRecord(E->ev_grp[g], E->stc));
+  // k_sort_validate of block B: skipped when the row pointers' word `pw` is set, verdict into `ew`
+  auto sort_validate = [&](const rs_engine::Blk &B, int pw, int ew) {
+    if (B.n) launch(s, k_sort_validate, B.n, E->F, (const uint64_t *)B.ptr, B.key, B.val, B.n, E->S, (const int *)(vf + pw), vf + ew);
+  };
+  auto verdict = [&](int g, int words) {
+    HC(hipMemcpyAsync(E->h_vflag + 2 * g, vf + 2 * g, 4 * words, hipMemcpyDeviceToHost, s));
+    HC(hipEventRecord(E->ev_grp[g], s));
     E->pending[g] = true;
+  };
+  // group 0
+  upload_block(E, in->cons_eq, E->ce, "in.ce");
+  upload_block(E, in->eq, E->eq, "in.eq", staged ? kUpKeys : kUpAll);
+  check(E->ce, 0);
+  check(E->eq, 0);
+  sort_validate(E->ce, 0, 1);
+  if (staged) {
+    if (E->eq.n) launch(s, k_check_keys, E->eq.n, (const uint64_t *)E->eq.ptr, (const uint32_t *)E->eq.key, E->eq.n, E->S,
+                        (const int *)vf, vf + 1, (int *)nullptr);
+  } else {
+    sort_validate(E->eq, 0, 1);
   }
+  verdict(0, 2);
+  // groups 1 and 2
+  upload_block(E, in->linear, E->lin, "in.lin", staged ? kUpKeys : kUpAll);
+  check(E->lin, 1);
+  if (staged) {
+    if (E->lin.n) launch(s, k_check_keys, E->lin.n, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, E->lin.n, E->S,
+                         (const int *)(vf + 2), vf + 3, vf + 8);
+    HC(hipMemcpyAsync(E->h_vflag + 8, vf + 8, 4, hipMemcpyDeviceToHost, s));
+    verdict(1, 2);
+    upload_block(E, in->linear, E->lin, "in.lin", kUpVals);
+    sort_validate(E->lin, 2, 5);
+    HC(hipMemcpyAsync(E->h_vflag + 4, vf + 2, 4, hipMemcpyDeviceToHost, s));  // the pointers' verdict
+    HC(hipMemcpyAsync(E->h_vflag + 5, vf + 5, 4, hipMemcpyDeviceToHost, s));
+    HC(hipEventRecord(E->ev_grp[2], s));
+    E->pending[2] = true;
+  } else {
+    sort_validate(E->lin, 2, 3);
+    E->h_vflag[8] = 0;
+    verdict(1, 2);
+  }
+  // group 3
+  const rs_lc *nl_src[3] = {&in->nl_a, &in->nl_b, &in->nl_c};
+  rs_engine::Blk *nl_dst[3] = {&E->na, &E->nb, &E->nc};
+  const char *nl_nm[3] = {"in.na", "in.nb", "in.nc"};
+  for (int q = 0; q < 3; ++q) upload_block(E, *nl_src[q], *nl_dst[q], nl_nm[q]);
+  for (int q = 0; q < 3; ++q) check(*nl_dst[q], 3);
+  for (int q = 0; q < 3; ++q) sort_validate(*nl_dst[q], 6, 7);
+  verdict(3, 2);
   E->loaded = true;
 }
 
@@ -287,7 +333,7 @@ static void load_wait(rs_engine *E, int g) {
   HC(hipStreamWaitEvent(E->st, E->ev_grp[g], 0));
 }
 static void load_wait_all(rs_engine *E) {
-  for (int g = 0; g < 3; ++g) load_wait(E, g);
+  for (int g = 0; g < 4; ++g) load_wait(E, g);
 }
 // After a failed call: the copy stream may still be reading the caller's buffers.
 static void load_abort(rs_engine *E) {
@@ -434,7 +480,7 @@ __global__ void k_eq_bf_info(const uint32_t *bf, uint64_t n, const uint64_t *ptr
     o[0] = r;
     o[1] = ((uint64_t)k1 << 32) | k0;
     o[2] = cnt[x];
-    for (int t = 0; t < 4; ++t) { o[3 + t] = val[p0].l[t]; o[7 + t] = val[p0 + 1].l[t]; }
+    for (int t = 0; t < 4; ++t) { o[3 + t] = val ? val[p0].l[t] : 0; o[7 + t] = val ? val[p0 + 1].l[t] : 0; }
   }
 }
 __global__ void k_flag_linear(const uint32_t *la, const uint32_t *lb, uint64_t n, uint64_t *flag_lin, uint64_t *flag_nl) {
@@ -909,9 +955,12 @@ using HeadOverlap = std::function<void(const uint32_t *head_ids, uint64_t n_head
 
 static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
                                       int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted,
-                                      const HeadOverlap *overlap = nullptr) {
+                                      const HeadOverlap *overlap = nullptr,
+                                      const std::function<void()> *before_elim = nullptr) {
   double t0 = now_ms();
   DevClusters D = gpu_clusters(E, view, old_heur, d_forb, eo);
+  // keys-first rows: their values now (main stream; every elimination kernel is ordered after it)
+  if (before_elim) (*before_elim)();
   double t1 = now_ms();
   E->stats.cluster_ms += t1 - t0;
   const uint64_t n_slots = D.n_slots, tot_nnz = D.tot_nnz;
@@ -1035,18 +1084,12 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hipLaunchKernelGGL(k_big_prep, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));
-        {  // the ordered loop with LDS-resident signal state; clusters that do not fit its table
-           // follow on k_big_main<512> (fb_only)
-          ElimArgs al = a;
-          al.lds_fb = E->A.get<uint8_t>("el.lds_fb", n_head);
-          static const bool no_lds = getenv("RS_NO_LDS_HEAD") != nullptr;  // diagnostic
-          if (no_lds) HC(hipMemsetAsync(al.lds_fb, 1, n_head, E->st2));
-          else hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, al, (const uint32_t *)d_big, n_head);
-          HC(hipGetLastError());
-          al.fb_only = 1;
-          hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, al, (const uint32_t *)d_big, n_head);
-          HC(hipGetLastError());
-        }
+        HC(hipEventRecord(E->evx[10], E->st2));
+        // the ordered loop with LDS-resident signal state (RS_NO_LDS_HEAD: k_big_main<512>, diagnostic)
+        static const bool no_lds = getenv("RS_NO_LDS_HEAD") != nullptr;
+        if (no_lds) hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        else hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
         hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -1062,6 +1105,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         // per-lane pool chunks are bounded by the grid size
         const unsigned gb = (unsigned)std::min<uint64_t>(n_tail, 2048), gm = (unsigned)std::min<uint64_t>(n_tail, 8192);
         const uint32_t *ids = d_big + n_head;
+        // the tail starts once the head's preparation is done: the tail's short prep workgroups come
+        // first, so the head's large-LDS workgroups find free CUs before the tail's ordered loop
+        // (8192 long-lived workgroups) holds every CU
+        if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[10], 0));
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         HC(hipEventRecord(E->ev5, E->st));
@@ -1558,13 +1605,29 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (nbf) {  // rows with both ends forbidden: kept as is when they are a cluster of their own
       std::vector<uint64_t> rec(11 * (uint64_t)nbf);
       uint64_t *d_rec = A.get<uint64_t>("eq.bfrec", 11 * (uint64_t)nbf);
+      // staged load: the eq values were never uploaded; these rows take theirs from the host input
       launch(st, k_eq_bf_info, nbf, (const uint32_t *)bf, (uint64_t)nbf, (const uint64_t *)E->eq.ptr,
-             (const uint32_t *)E->eq.key, (const Fe *)E->eq.val, (const uint32_t *)uf, (const uint32_t *)cnt, d_rec);
+             (const uint32_t *)E->eq.key, E->hin ? (const Fe *)nullptr : (const Fe *)E->eq.val, (const uint32_t *)uf,
+             (const uint32_t *)cnt, d_rec);
       HC(hipMemcpyAsync(rec.data(), d_rec, 88 * (uint64_t)nbf, hipMemcpyDeviceToHost, st));
       HC(hipStreamSynchronize(st));
       for (uint32_t q = 0; q < nbf; ++q) {
-        const uint64_t *x = &rec[11 * (uint64_t)q];
+        uint64_t *x = &rec[11 * (uint64_t)q];
         if (x[2] != 1) continue;  // a single-constraint cluster with both ends forbidden: kept as is
+        if (E->hin) {
+          const rs_lc &H = E->hin->eq;
+          const uint64_t p0 = H.ptr[x[0]];
+          for (int t = 0; t < 4; ++t) { x[3 + t] = H.val[4 * p0 + t]; x[7 + t] = H.val[4 * (p0 + 1) + t]; }
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const uint64_t *v = x + 3 + 4 * e2;
+            if ((v[0] | v[1] | v[2] | v[3]) == 0 || geq4(v, E->prime))
+              throw RsError(RS_E_INVALID, "eq block: zero or non-canonical value");
+          }
+          if ((uint32_t)x[1] > (uint32_t)(x[1] >> 32)) {  // the device sorted rows; these are as given
+            x[1] = (x[1] << 32) | (x[1] >> 32);
+            for (int t = 0; t < 4; ++t) std::swap(x[3 + t], x[7 + t]);
+          }
+        }
         EqCon e;
         e.order = (int64_t)x[0];
         e.f = 0;
@@ -1580,7 +1643,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   }
 
   // working copies (Montgomery): cons_eq (C), linear (C, one spare slot per row)
-  load_wait(E, 1);
   DRows ce{}, lin{};
   ce.n = E->ce.n;
   ce.off = A.get<uint64_t>("ce.off", ce.n);
@@ -1594,8 +1656,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   lin.len = A.get<uint32_t>("lin.len", lin.n);
   lin.key = A.get<uint32_t>("lin.key", E->lin.nnz + lin.n);
   lin.val = A.get<Fe>("lin.val", E->lin.nnz + lin.n);
-  if (lin.n) launch(st, k_make_ragged, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
-                    lin.n, (uint64_t)1, lin.off, lin.len, lin.key, lin.val);
   if (ce.n) launch(st, k_rename_rows, ce.n, E->F, ce, (const int32_t *)eq_rep);
   if (E->log_on && ce.n) {  // log_substitutions (:271), row order
     uint32_t *lsig = A.get<uint32_t>("lg.cesig", ce.n);
@@ -1650,7 +1710,70 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       }
     }
   }
-  if (lin.n) launch(st, k_linear_frames12, lin.n, E->F, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val);
+  // the linear rows: keys first when their values are still on the way (staged load, sorted rows,
+  // no renaming collision) -- build_clusters needs keys only; the values follow in
+  // `linear_values`, run just before the elimination reads them
+  bool keys_first = false;
+  load_wait(E, 1);
+  uint8_t *lin_fixed = nullptr;
+  if (E->staged && apply_linear && lin.n && !E->h_vflag[8]) {
+    // rows that keys alone cannot settle (a renaming collision, or no non-constant key left) take
+    // their values from the host input now (hundreds of rows out of millions, typically); the rest
+    // wait for their values
+    const uint64_t unc_cap = std::max<uint64_t>(1024, lin.n / 16);
+    int *unc = A.get<int>("lin.unc", 1);
+    uint32_t *unc_list = A.get<uint32_t>("lin.unc_list", unc_cap);
+    lin_fixed = A.get<uint8_t>("lin.fixed", lin.n);
+    HC(hipMemsetAsync(unc, 0, 4, st));
+    HC(hipMemsetAsync(lin_fixed, 0, lin.n, st));
+    launch(st, k_lin_keyframes, lin.n, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, lin.n, lin,
+           (const int32_t *)eq_rep, (const uint8_t *)ce_has, unc, unc_list, unc_cap);
+    int hu = 0;
+    HC(hipMemcpyAsync(&hu, unc, 4, hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    keys_first = (uint64_t)hu <= unc_cap;
+    if (keys_first && hu) {
+      std::vector<uint32_t> rows(hu);
+      HC(hipMemcpyAsync(rows.data(), unc_list, 4 * (uint64_t)hu, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      const rs_lc &H = E->hin->linear;
+      std::vector<uint64_t> hp(1, 0);
+      std::vector<uint32_t> hk;
+      std::vector<uint64_t> hv;
+      for (uint32_t r : rows) {
+        const uint64_t b = H.ptr[r], e = H.ptr[r + 1];
+        hk.insert(hk.end(), H.col + b, H.col + e);
+        hv.insert(hv.end(), H.val + 4 * b, H.val + 4 * e);
+        hp.push_back(hk.size());
+      }
+      uint64_t *d_hp = A.get<uint64_t>("lin.fx_ptr", hp.size());
+      uint32_t *d_hk = A.get<uint32_t>("lin.fx_key", std::max<size_t>(hk.size(), 1));
+      Fe *d_hv = A.get<Fe>("lin.fx_val", std::max<size_t>(hk.size(), 1));
+      uint32_t *d_rows = A.get<uint32_t>("lin.fx_rows", hu);
+      h2d(E, d_hp, hp.data(), 8 * hp.size());
+      h2d(E, d_hk, hk.data(), 4 * hk.size());
+      h2d(E, d_hv, hv.data(), 8 * hv.size());
+      h2d(E, d_rows, rows.data(), 4 * rows.size());
+      launch(st, k_lin_fixrows, (uint64_t)hu, E->F, (const uint64_t *)d_hp, (const uint32_t *)d_hk, (const Fe *)d_hv,
+             (const uint32_t *)d_rows, (uint64_t)hu, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has,
+             (const Fe *)ce_val, lin_fixed);
+    }
+    if (g_prof_env) fprintf(stderr, "[rs-prof] keys-first: %d rows settled from host values\n", hu);
+  }
+  if (!keys_first) {
+    load_wait(E, 2);
+    if (lin.n) {
+      launch(st, k_make_ragged, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
+             lin.n, (uint64_t)1, lin.off, lin.len, lin.key, lin.val);
+      launch(st, k_linear_frames12, lin.n, E->F, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val);
+    }
+  }
+  const std::function<void()> linear_values = [&]() {
+    load_wait(E, 2);
+    launch(st, k_lin_valframes, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
+           lin.n, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val, (const uint8_t *)lin_fixed);
+  };
+  if (g_prof_env) fprintf(stderr, "[rs-prof] linear rows: %s\n", keys_first ? "keys first" : "keys + values");
   HC(hipStreamSynchronize(st));
   E->stats.eq_ms = now_ms() - T0;
 
@@ -1671,7 +1794,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   bool nl_staged = false;
   auto stage_nl = [&]() {
     if (nl_staged) return;
-    load_wait(E, 2);
+    load_wait(E, 3);
     mk_in(E->na, ia, "nla");
     mk_in(E->nb, ib, "nlb");
     mk_in(E->nc, ic, "nlc");
@@ -1791,7 +1914,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   Pool P = get_pool(E, 1 << 20);
   if (apply_linear) {
     run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted,
-                              n_nl && !E->comm ? &overlap : nullptr);
+                              n_nl && !E->comm ? &overlap : nullptr, keys_first ? &linear_values : nullptr);
     if (E->log_on) log_linear_round(E, eo, P);
     collect_leftovers(E, eo, P, lconst);
     E->stats.rounds++;
@@ -2349,13 +2472,18 @@ int rs_engine_create(int device, rs_engine **eng) {
       // The main stream leaves kHeadCUs compute units to the second stream: the head's ordered loop
       // (k_big_main_lds, one workgroup of ~154 KB LDS per cluster) finds whole CUs free there
       // instead of waiting for the tail kernels to drain a CU (RS_HEAD_CUS overrides; 0 = no mask).
-      uint32_t head_cus = 16;
+      uint32_t head_cus = 0;
       if (const char *hc = getenv("RS_HEAD_CUS")) head_cus = (uint32_t)std::min<unsigned long>(strtoul(hc, nullptr, 10), 64ul);
       const uint32_t n_cu = (uint32_t)prop.multiProcessorCount;
       bool masked = false;
       if (head_cus && n_cu >= 4 * head_cus) {
+        // mask bits go 32 to an XCD, and workgroups are dealt to the XCDs round-robin: the free CUs
+        // are spread evenly (head_cus / #XCD per XCD) so head workgroup i finds one on XCD i % #XCD
+        const uint32_t n_xcd = std::max<uint32_t>(1, n_cu / 32);
+        const uint32_t per = std::max<uint32_t>(1, head_cus / n_xcd);
         std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
-        for (uint32_t cu = 0; cu < n_cu - head_cus; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+        for (uint32_t cu = 0; cu < n_cu; ++cu)
+          if (cu % 32 < 32 - per) mask[cu / 32] |= 1u << (cu % 32);
         masked = hipExtStreamCreateWithCUMask(&E->st, (uint32_t)mask.size(), mask.data()) == hipSuccess;
         if (masked && g_prof_env) {
           std::vector<uint32_t> got(mask.size(), 0u);
@@ -2367,12 +2495,17 @@ int rs_engine_create(int device, rs_engine **eng) {
       }
       if (!masked) HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
     }
-    HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
+    {  // the second stream carries the critical path (the largest clusters' chain): high priority
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+          hipStreamCreateWithPriority(&E->st2, hipStreamNonBlocking, hi) != hipSuccess)
+        HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
+    }
     HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));
     for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HC(hipHostMalloc((void **)&E->h_vflag, 6 * sizeof(int), hipHostMallocDefault));
-    memset(E->h_vflag, 0, 6 * sizeof(int));
+    HC(hipHostMalloc((void **)&E->h_vflag, 10 * sizeof(int), hipHostMallocDefault));
+    memset(E->h_vflag, 0, 10 * sizeof(int));
     HC(hipHostMalloc((void **)&E->h_lvl, 4 * sizeof(unsigned long long), hipHostMallocDefault));
     for (auto &ev : E->ev_lvl) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipEventCreate(&E->ev0));
@@ -2428,7 +2561,7 @@ void rs_engine_destroy(rs_engine *E) {
 int rs_engine_load(rs_engine *E, const rs_input *in) {
   try {
     HC(hipSetDevice(E->device));
-    load_enqueue(E, in);
+    load_enqueue(E, in, false);
     load_wait_all(E);
     return RS_OK;
   } catch (const RsError &e) {
@@ -2585,8 +2718,9 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
   try {
     const double t0 = now_ms();
     HC(hipSetDevice(E->device));
-    load_enqueue(E, in);
+    load_enqueue(E, in, true);
     engine_run(E, fl);
+    E->hin = nullptr;
     const double t1 = now_ms();
     E->view = rs_output{};
     fetch_result(E, &E->view, [E](int slot, size_t bytes) { return pin_get(E, slot, bytes); }, false);

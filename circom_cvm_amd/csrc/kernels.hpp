@@ -107,6 +107,26 @@ __global__ void k_check_ptr(const uint64_t *ptr, uint64_t n, uint64_t nnz, int *
     if (bad) atomicOr(flag, 1);
   }
 }
+// Keys of a block whose values are still on the way (rs_engine_simplify's staged load): every key
+// < S; a row not strictly ascending sets `unsorted` (its values will be sorted with it once they
+// land), or, without `unsorted` (2-key eq rows), is invalid unless its keys are distinct.
+__global__ void k_check_keys(const uint64_t *ptr, const uint32_t *key, uint64_t n, uint64_t S, const int *ptr_bad, int *err,
+                             int *unsorted) {
+  if (*ptr_bad) return;
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    const uint64_t b = ptr[r], e = ptr[r + 1];
+    bool asc = true;
+    for (uint64_t i = b; i < e; ++i) {
+      if (key[i] >= S) atomicOr(err, 1);
+      if (i > b && key[i - 1] >= key[i]) asc = false;
+    }
+    if (asc) continue;
+    if (unsorted) { atomicOr(unsorted, 1); continue; }
+    for (uint64_t i = b; i < e; ++i)
+      for (uint64_t j = i + 1; j < e && j < b + 64; ++j)
+        if (key[i] == key[j]) atomicOr(err, 1);
+  }
+}
 // heap sort of (key, value) pairs by key (rows too long for an insertion sort)
 __device__ inline void d_heap_sort_pairs(uint32_t *k, Fe *v, uint32_t n) {
   auto sift = [&](uint32_t i, uint32_t m) {
@@ -313,12 +333,11 @@ __global__ void k_const_value(FieldP F, DRows R, const uint8_t *forb, const int3
     }
   }
 }
-// eq frame then constant frame on the linear rows (each frame + fix, :493-527); capacity len+1.
-__global__ void k_linear_frames12(FieldP F, DRows R, const int32_t *eq_rep, const uint8_t *ce_has, const Fe *ce_val) {
-  for (uint64_t r = gtid(); r < R.n; r += gstride()) {
-    uint32_t *k = R.key + R.off[r];
-    Fe *v = R.val + R.off[r];
-    uint32_t n = d_rename_row(F, k, v, R.len[r], eq_rep);
+// eq frame then constant frame on one linear row (each frame + fix, :493-527); capacity n+1.
+__device__ inline uint32_t d_linear_frames12(const FieldP &F, uint32_t *k, Fe *v, uint32_t n0, const int32_t *eq_rep,
+                                             const uint8_t *ce_has, const Fe *ce_val) {
+  {
+    uint32_t n = d_rename_row(F, k, v, n0, eq_rep);
     bool any = false;
     for (uint32_t i = 0; i < n; ++i)
       if (ce_has[k[i]]) any = true;
@@ -336,7 +355,115 @@ __global__ void k_linear_frames12(FieldP F, DRows R, const int32_t *eq_rep, cons
       v[0] = c0;
       n = d_drop_zeros(k, v, w + 1);
     }
-    R.len[r] = n;
+    return n;
+  }
+}
+__global__ void k_linear_frames12(FieldP F, DRows R, const int32_t *eq_rep, const uint8_t *ce_has, const Fe *ce_val) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride())
+    R.len[r] = d_linear_frames12(F, R.key + R.off[r], R.val + R.off[r], R.len[r], eq_rep, ce_has, ce_val);
+}
+
+// Keys-first linear rows (rs_engine_simplify): the eq and constant frames applied to the keys
+// alone, so build_clusters runs before the values land.  Row r of the upload (sorted, distinct keys)
+// becomes [0 if any constant or key 0] ++ sorted renamed non-constant keys in the ragged copy R
+// (off = ptr + r, room for len + 1).  Exact when no two keys of a row rename to the same signal
+// (their coefficients could cancel) and a row keeps a non-constant key (else whether it is empty
+// depends on its constant term): a row that breaks either sets `uncertain`, and the caller falls
+// back to the frames on values (k_make_ragged + k_linear_frames12) before clustering.
+__global__ void k_lin_keyframes(const uint64_t *ptr, const uint32_t *key, uint64_t n, DRows R, const int32_t *eq_rep,
+                                const uint8_t *ce_has, int *uncertain, uint32_t *unc_list, uint64_t unc_cap) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    const uint64_t b = ptr[r];
+    const uint32_t m = (uint32_t)(ptr[r + 1] - b);
+    const uint64_t o = b + r;
+    R.off[r] = o;
+    uint32_t *out = R.key + o + 1;  // slot 0 is reserved for key 0
+    bool has0 = false;
+    uint32_t w = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+      const uint32_t k = key[b + i];
+      const int32_t t = eq_rep[k];
+      const uint32_t k1 = t >= 0 ? (uint32_t)t : k;
+      if (k1 == 0 || ce_has[k1]) { has0 = true; continue; }
+      uint32_t j = w++;  // insertion into the sorted prefix
+      while (j > 0 && out[j - 1] > k1) { out[j] = out[j - 1]; --j; }
+      out[j] = k1;
+    }
+    uint32_t u = 0;  // distinct
+    bool dup = false;
+    for (uint32_t i = 0; i < w; ++i) {
+      if (u > 0 && out[u - 1] == out[i]) { dup = true; continue; }
+      out[u++] = out[i];
+    }
+    if (dup || u == 0) {
+      const int q = atomicAdd(uncertain, 1);
+      if ((uint64_t)q < unc_cap) unc_list[q] = (uint32_t)r;
+    }
+    if (has0) {
+      R.key[o] = 0;
+      R.len[r] = u + 1;
+    } else {
+      for (uint32_t i = 0; i < u; ++i) R.key[o + i] = out[i];
+      R.len[r] = u;
+    }
+  }
+}
+// The values of the keys-first rows once they land: each renamed non-constant entry fills its key's
+// slot (one contribution: no two keys of the row met), constant entries and key 0 sum into the
+// constant term c0 (Montgomery), which is dropped when zero -- the result of k_make_ragged +
+// k_linear_frames12 on the same row.
+__global__ void k_lin_valframes(FieldP F, const uint64_t *ptr, const uint32_t *key, const Fe *val, uint64_t n, DRows R,
+                                const int32_t *eq_rep, const uint8_t *ce_has, const Fe *ce_val, const uint8_t *fixed) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    if (fixed[r]) continue;  // done by k_lin_fixrows
+    const uint64_t b = ptr[r];
+    const uint32_t m = (uint32_t)(ptr[r + 1] - b);
+    const uint64_t o = R.off[r];
+    uint32_t len = R.len[r];
+    uint32_t *ok = R.key + o;
+    Fe *ov = R.val + o;
+    const bool has0 = len > 0 && ok[0] == 0;
+    const uint32_t s0 = has0 ? 1 : 0;
+    Fe c0 = fe_zero();
+    for (uint32_t i = 0; i < m; ++i) {
+      const uint32_t k = key[b + i];
+      const Fe v = fto_mont(F, val[b + i]);
+      const int32_t t = eq_rep[k];
+      const uint32_t k1 = t >= 0 ? (uint32_t)t : k;
+      if (k1 == 0) { c0 = fadd(F, c0, v); continue; }
+      if (ce_has[k1]) { c0 = fadd(F, c0, fmul(F, v, ce_val[k1])); continue; }
+      uint32_t lo = s0, hi = len;  // lower bound of k1 among the non-constant keys
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ok[mid] < k1) lo = mid + 1; else hi = mid;
+      }
+      ov[lo] = v;
+    }
+    if (has0) {
+      if (fe_is_zero(c0)) {
+        for (uint32_t i = 1; i < len; ++i) { ok[i - 1] = ok[i]; ov[i - 1] = ov[i]; }
+        R.len[r] = len - 1;
+      } else {
+        ov[0] = c0;
+      }
+    }
+  }
+}
+
+// The rows k_lin_keyframes could not settle from keys, with their values (copied from the host
+// input, canonical, as given): the frames on values, exactly as k_make_ragged + k_linear_frames12.
+__global__ void k_lin_fixrows(FieldP F, const uint64_t *hptr, const uint32_t *hkey, const Fe *hval, const uint32_t *rows,
+                              uint64_t m, DRows R, const int32_t *eq_rep, const uint8_t *ce_has, const Fe *ce_val,
+                              uint8_t *fixed) {
+  for (uint64_t q = gtid(); q < m; q += gstride()) {
+    const uint32_t r = rows[q];
+    const uint64_t b = hptr[q];
+    const uint32_t len = (uint32_t)(hptr[q + 1] - b);
+    uint32_t *k = R.key + R.off[r];
+    Fe *v = R.val + R.off[r];
+    for (uint32_t i = 0; i < len; ++i) { k[i] = hkey[b + i]; v[i] = fto_mont(F, hval[b + i]); }
+    R.len[r] = d_linear_frames12(F, k, v, len, eq_rep, ce_has, ce_val);
+    fixed[r] = 1;
   }
 }
 
@@ -393,10 +520,6 @@ struct ElimArgs {
   uint32_t *cf_done;          // per cluster: substitutions that reached a frontier
   uint64_t *cf_big;           // a level's compositions too long for k_compose_level's waves
   unsigned long long *cf_nbig;
-  // the head's ordered loop: k_big_main_lds takes every cluster whose signals fit its LDS table and
-  // flags the others in lds_fb; k_big_main<512> then runs with fb_only = 1 over the flagged ones
-  uint8_t *lds_fb = nullptr;
-  int fb_only = 0;
 
 };
 
@@ -1211,23 +1334,38 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t *a, uint32_t 
 // largest clusters; 256 for the tail, whose many clusters are throughput-bound: 34 KB of LDS lets
 // four single-wave workgroups share a CU, as many as the kernel's VGPR budget allows.
 template <uint32_t CAP>
-__global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+struct BigSmem {
+  uint32_t wk[2][CAP];
+  uint32_t ws[2][CAP];  // per work entry: its signal's state (kStForb / kStTake / holder slot)
+  Fe wv[2][CAP];
+  uint32_t rk[CAP];
+  Fe rv[CAP];
+  uint32_t fw[CAP], fr[CAP], lbw[CAP], lbr[CAP];
+  uint32_t s_fdel, s_m, s_nl, s_ok;
+  unsigned long long s_best;
+  uint64_t s_o;
+};
+// One cluster's ordered loop (the body of k_big_main; k_big_main_lds also runs it, on its LDS, for
+// the clusters whose signals do not fit its table).
+template <uint32_t CAP>
+__device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint32_t *ids, uint64_t ci, BigSmem<CAP> &S,
+                                                   Alloc &al0) {
   constexpr uint32_t kBigCap = CAP;
   const FieldP &F = A.F;
-  __shared__ uint32_t wk[2][kBigCap];
-  __shared__ uint32_t ws[2][kBigCap];  // per work entry: its signal's state (kStForb / kStTake / holder slot)
-  __shared__ Fe wv[2][kBigCap];
-  __shared__ uint32_t rk[kBigCap];
-  __shared__ Fe rv[kBigCap];
-  __shared__ uint32_t fw[kBigCap], fr[kBigCap], lbw[kBigCap], lbr[kBigCap];
-  __shared__ uint32_t s_fdel, s_m, s_nl, s_ok;
-  __shared__ unsigned long long s_best;
-  __shared__ uint64_t s_o;
+  auto &wk = S.wk;
+  auto &ws = S.ws;
+  auto &wv = S.wv;
+  auto &rk = S.rk;
+  auto &rv = S.rv;
+  auto &fw = S.fw;
+  auto &fr = S.fr;
+  auto &lbw = S.lbw;
+  auto &lbr = S.lbr;
+  uint32_t &s_fdel = S.s_fdel, &s_m = S.s_m, &s_nl = S.s_nl, &s_ok = S.s_ok;
+  unsigned long long &s_best = S.s_best;
+  uint64_t &s_o = S.s_o;
   const uint32_t tid = threadIdx.x, nt = 64;
-  Alloc al0;  // lane 0's allocator
-  al0.chunk = 4096;
-  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
-    if (A.fb_only && !A.lds_fb[ci]) continue;  // done by k_big_main_lds
+  {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     unsigned long long t_1 = 0;
@@ -1590,6 +1728,13 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
     __syncthreads();
   }
 }
+template <uint32_t CAP>
+__global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  __shared__ BigSmem<CAP> S;
+  Alloc al0;  // lane 0's allocator
+  al0.chunk = 4096;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) d_big_main_cluster<CAP>(A, ids, ci, S, al0);
+}
 
 // ---------------------------------------------------------------- the head's ordered loop, LDS state
 // k_big_main with the per-signal state of the cluster in LDS.  The loop of the largest clusters is
@@ -1603,8 +1748,8 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
 //                else -> occurrences (SignalsInformation, remove_constraint keeps it current).
 // The same row walk, pivot rules (take_signal_3 / take_signal_4), merges and pool writes as
 // k_big_main; the dense global arrays (holder_idx, del, occ) are still written, so the lane-serial
-// spill path (d_treat_scalar) and the kernels after the loop see the same state.  Clusters whose
-// signals do not fit the table are flagged in lds_fb and left to k_big_main<512>.
+// spill path (d_treat_scalar) and the kernels after the loop see the same state.  A cluster whose
+// signals do not fit the table runs k_big_main's loop (d_big_main_cluster<512>) on the same LDS.
 constexpr uint32_t kHeadTab = 15360;     // LDS hash slots (60 KB keys + 60 KB states)
 constexpr uint32_t kHeadTabMax = 9216;   // signals per cluster at most (load factor 0.6)
 constexpr uint32_t kHeadCap = 256;       // LDS work-list capacity
@@ -1628,18 +1773,40 @@ __device__ __forceinline__ uint32_t tab_state(const uint32_t *tk, const uint32_t
   return i == kTabEmpty ? kStForb : tv[i];
 }
 
+struct HeadSmem {
+  uint32_t tk[kHeadTab], tv[kHeadTab];
+  uint32_t wk[2][kHeadCap], ws[2][kHeadCap];
+  Fe wv[2][kHeadCap];
+  uint32_t rk[kHeadCap], rs[kHeadCap];
+  Fe rv[kHeadCap];
+  uint32_t fw[kHeadCap], fr[kHeadCap], lbw[kHeadCap], lbr[kHeadCap];
+  uint32_t s_fdel, s_m, s_nl, s_ok;
+  unsigned long long s_best;
+  uint64_t s_o;
+};
+union HeadLds {
+  HeadSmem h;
+  BigSmem<512> b;  // a cluster too large for the table runs k_big_main's loop on the same LDS
+};
 __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   constexpr uint32_t CAP = kHeadCap;
   const FieldP &F = A.F;
-  __shared__ uint32_t tk[kHeadTab], tv[kHeadTab];
-  __shared__ uint32_t wk[2][CAP], ws[2][CAP];
-  __shared__ Fe wv[2][CAP];
-  __shared__ uint32_t rk[CAP], rs[CAP];
-  __shared__ Fe rv[CAP];
-  __shared__ uint32_t fw[CAP], fr[CAP], lbw[CAP], lbr[CAP];
-  __shared__ uint32_t s_fdel, s_m, s_nl, s_ok;
-  __shared__ unsigned long long s_best;
-  __shared__ uint64_t s_o;
+  __shared__ HeadLds U;
+  auto &tk = U.h.tk;
+  auto &tv = U.h.tv;
+  auto &wk = U.h.wk;
+  auto &ws = U.h.ws;
+  auto &wv = U.h.wv;
+  auto &rk = U.h.rk;
+  auto &rs = U.h.rs;
+  auto &rv = U.h.rv;
+  auto &fw = U.h.fw;
+  auto &fr = U.h.fr;
+  auto &lbw = U.h.lbw;
+  auto &lbr = U.h.lbr;
+  uint32_t &s_fdel = U.h.s_fdel, &s_m = U.h.s_m, &s_nl = U.h.s_nl, &s_ok = U.h.s_ok;
+  unsigned long long &s_best = U.h.s_best;
+  uint64_t &s_o = U.h.s_o;
   const uint32_t tid = threadIdx.x, nt = 64;
   Alloc al0;  // lane 0's allocator
   al0.chunk = 4096;
@@ -1652,7 +1819,7 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
     const uint32_t n_touch = A.big_touch_n[ci];
     const uint64_t touch_off = A.big_touch_off[ci];
     if (n_loop == 0) {  // nothing for the ordered loop (every row went to the uniques phase)
-      if (tid == 0) { A.n_left[c] = 0; A.lds_fb[ci] = 0; }
+      if (tid == 0) A.n_left[c] = 0;
       continue;
     }
     // process_3 clusters have no touched list (no occurrence bookkeeping, no uniques phase): their
@@ -1664,7 +1831,8 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
       for (int d = 32; d >= 1; d >>= 1) n_ent += __shfl_xor(n_ent, d);
     }
     if ((p4 ? n_touch : n_ent) > kHeadTabMax || A.pool_cap >= (uint64_t)kStDel) {
-      if (tid == 0) A.lds_fb[ci] = 1;
+      __syncthreads();
+      d_big_main_cluster<512>(A, ids, ci, U.b, al0);
       continue;
     }
     const unsigned long long t_1 = A.prof ? wall_clock64() : 0ull;
@@ -1781,6 +1949,10 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
         ws[0][i] = st;
       }
       uint32_t cur = 0;
+      // the next merge's holder, loaded speculatively while the current merge computes: pf_st is
+      // the holder state it was loaded for (0: none)
+      uint32_t pf_st = 0, hpf_k = 0;
+      Fe hpf_v = fe_zero();
       __syncthreads();
       while (len > 0) {
         // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
@@ -1874,9 +2046,17 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
         // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p).  One round trip: lane 0
         // reads the header (RHS length, coefficient), lane l >= 1 the RHS entry l - 1.
         const uint64_t ho = hst & ~kStDel;
-        const bool in_pool = ho + tid < A.pool_cap;
-        const uint32_t hk_ = in_pool ? A.pk[ho + tid] : 0u;
-        const Fe hv_ = in_pool ? A.pv[ho + tid] : fe_zero();
+        uint32_t hk_;
+        Fe hv_;
+        if (pf_st == hst) {  // prefetched during the previous merge
+          hk_ = hpf_k;
+          hv_ = hpf_v;
+        } else {
+          const bool in_pool = ho + tid < A.pool_cap;
+          hk_ = in_pool ? A.pk[ho + tid] : 0u;
+          hv_ = in_pool ? A.pv[ho + tid] : fe_zero();
+        }
+        pf_st = 0;
         const uint32_t rl = (uint32_t)__shfl((int)hk_, 0);
         Fe c2;
 #pragma unroll
@@ -1929,6 +2109,26 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
           const uint32_t on = isw ? rl : (isr ? len : 0u);
           bool hit;
           const uint32_t lb = lds_lb64(ok, on, key, hit);
+          if (p4) {
+            // take_signal_4's next pivot is the smallest deleted key of the merged list: known from
+            // the keys alone unless a key of both lists cancels (then the prefetch is just unused)
+            const bool cand = ((isw && l != oi) || (isr && !hit)) && stv != kStForb && (stv & kStDel);
+            uint32_t mk = cand ? key : RS_NONE;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+              const uint32_t o2 = (uint32_t)__shfl_xor((int)mk, d);
+              mk = o2 < mk ? o2 : mk;
+            }
+            if (mk != RS_NONE) {
+              const uint64_t own = __ballot(cand && key == mk);
+              const uint32_t pst = (uint32_t)__shfl((int)stv, __ffsll((long long)own) - 1);
+              const uint64_t pho = pst & ~kStDel;
+              const bool inp = pho + tid < A.pool_cap;
+              hpf_k = inp ? A.pk[pho + tid] : 0u;
+              hpf_v = inp ? A.pv[pho + tid] : fe_zero();
+              pf_st = pst;
+            }
+          }
           val = fmul(F, isw ? c2 : coef, val);
           if (isr) rv[j] = val;
           wave_sync();
@@ -2020,7 +2220,6 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
     if (tid == 0) {
       A.n_sub[c] = s_m;
       A.n_left[c] = s_nl;
-      A.lds_fb[ci] = 0;
       atomicAdd(A.bytes_main, by);
       if (!s_ok) atomicOr(A.err, 8);
       if (A.prof) {
