@@ -41,7 +41,7 @@ class RsFlags(C.Structure):
 
 class RsOutput(C.Structure):
     _fields_ = [("n_constraints", C.c_uint64), ("a", RsLc), ("b", RsLc), ("c", RsLc),
-                ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int64)),
+                ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int32)),
                 ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64),
                 ("n_log", C.c_uint64), ("log_from", C.POINTER(C.c_uint32)), ("log_to", RsLc)]
 

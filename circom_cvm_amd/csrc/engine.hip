@@ -230,7 +230,7 @@ static const char *kGroupName[4] = {"cons_eq/eq", "linear", "linear", "non-linea
 static void load_enqueue(rs_engine *E, const rs_input *in, bool staged) {
   uint64_t p[4];
   if (!prime_of(in, p)) throw RsError(RS_E_INVALID, "unknown prime");
-  if (in->max_signal == 0 || in->max_signal > 0xfffffff0ull) throw RsError(RS_E_INVALID, "bad max_signal");
+  if (in->max_signal == 0 || in->max_signal > 0x7fffffffull) throw RsError(RS_E_INVALID, "bad max_signal (label_to_wire is int32)");
   if (in->n_forbidden && !in->forbidden) throw RsError(RS_E_INVALID, "forbidden list missing");
   std::vector<uint32_t> forb(in->forbidden, in->forbidden + in->n_forbidden);
   bool has0 = false;
@@ -2360,7 +2360,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   uint32_t *kept = A.get<uint32_t>("fin.kept", S);
   uint64_t *kept64 = A.get<uint64_t>("fin.kept64", S);
   uint64_t *rank = A.get<uint64_t>("fin.rank", S);
-  int64_t *l2w = A.get<int64_t>("fin.l2w", S);
+  int32_t *l2w = A.get<int32_t>("fin.l2w", S);
   launch(st, k_kept, S, (const uint8_t *)d_deleted, (const uint8_t *)d_forb, (const uint8_t *)nlmap, kept, S);
   launch(st, k_u32_to_u64, S, (const uint32_t *)kept, kept64, S);
   E->n_wires = excl_scan_u64(E, kept64, rank, S, "kept");
@@ -2631,8 +2631,8 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
     }
   }
   o->n_labels = E->S;
-  o->label_to_wire = (int64_t *)buf(9, 8 * E->S);
-  HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int64_t>("fin.l2w", 1), 8 * E->S, hipMemcpyDeviceToHost, E->st));
+  o->label_to_wire = (int32_t *)buf(9, 4 * E->S);
+  HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int32_t>("fin.l2w", 1), 4 * E->S, hipMemcpyDeviceToHost, E->st));
   HC(hipStreamSynchronize(E->st));
   for (int q = 0; q < 3; ++q) {
     rs_lc &L = *dst[q];

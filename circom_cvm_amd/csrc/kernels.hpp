@@ -3270,8 +3270,8 @@ __global__ void k_mark_list(const uint32_t *sig, uint64_t n, uint8_t *bits) {
 __global__ void k_kept(const uint8_t *deleted, const uint8_t *forb, const uint8_t *nlmap, uint32_t *kept, uint64_t S) {
   for (uint64_t s = gtid(); s < S; s += gstride()) kept[s] = (!deleted[s] && (forb[s] || nlmap[s])) ? 1u : 0u;
 }
-__global__ void k_l2w(const uint32_t *kept, const uint64_t *rank, int64_t *l2w, uint64_t S) {
-  for (uint64_t s = gtid(); s < S; s += gstride()) l2w[s] = kept[s] ? (int64_t)rank[s] : -1;
+__global__ void k_l2w(const uint32_t *kept, const uint64_t *rank, int32_t *l2w, uint64_t S) {
+  for (uint64_t s = gtid(); s < S; s += gstride()) l2w[s] = kept[s] ? (int32_t)rank[s] : -1;
 }
 // gathers ragged rows (selected ids) into a compact CSR with canonical values
 __global__ void k_gather_rows(FieldP F, DRows R, const uint32_t *ids, uint64_t n, const uint64_t *optr,

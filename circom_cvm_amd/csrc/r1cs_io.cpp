@@ -156,7 +156,7 @@ static std::string dec_string(const uint64_t *v) {
 
 // hashmap_as_json (json_porting.rs:16-26) + JsonValue::to_string: {"k":"v",...}, keys ascending
 // (as numbers), `ids` mapped through `l2w` when given (apply_correspondence).
-static bool map_json(std::string &o, const rs_lc &L, uint64_t r, const int64_t *l2w, uint64_t n_labels) {
+static bool map_json(std::string &o, const rs_lc &L, uint64_t r, const int32_t *l2w, uint64_t n_labels) {
   std::vector<std::pair<uint64_t, uint64_t>> ord;  // (key, entry)
   for (uint64_t e = L.ptr[r]; e < L.ptr[r + 1]; ++e) {
     uint64_t k = L.col[e];
@@ -202,7 +202,7 @@ int rs_read_r1cs_o0(const char *path, rs_input **out) {
   if (!hc.bytes(p, fs) || !hc.u32(n_wires) || !hc.u32(n_out) || !hc.u32(n_pub) || !hc.u32(n_prv) ||
       !hc.u64(n_labels) || !hc.u32(n_cons))
     return RS_E_INVALID;
-  if (n_labels == 0 || n_labels > 0xfffffff0ull || 1 + (uint64_t)n_out + n_pub > n_labels) {
+  if (n_labels == 0 || n_labels > 0x7fffffffull || 1 + (uint64_t)n_out + n_pub > n_labels) {
     set_error("r1cs header: bad label count");
     return RS_E_INVALID;
   }

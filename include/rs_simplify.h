@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 4
+#define RS_ABI_VERSION 5
 
 enum rs_status {
   RS_OK = 0,
@@ -112,7 +112,7 @@ typedef struct rs_output {
   uint64_t n_constraints;
   rs_lc a, b, c;                  /* owned by the library; free with rs_output_free         */
   uint64_t n_labels;              /* = max_signal                                           */
-  int64_t *label_to_wire;         /* n_labels entries, -1 = not a wire                      */
+  int32_t *label_to_wire;         /* n_labels entries, -1 = not a wire (int32)  */
   uint64_t n_wires;               /* = SignalMap.len()                                      */
   uint64_t no_private_inputs_witness;
   /* The substitution log (--simplification_substitution, constraint_simplification.rs:9-17),

@@ -41,7 +41,7 @@ static bool same_lc(const rs_lc &x, const rs_lc &y) {
 static bool same_out(const rs_output *x, const rs_output *y) {
   return x->n_constraints == y->n_constraints && same_lc(x->a, y->a) && same_lc(x->b, y->b) && same_lc(x->c, y->c) &&
          x->n_wires == y->n_wires && x->no_private_inputs_witness == y->no_private_inputs_witness &&
-         !memcmp(x->label_to_wire, y->label_to_wire, 8 * x->n_labels);
+         !memcmp(x->label_to_wire, y->label_to_wire, 4 * x->n_labels);
 }
 static std::vector<uint8_t> slurp(const std::string &p) {
   std::vector<uint8_t> b;

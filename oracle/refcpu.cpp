@@ -528,7 +528,7 @@ struct Input {
 };
 struct Output {
   std::vector<Con> constraints;
-  std::vector<int64_t> label_to_wire;
+  std::vector<int32_t> label_to_wire;
   uint64_t n_wires = 0, no_private_inputs_witness = 0;
   uint64_t rounds = 0, n_clusters = 0;
 };
@@ -831,8 +831,8 @@ int refcpu_simplify(const rs_input *in, const rs_flags *fl, int n_threads, rs_ou
     store_block(X.F, O.constraints, 1, o->b);
     store_block(X.F, O.constraints, 2, o->c);
     o->n_labels = X.max_signal;
-    o->label_to_wire = (int64_t *)malloc(sizeof(int64_t) * (X.max_signal ? X.max_signal : 1));
-    memcpy(o->label_to_wire, O.label_to_wire.data(), sizeof(int64_t) * X.max_signal);
+    o->label_to_wire = (int32_t *)malloc(sizeof(int32_t) * (X.max_signal ? X.max_signal : 1));
+    memcpy(o->label_to_wire, O.label_to_wire.data(), sizeof(int32_t) * X.max_signal);
     o->n_wires = O.n_wires;
     o->no_private_inputs_witness = O.no_private_inputs_witness;
     *out = o;

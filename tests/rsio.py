@@ -167,14 +167,14 @@ class OutputHolder:
     def __init__(self, res: "R.Result", n_labels: int, log=()):
         self.blocks = [_Block([c.a for c in res.constraints]), _Block([c.b for c in res.constraints]),
                        _Block([c.c for c in res.constraints])]
-        self.l2w = np.array([res.signal_map.get(i, -1) for i in range(n_labels)] or [0], dtype=np.int64)
+        self.l2w = np.array([res.signal_map.get(i, -1) for i in range(n_labels)] or [0], dtype=np.int32)
         self.log_blk = _Block([to for _, to in log])
         self.log_from = np.array([f for f, _ in log] or [0], dtype=np.uint32)
         o = RsOutput()
         o.n_constraints = len(res.constraints)
         o.a, o.b, o.c = [b.lc for b in self.blocks]
         o.n_labels = n_labels
-        o.label_to_wire = self.l2w.ctypes.data_as(C.POINTER(C.c_int64))
+        o.label_to_wire = self.l2w.ctypes.data_as(C.POINTER(C.c_int32))
         o.n_wires = len(res.signal_map)
         o.no_private_inputs_witness = res.no_private_inputs_witness
         o.n_log = len(log)
