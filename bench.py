@@ -89,7 +89,7 @@ def shard_seed(seed: int, rank: int) -> int:
 
 
 KERNELS = (  # (name, stats fields: ms, bytes, launches)
-    ("k_big_main<512> (head)", "head_main_ms", "head_main_bytes", "head_launches"),
+    ("k_big_main_lds (head)", "head_main_ms", "head_main_bytes", "head_launches"),
     ("k_big_main<256> (tail)", "tail_main_ms", "tail_main_bytes", "tail_launches"),
     ("k_nl_fill", "apply_kernel_ms", "apply_bytes", "apply_kernel_launches"),
     ("k_round_fill", "round_fill_ms", "round_fill_bytes", "round_fill_launches"),
@@ -178,6 +178,16 @@ def main():
     if rank == 0 and not args.no_cpu:
         import rsio
         got = rsio.output_arrays(out)  # copy of the last timed step's result (the view is reused)
+    # the last result written as .r1cs by the device writer (8(d): write timed apart)
+    write = None
+    if rank == 0:
+        import tempfile
+        with tempfile.TemporaryDirectory() as tmp:
+            path = os.path.join(tmp, "bench_O2.r1cs")
+            ms_w = eng.write_r1cs(path)
+            write = {"ms": round(ms_w, 2), "bytes": os.path.getsize(path),
+                     "what": "rs_engine_write_r1cs: the last step's result as a .r1cs file (constraint section "
+                             "built on the device, streamed to a file in a temporary directory)"}
     # ---- extra: the same engine with the input resident in HBM (rs_engine_run only)
     eng.load(pin.c)
     barrier()
@@ -252,6 +262,8 @@ def main():
                              "ms_per_step": round(dt_hbm * 1000.0 / K, 3),
                              "what": "rs_engine_run: input already in HBM -> result in HBM (no PCIe)"},
         }
+        if write is not None:
+            line["write_r1cs"] = write
         if weak is not None:
             line["weak_shards"] = weak
         if not args.no_cpu:

@@ -63,7 +63,7 @@ class RsStats(C.Structure):
                 ("tail_main_ms", C.c_double), ("tail_main_bytes", C.c_uint64), ("tail_launches", C.c_uint64),
                 ("round_fill_ms", C.c_double), ("round_fill_bytes", C.c_uint64),
                 ("round_fill_launches", C.c_uint64), ("alg_bytes", C.c_uint64), ("h2d_wait_ms", C.c_double),
-                ("d2h_ms", C.c_double), ("host_total_ms", C.c_double)]
+                ("d2h_ms", C.c_double), ("host_total_ms", C.c_double), ("write_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -81,6 +81,7 @@ SYMBOLS = [
     ("rs_engine_fetch", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(RsOutput))]),
     ("rs_engine_stats", C.c_int, [C.c_void_p, C.POINTER(RsStats)]),
     ("rs_engine_destroy", None, [C.c_void_p]),
+    ("rs_engine_write_r1cs", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
     ("rs_engine_simplify", C.c_int, [C.c_void_p, C.POINTER(RsInput), C.POINTER(RsFlags),
                                      C.POINTER(C.POINTER(RsOutput))]),
     ("rs_host_alloc", C.c_void_p, [C.c_uint64]),
@@ -218,6 +219,12 @@ class Engine:
         out = C.POINTER(RsOutput)()
         check(lib().rs_engine_simplify(self._h, C.byref(inp), C.byref(flags), C.byref(out)))
         return out.contents
+
+    def write_r1cs(self, path: str, o0_r1cs: str | None = None) -> float:
+        """rs_engine_write_r1cs: the last result as a .r1cs file (device-built constraint section).
+        Returns the write time (ms)."""
+        check(lib().rs_engine_write_r1cs(self._h, path.encode(), o0_r1cs.encode() if o0_r1cs else None))
+        return self.stats().write_ms
 
     def close(self):
         if self._h:

@@ -26,6 +26,7 @@
 #include "host_common.hpp"
 #include "kernels.hpp"
 #include "cluster.hpp"
+#include "writer.hpp"
 
 namespace rs {
 
@@ -185,7 +186,7 @@ struct rs_engine {
     void *p = nullptr;
     size_t cap = 0;
   };
-  Pin pin[11];  // a/b/c: ptr, col, val; label_to_wire; spare
+  Pin pin[13];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers
   rs_output view{};
 };
 
@@ -613,40 +614,79 @@ __global__ void k_shard_pick(const uint32_t *ids, uint64_t n_out, int W, int r, 
 __global__ void k_shard_owner(const uint32_t *ids, uint64_t n, int W, uint8_t *owner) {
   for (uint64_t i = gtid(); i < n; i += gstride()) owner[ids[i]] = (uint8_t)snake_rank(i, W);
 }
-// Before the exchange: the rank's own slots get their pool offsets rebased into the gathered pool;
-// every other slot (and every other cluster's counts) is zeroed, so a sum over ranks assembles the
-// complete per-slot map.
-__global__ void k_shard_rebase(const uint32_t *cid, const uint64_t *cl_off, const uint8_t *owner, int r,
-                               const uint32_t *n_sub, const uint32_t *n_left, uint64_t base, uint32_t *h_sig,
-                               uint64_t *h_off, uint32_t *h_len, uint64_t *l_off, uint32_t *l_len, uint64_t n_slots) {
+// The exchange, packed: each rank sends only its own clusters' records -- a substitution as
+// (slot, from, RHS length, entry offset), its right-hand side only when `from` is needed by some
+// row still to be substituted (round 1: the relevant set, build_relevant_set :398-429 -- signals of
+// the non-linear rows after the eq renames, minus the constant ones; later rounds: the keys of the
+// non-linear signal map, :345-396), a leftover as (slot, length, entry offset) with its entries.
+// Every rank unpacks every rank's records into its per-slot arrays (slot = cluster start + index,
+// so the counts per cluster follow from the records).
+struct XRec {
+  uint32_t slot, sig, len, eoff;
+};
+__global__ void k_xpk_count(const uint32_t *cid, const uint64_t *cl_off, const uint8_t *owner, int r, const uint32_t *n_sub,
+                            const uint32_t *n_left, const uint32_t *h_sig, const uint32_t *h_len, const uint32_t *l_len,
+                            const uint8_t *need, uint64_t n_slots, uint64_t *sf, uint64_t *lf, uint64_t *se, uint64_t *le) {
   for (uint64_t s = gtid(); s < n_slots; s += gstride()) {
     const uint32_t c = cid[s];
     const uint64_t i = s - cl_off[c];
-    if (owner[c] == r) {
-      if (i < n_sub[c]) h_off[s] += base;
-      else { h_sig[s] = 0; h_off[s] = 0; h_len[s] = 0; }
-      if (i < n_left[c]) l_off[s] += base;
-      else { l_off[s] = 0; l_len[s] = 0; }
-    } else {
-      h_sig[s] = 0; h_off[s] = 0; h_len[s] = 0; l_off[s] = 0; l_len[s] = 0;
-    }
+    const bool own = owner[c] == r;
+    const bool is_sub = own && i < n_sub[c], is_left = own && i < n_left[c];
+    sf[s] = is_sub;
+    se[s] = is_sub && (!need || need[h_sig[s]]) ? h_len[s] : 0;
+    lf[s] = is_left;
+    le[s] = is_left ? l_len[s] : 0;
   }
 }
-__global__ void k_shard_zero_counts(const uint8_t *owner, int r, uint64_t n_cl, uint32_t *n_sub, uint32_t *n_left) {
-  for (uint64_t c = gtid(); c < n_cl; c += gstride())
-    if (owner[c] != r) { n_sub[c] = 0; n_left[c] = 0; }
-}
-// After the exchange: the dense signal -> substitution index and the deleted bits of every rank's
-// substitutions (the owner's own entries are rewritten with the same values).
-__global__ void k_shard_subof(const uint32_t *cid, const uint64_t *cl_off, const uint32_t *n_sub, const uint32_t *h_sig,
-                              int32_t *sub_of, uint8_t *deleted, uint64_t n_slots) {
+__global__ void k_xpk_fill(const uint32_t *cid, const uint64_t *cl_off, const uint64_t *sf, const uint64_t *sp,
+                           const uint64_t *se, const uint64_t *sep, const uint64_t *lf, const uint64_t *lp, const uint64_t *le,
+                           const uint64_t *lep, uint64_t sub_ent, const uint32_t *h_sig, const uint64_t *h_off,
+                           const uint64_t *l_off, const uint32_t *pk, const Fe *pv, uint64_t n_slots, XRec *srec, XRec *lrec,
+                           uint32_t *ek, Fe *ev) {
   for (uint64_t s = gtid(); s < n_slots; s += gstride()) {
-    const uint32_t c = cid[s];
-    if (s - cl_off[c] < n_sub[c]) {
-      sub_of[h_sig[s]] = (int32_t)s;
-      deleted[h_sig[s]] = 1;
+    if (sf[s]) {
+      const uint64_t o = sep[s], m = se[s];
+      srec[sp[s]] = XRec{(uint32_t)s, h_sig[s], (uint32_t)m, (uint32_t)o};
+      for (uint64_t t = 0; t < m; ++t) { ek[o + t] = pk[h_off[s] + t]; ev[o + t] = pv[h_off[s] + t]; }
+    }
+    if (lf[s]) {
+      const uint64_t o = sub_ent + lep[s], m = le[s];
+      lrec[lp[s]] = XRec{(uint32_t)s, 0u, (uint32_t)m, (uint32_t)o};
+      for (uint64_t t = 0; t < m; ++t) { ek[o + t] = pk[l_off[s] + t]; ev[o + t] = pv[l_off[s] + t]; }
     }
   }
+}
+// one rank's block of records; `base` = where that rank's entries start in the gathered pool
+__global__ void k_xunpack(const XRec *srec, uint64_t ns, const XRec *lrec, uint64_t nl, uint64_t base, const uint32_t *cid,
+                          uint32_t *h_sig, uint64_t *h_off, uint32_t *h_len, uint64_t *l_off, uint32_t *l_len, uint32_t *n_sub,
+                          uint32_t *n_left, int32_t *sub_of, uint8_t *deleted) {
+  for (uint64_t j = gtid(); j < ns + nl; j += gstride()) {
+    if (j < ns) {
+      const XRec x = srec[j];
+      h_sig[x.slot] = x.sig;
+      h_len[x.slot] = x.len;
+      h_off[x.slot] = base + x.eoff;
+      sub_of[x.sig] = (int32_t)x.slot;
+      deleted[x.sig] = 1;
+      atomicAdd(&n_sub[cid[x.slot]], 1u);
+    } else {
+      const XRec x = lrec[j - ns];
+      l_len[x.slot] = x.len;
+      l_off[x.slot] = base + x.eoff;
+      atomicAdd(&n_left[cid[x.slot]], 1u);
+    }
+  }
+}
+// round 1's relevant set: the signals of the non-linear rows after the eq renames, minus the
+// constant ones (build_relevant_set :398-429)
+__global__ void k_mark_relevant(DRows R, const int32_t *eq_rep, const uint8_t *ce_has, uint8_t *need) {
+  for (uint64_t r = gtid(); r < R.n; r += gstride())
+    for (uint32_t i = 0; i < R.len[r]; ++i) {
+      const uint32_t k = R.key[R.off[r] + i];
+      const int32_t t = eq_rep[k];
+      const uint32_t k1 = t >= 0 ? (uint32_t)t : k;
+      if (!ce_has[k1]) need[k1] = 1;
+    }
 }
 
 // ---------------------------------------------------------------- host clustering
@@ -901,50 +941,64 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
 }
 
 // The exchange step of the sharded elimination: after it every rank holds the complete
-// eliminated-signal map of the round -- per slot (from, RHS offset/length) and leftovers (offset,
-// length), per cluster #subs/#leftovers, the gathered pool those offsets index, and the dense
-// sub_of / deleted of every substitution.  The offsets are rebased into the gathered pool (rank q's
-// entries start at the sum of the lower ranks' pool tops) before a sum-allreduce of the zero-padded
-// per-slot arrays; the pool itself is an allgatherv.
-static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D, const uint8_t *owner, Pool &P) {
+// eliminated-signal map of the round -- every substitution's `from` (sub_of, deleted), the
+// right-hand sides some later substitution step will read (`need`; null = all, e.g. for the
+// substitution log), every leftover -- in a pool made of every rank's packed entries.  Four
+// allgathervs of packed records and entries replace the round-1 design's zero-padded per-slot
+// sum-allreduce and whole-pool gather.
+static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D, const uint8_t *owner, Pool &P,
+                           const uint8_t *need) {
   Comm &CM = *E->comm;
+  Arena &A = E->A;
   hipStream_t st = E->st;
   const double t0 = now_ms();
   const uint64_t n_slots = D.n_slots, n_cl = a.n_clusters;
-  uint64_t top = 0;
-  HC(hipMemcpyAsync(&top, P.top, 8, hipMemcpyDeviceToHost, st));
-  HC(hipStreamSynchronize(st));
-  top = std::min<uint64_t>(top, P.cap);
-  const std::vector<uint64_t> tops = CM.gather_u64(top, st);
-  uint64_t base = 0, tot = 0;
-  std::vector<uint64_t> ck(CM.world), cv(CM.world);
+  uint64_t *sf = A.get<uint64_t>("x.sf", n_slots), *sp = A.get<uint64_t>("x.sp", n_slots);
+  uint64_t *se = A.get<uint64_t>("x.se", n_slots), *sep = A.get<uint64_t>("x.sep", n_slots);
+  uint64_t *lf = A.get<uint64_t>("x.lf", n_slots), *lp = A.get<uint64_t>("x.lp", n_slots);
+  uint64_t *le = A.get<uint64_t>("x.le", n_slots), *lep = A.get<uint64_t>("x.lep", n_slots);
+  launch(st, k_xpk_count, n_slots, (const uint32_t *)D.cid, (const uint64_t *)D.cl_off, owner, CM.rank,
+         (const uint32_t *)a.n_sub, (const uint32_t *)a.n_left, (const uint32_t *)a.h_sig, (const uint32_t *)a.h_len,
+         (const uint32_t *)a.l_len, need, n_slots, sf, lf, se, le);
+  const uint64_t n_s = excl_scan_u64(E, sf, sp, n_slots, "xs");
+  const uint64_t n_l = excl_scan_u64(E, lf, lp, n_slots, "xl");
+  const uint64_t e_s = excl_scan_u64(E, se, sep, n_slots, "xse");
+  const uint64_t e_l = excl_scan_u64(E, le, lep, n_slots, "xle");
+  XRec *srec = A.get<XRec>("x.srec", n_s + 1), *lrec = A.get<XRec>("x.lrec", n_l + 1);
+  uint32_t *ek = A.get<uint32_t>("x.ek", e_s + e_l + 1);
+  Fe *ev = A.get<Fe>("x.ev", e_s + e_l + 1);
+  launch(st, k_xpk_fill, n_slots, (const uint32_t *)D.cid, (const uint64_t *)D.cl_off, (const uint64_t *)sf,
+         (const uint64_t *)sp, (const uint64_t *)se, (const uint64_t *)sep, (const uint64_t *)lf, (const uint64_t *)lp,
+         (const uint64_t *)le, (const uint64_t *)lep, e_s, (const uint32_t *)a.h_sig, (const uint64_t *)a.h_off,
+         (const uint64_t *)a.l_off, (const uint32_t *)P.pk, (const Fe *)P.pv, n_slots, srec, lrec, ek, ev);
+  const std::vector<uint64_t> ns = CM.gather_u64(n_s, st), nl = CM.gather_u64(n_l, st), ne = CM.gather_u64(e_s + e_l, st);
+  uint64_t ts = 0, tl = 0, te = 0;
+  std::vector<uint64_t> cs(CM.world), cl(CM.world), ck(CM.world), cv(CM.world);
   for (int q = 0; q < CM.world; ++q) {
-    if (q < CM.rank) base += tops[q];
-    tot += tops[q];
-    ck[q] = 4 * tops[q];
-    cv[q] = 32 * tops[q];
+    ts += ns[q]; tl += nl[q]; te += ne[q];
+    cs[q] = sizeof(XRec) * ns[q]; cl[q] = sizeof(XRec) * nl[q]; ck[q] = 4 * ne[q]; cv[q] = 32 * ne[q];
   }
-  launch(st, k_shard_zero_counts, n_cl, owner, CM.rank, n_cl, a.n_sub, a.n_left);
-  launch(st, k_shard_rebase, n_slots, (const uint32_t *)D.cid, (const uint64_t *)D.cl_off, owner, CM.rank,
-         (const uint32_t *)a.n_sub, (const uint32_t *)a.n_left, base, a.h_sig, a.h_off, a.h_len, a.l_off, a.l_len, n_slots);
-  uint32_t *gk = E->A.get<uint32_t>("pool.gk", tot);
-  Fe *gv = E->A.get<Fe>("pool.gv", tot);
-  CM.allgatherv(P.pk, gk, ck, st);
-  CM.allgatherv(P.pv, gv, cv, st);
-  CM.allreduce_sum(a.h_sig, n_slots, 4, st);
-  CM.allreduce_sum(a.h_off, n_slots, 8, st);
-  CM.allreduce_sum(a.h_len, n_slots, 4, st);
-  CM.allreduce_sum(a.l_off, n_slots, 8, st);
-  CM.allreduce_sum(a.l_len, n_slots, 4, st);
-  CM.allreduce_sum(a.n_sub, n_cl, 4, st);
-  CM.allreduce_sum(a.n_left, n_cl, 4, st);
-  launch(st, k_shard_subof, n_slots, (const uint32_t *)D.cid, (const uint64_t *)D.cl_off, (const uint32_t *)a.n_sub,
-         (const uint32_t *)a.h_sig, a.sub_of, a.deleted, n_slots);
+  XRec *gs = A.get<XRec>("x.gs", ts + 1), *gl = A.get<XRec>("x.gl", tl + 1);
+  uint32_t *gk = A.get<uint32_t>("pool.gk", te + 1);
+  Fe *gv = A.get<Fe>("pool.gv", te + 1);
+  CM.allgatherv(srec, gs, cs, st);
+  CM.allgatherv(lrec, gl, cl, st);
+  CM.allgatherv(ek, gk, ck, st);
+  CM.allgatherv(ev, gv, cv, st);
+  HC(hipMemsetAsync(a.n_sub, 0, 4 * n_cl, st));
+  HC(hipMemsetAsync(a.n_left, 0, 4 * n_cl, st));
+  uint64_t os = 0, ol = 0, oe = 0;
+  for (int q = 0; q < CM.world; ++q) {
+    if (ns[q] + nl[q])
+      launch(st, k_xunpack, ns[q] + nl[q], (const XRec *)(gs + os), ns[q], (const XRec *)(gl + ol), nl[q], oe,
+             (const uint32_t *)D.cid, a.h_sig, a.h_off, a.h_len, a.l_off, a.l_len, a.n_sub, a.n_left, a.sub_of, a.deleted);
+    os += ns[q]; ol += nl[q]; oe += ne[q];
+  }
   HC(hipStreamSynchronize(st));
   P.pk = gk;
   P.pv = gv;
   E->stats.exchange_ms += now_ms() - t0;
-  E->stats.exchange_bytes += 36 * tot + n_slots * 28 + n_cl * 8;
+  E->stats.exchange_bytes += sizeof(XRec) * (ts + tl) + 36 * te + 24 * CM.world;
 }
 
 // Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
@@ -956,7 +1010,8 @@ using HeadOverlap = std::function<void(const uint32_t *head_ids, uint64_t n_head
 static void run_linear_simplification(rs_engine *E, const DRows &view, int old_heur, ElimOut &eo, Pool &P,
                                       int *d_err, uint8_t *d_forb, int32_t *sub_of, uint8_t *deleted,
                                       const HeadOverlap *overlap = nullptr,
-                                      const std::function<void()> *before_elim = nullptr) {
+                                      const std::function<void()> *before_elim = nullptr,
+                                      const uint8_t *need = nullptr) {
   double t0 = now_ms();
   DevClusters D = gpu_clusters(E, view, old_heur, d_forb, eo);
   // keys-first rows: their values now (main stream; every elimination kernel is ordered after it)
@@ -1200,7 +1255,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
     E->pool_want = std::max(E->pool_want, want);  // the next run starts from a size that fitted
-    if (W > 1 && eo.n_clusters) shard_exchange(E, a, D, d_owner, P);
+    if (W > 1 && eo.n_clusters) shard_exchange(E, a, D, d_owner, P, need);
     if (eo.n_clusters) {
       float ms = 0;
       unsigned long long by = 0;
@@ -1913,8 +1968,19 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   ElimOut eo;
   Pool P = get_pool(E, 1 << 20);
   if (apply_linear) {
+    // sharded: only the relevant substitutions' right-hand sides travel (the log needs them all)
+    uint8_t *relevant = nullptr;
+    if (E->comm && E->comm->world > 1 && !E->log_on) {
+      relevant = A.get<uint8_t>("x.relevant", S);
+      HC(hipMemsetAsync(relevant, 0, S, st));
+      if (n_nl) {
+        stage_nl();
+        for (const DRows *R : {&ia, &ib, &ic})
+          launch(st, k_mark_relevant, R->n, *R, (const int32_t *)eq_rep, (const uint8_t *)ce_has, relevant);
+      }
+    }
     run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted,
-                              n_nl && !E->comm ? &overlap : nullptr, keys_first ? &linear_values : nullptr);
+                              n_nl && !E->comm ? &overlap : nullptr, keys_first ? &linear_values : nullptr, relevant);
     if (E->log_on) log_linear_round(E, eo, P);
     collect_leftovers(E, eo, P, lconst);
     E->stats.rounds++;
@@ -2079,7 +2145,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       // linear_simplification over the current list
       ElimOut er;
       HC(hipMemsetAsync(r_sub_of, 0xff, 4 * S, st));
-      run_linear_simplification(E, lv, fl->use_old_heuristics, er, P, d_err, d_forb, r_sub_of, d_deleted);
+      run_linear_simplification(E, lv, fl->use_old_heuristics, er, P, d_err, d_forb, r_sub_of, d_deleted, nullptr, nullptr,
+                                E->comm && E->comm->world > 1 && !E->log_on ? nlmap : nullptr);
       if (E->log_on) log_linear_round(E, er, P);
       E->stats.rounds++;
       Marks MK;
@@ -2737,6 +2804,153 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
   } catch (const std::exception &e) {
     load_abort(E);
     E->loaded = false;
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
+// The last result as a .r1cs file (constraint_list/src/r1cs_porting.rs:4-124, the same bytes as
+// rs_write_r1cs on the fetched output): the constraint section is built on the device (writer.hpp)
+// and streamed to the file through two pinned staging buffers; the host-side tail rows (lconst) and
+// the small sections follow.  o0_r1cs (optional): custom-gate sections as rs_write_r1cs_gates.
+int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
+  FILE *f = nullptr;
+  try {
+    if (!E->have_result) { set_error("no result"); return RS_E_INVALID; }
+    HC(hipSetDevice(E->device));
+    const double t0 = now_ms();
+    Arena &A = E->A;
+    hipStream_t st = E->st;
+    const uint32_t fs = (uint32_t)field_size_bytes(E->prime);
+    const uint64_t n = E->out_n_dev, S = E->S;
+    const char *nm[3] = {"out.a", "out.b", "out.c"};
+    const uint64_t *pq[3];
+    for (int q = 0; q < 3; ++q) pq[q] = A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1);
+    const int32_t *l2w = A.get<int32_t>("fin.l2w", 1);
+    int *d_err = A.get<int>("w.err", 1);
+    HC(hipMemsetAsync(d_err, 0, 4, st));
+    // record offsets
+    uint64_t *sz = A.get<uint64_t>("w.sz", n + 1), *roff = A.get<uint64_t>("w.roff", n + 1);
+    if (n) launch(st, k_w_rowbytes, n, pq[0], pq[1], pq[2], n, fs, sz);
+    HC(hipMemsetAsync(sz + n, 0, 8, st));
+    const uint64_t dev_bytes = excl_scan_u64(E, sz, roff, n + 1, "wsz");
+    uint32_t *img = A.get<uint32_t>("w.img", dev_bytes / 4 + 1);
+    if (n) launch(st, k_w_counts, n, pq[0], pq[1], pq[2], (const uint64_t *)roff, n, fs, img);
+    int rbits = 1;
+    while (rbits < 28 && (1ull << rbits) <= n) ++rbits;
+    for (int q = 0; q < 3; ++q) {
+      const uint64_t nnz = E->out_nnz[q];
+      if (!nnz) continue;
+      uint64_t *k1 = A.get<uint64_t>("w.k1", nnz), *k2 = A.get<uint64_t>("w.k2", nnz);
+      uint32_t *i1 = A.get<uint32_t>("w.i1", nnz), *i2 = A.get<uint32_t>("w.i2", nnz);
+      const uint32_t *col = A.get<uint32_t>(std::string(nm[q]) + ".col", 1);
+      const uint64_t *val = A.get<uint64_t>(std::string(nm[q]) + ".val", 1);
+      launch(st, k_w_keys, n, pq[q], n, col, l2w, k1, i1, d_err);
+      sort_pairs(E, (const uint64_t *)k1, k2, (const uint32_t *)i1, i2, nnz, kLeKeyBits + rbits, "w");
+      launch(st, k_w_entries, nnz, (const uint64_t *)k2, (const uint32_t *)i2, nnz, q, pq[0], pq[1], pq[2],
+             (const uint64_t *)roff, col, val, l2w, fs, img);
+    }
+    uint64_t *w2l = A.get<uint64_t>("w.w2l", E->n_wires + 1);
+    launch(st, k_w_w2l, S, l2w, S, w2l);
+    std::vector<int32_t> hl2w(S);
+    HC(hipMemcpyAsync(hl2w.data(), l2w, 4 * S, hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> hw2l(E->n_wires);
+    if (E->n_wires) HC(hipMemcpyAsync(hw2l.data(), w2l, 8 * E->n_wires, hipMemcpyDeviceToHost, st));
+    int err = 0;
+    HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    if (err) throw RsError(RS_E_INTERNAL, "constraint mentions a removed signal (apply_raw_correspondence panics)");
+    // the host-side tail rows, serialised like the device records
+    std::vector<uint8_t> tail;
+    uint64_t n_tail = 0;
+    for (const HostCon &c : E->out_host_tail) {
+      if (c.k[0].empty() && c.k[1].empty() && c.k[2].empty()) continue;
+      ++n_tail;
+      for (int q = 0; q < 3; ++q) {
+        std::vector<std::pair<uint64_t, uint32_t>> ord;
+        for (uint32_t i = 0; i < c.k[q].size(); ++i) {
+          const uint32_t k = c.k[q][i];
+          const int32_t w = k == 0 ? 0 : hl2w[k];
+          if (w < 0) throw RsError(RS_E_INTERNAL, "constraint mentions a removed signal (apply_raw_correspondence panics)");
+          uint64_t key = 0;  // the LE-byte-string key (injective in w)
+          const int len = w == 0 ? 1 : (32 - __builtin_clz((uint32_t)w) + 7) / 8;
+          for (int b = 0; b < 4; ++b) key = (key << 9) | (b < len ? ((((uint32_t)w) >> (8 * b)) & 0xffu) + 1 : 0);
+          ord.push_back({key, i});
+        }
+        std::sort(ord.begin(), ord.end());
+        const uint32_t m = (uint32_t)ord.size();
+        tail.insert(tail.end(), (const uint8_t *)&m, (const uint8_t *)&m + 4);
+        for (auto &x : ord) {
+          const uint32_t k = c.k[q][x.second];
+          const uint32_t w = k == 0 ? 0u : (uint32_t)hl2w[k];
+          tail.insert(tail.end(), (const uint8_t *)&w, (const uint8_t *)&w + 4);
+          const uint8_t *v = (const uint8_t *)&c.v[q][4 * x.second];
+          tail.insert(tail.end(), v, v + fs);
+        }
+      }
+    }
+    std::vector<uint8_t> gates;
+    bool with_gates = false;
+    if (o0_r1cs && !r1cs_gate_sections(o0_r1cs, hl2w.data(), S, gates, with_gates)) return RS_E_INVALID;
+    f = fopen(path, "wb");
+    if (!f) throw RsError(RS_E_INVALID, std::string("cannot write ") + path);
+    auto put32 = [&](uint32_t v) { fwrite(&v, 4, 1, f); };
+    auto put64 = [&](uint64_t v) { fwrite(&v, 8, 1, f); };
+    fwrite(with_gates ? "r1cs\x01\x00\x00\x00\x05\x00\x00\x00" : "r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
+    put32(2);
+    put64(dev_bytes + tail.size());
+    // the device image in chunks: D2H of chunk i + 1 overlaps the write of chunk i
+    constexpr uint64_t kChunk = 64ull << 20;
+    void *pb[2] = {pin_get(E, 11, kChunk), pin_get(E, 12, kChunk)};
+    hipEvent_t evc[2] = {E->ev_lvl[0], E->ev_lvl[1]};
+    const uint8_t *src = (const uint8_t *)img;
+    uint64_t done = 0;
+    int cur = 0;
+    if (dev_bytes) {
+      HC(hipMemcpyAsync(pb[0], src, std::min(kChunk, dev_bytes), hipMemcpyDeviceToHost, st));
+      HC(hipEventRecord(evc[0], st));
+    }
+    while (done < dev_bytes) {
+      const uint64_t len = std::min(kChunk, dev_bytes - done);
+      const uint64_t nx = done + len;
+      if (nx < dev_bytes) {
+        HC(hipMemcpyAsync(pb[cur ^ 1], src + nx, std::min(kChunk, dev_bytes - nx), hipMemcpyDeviceToHost, st));
+        HC(hipEventRecord(evc[cur ^ 1], st));
+      }
+      HC(hipEventSynchronize(evc[cur]));
+      fwrite(pb[cur], 1, len, f);
+      done = nx;
+      cur ^= 1;
+    }
+    if (!tail.empty()) fwrite(tail.data(), 1, tail.size(), f);
+    // header (r1cs_writer.rs:246-269)
+    put32(1);
+    put64(4 + fs + 4 * 4 + 8 + 4);
+    put32(fs);
+    fwrite(E->prime, 1, fs, f);
+    put32((uint32_t)E->n_wires);
+    put32((uint32_t)E->n_pub_out);
+    put32((uint32_t)E->n_pub_in);
+    put32((uint32_t)E->n_priv_in);
+    put64(S);
+    put32((uint32_t)(n + n_tail));
+    // wire -> label
+    put32(3);
+    put64(8 * E->n_wires);
+    if (E->n_wires) fwrite(hw2l.data(), 8, E->n_wires, f);
+    if (with_gates) fwrite(gates.data(), 1, gates.size(), f);
+    const bool ok = !ferror(f);
+    fclose(f);
+    f = nullptr;
+    if (!ok) throw RsError(RS_E_INVALID, "write error");
+    E->stats.write_ms = now_ms() - t0;
+    return RS_OK;
+  } catch (const RsError &e) {
+    if (f) fclose(f);
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    if (f) fclose(f);
     set_error(e.what());
     return RS_E_INTERNAL;
   }

@@ -64,6 +64,10 @@ inline void to_lc(Block &b, rs_lc &lc) {
   b = Block();
 }
 
+// r1cs_io.cpp: the output's custom-gate sections (4 and 5) from an --O0 file, label_to_wire applied
+bool r1cs_gate_sections(const char *o0_r1cs, const int32_t *l2w, uint64_t n_labels, std::vector<uint8_t> &out,
+                        bool &present);
+
 inline void free_lc(rs_lc &lc) {
   free(lc.ptr);
   free(lc.col);

@@ -129,6 +129,55 @@ static bool read_gate_applications(const std::vector<uint8_t> &buf, const R1csSe
   return true;
 }
 
+// Sections 4 and 5 of the output as r1cs_porting.rs:54-121 writes them, from an --O0 file's:
+// section 4 unchanged, section 5 with its signals mapped label -> wire.  `out` gets the two sections
+// with their headers (empty, present = false, when the --O0 file has neither).
+bool r1cs_gate_sections(const char *o0_r1cs, const int32_t *l2w, uint64_t n_labels, std::vector<uint8_t> &out,
+                        bool &present) {
+  out.clear();
+  present = false;
+  std::vector<uint8_t> buf;
+  if (!read_file(o0_r1cs, buf) || buf.size() < 12 || memcmp(buf.data(), "r1cs", 4) != 0) {
+    set_error(std::string("cannot read r1cs file ") + o0_r1cs);
+    return false;
+  }
+  R1csSections S;
+  if (!scan_sections(buf, S)) return false;
+  if (!S.have[4] && !S.have[5]) return true;
+  present = true;
+  auto put32 = [&](uint32_t v) { out.insert(out.end(), (uint8_t *)&v, (uint8_t *)&v + 4); };
+  auto put64 = [&](uint64_t v) { out.insert(out.end(), (uint8_t *)&v, (uint8_t *)&v + 8); };
+  put32(4);
+  if (S.have[4]) {
+    put64(S.size[4]);
+    out.insert(out.end(), buf.begin() + S.off[4], buf.begin() + S.off[4] + S.size[4]);
+  } else {
+    put64(4);
+    put32(0);
+  }
+  std::vector<std::pair<uint32_t, std::vector<uint64_t>>> apps;
+  if (S.have[5] && !read_gate_applications(buf, S, n_labels, nullptr, &apps)) return false;
+  std::vector<uint8_t> s5;
+  auto p32 = [&](uint32_t v) { s5.insert(s5.end(), (uint8_t *)&v, (uint8_t *)&v + 4); };
+  auto p64 = [&](uint64_t v) { s5.insert(s5.end(), (uint8_t *)&v, (uint8_t *)&v + 8); };
+  p32((uint32_t)apps.size());
+  for (auto &a : apps) {
+    p32(a.first);
+    p32((uint32_t)a.second.size());
+    for (uint64_t sg : a.second) {
+      if (l2w[sg] < 0) {
+        set_error("custom-gate signal without a wire (SignalMap::get(..).unwrap() panics)");
+        return false;
+      }
+      p64((uint64_t)l2w[sg]);
+    }
+  }
+  put32(5);
+  put64(s5.size());
+  out.insert(out.end(), s5.begin(), s5.end());
+  return true;
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -307,7 +356,7 @@ void rs_input_free(rs_input *in) {
 
 // r1cs_porting.rs:4-124.  `gates` (optional): the --O0 file's custom-gate sections, re-emitted as
 // the O2 writer does (:54-121): section 4 unchanged, section 5 with every signal mapped label -> wire.
-static int write_r1cs(const char *path, const rs_input *in, const rs_output *out, const std::vector<uint8_t> *o0,
+static int write_r1cs(const char *path, const rs_input *in, const rs_output *out, const char *o0_path,
                       const R1csSections *gates) {
   uint64_t p[4];
   if (!prime_of(in, p)) { set_error("unknown prime"); return RS_E_INVALID; }
@@ -396,39 +445,13 @@ static int write_r1cs(const char *path, const rs_input *in, const rs_output *out
   fwrite(hdr.data(), 1, hdr.size(), f);
   fwrite(w2l.data(), 8, w2l.size(), f);
   if (with_gates) {
-    hdr.clear();
-    put32(hdr, 4);
-    if (gates->have[4]) {
-      put64(hdr, gates->size[4]);
-      hdr.insert(hdr.end(), o0->begin() + gates->off[4], o0->begin() + gates->off[4] + gates->size[4]);
-    } else {
-      put64(hdr, 4);
-      put32(hdr, 0);
-    }
-    std::vector<std::pair<uint32_t, std::vector<uint64_t>>> apps;
-    if (gates->have[5] && !read_gate_applications(*o0, *gates, out->n_labels, nullptr, &apps)) {
+    std::vector<uint8_t> gs;
+    bool present = false;
+    if (!r1cs_gate_sections(o0_path, out->label_to_wire, out->n_labels, gs, present)) {
       fclose(f);
       return RS_E_INVALID;
     }
-    std::vector<uint8_t> s5;
-    put32(s5, (uint32_t)apps.size());
-    for (auto &a : apps) {
-      put32(s5, a.first);
-      put32(s5, (uint32_t)a.second.size());
-      for (uint64_t s : a.second) {
-        const int64_t w = out->label_to_wire[s];
-        if (w < 0) {
-          fclose(f);
-          set_error("custom-gate signal without a wire (SignalMap::get(..).unwrap() panics)");
-          return RS_E_INTERNAL;
-        }
-        put64(s5, (uint64_t)w);
-      }
-    }
-    put32(hdr, 5);
-    put64(hdr, s5.size());
-    hdr.insert(hdr.end(), s5.begin(), s5.end());
-    fwrite(hdr.data(), 1, hdr.size(), f);
+    fwrite(gs.data(), 1, gs.size(), f);
   }
   bool ok = !ferror(f);
   fclose(f);
@@ -450,7 +473,7 @@ int rs_write_r1cs_gates(const char *path, const rs_input *in, const rs_output *o
   }
   R1csSections S;
   if (!scan_sections(buf, S)) return RS_E_INVALID;
-  return write_r1cs(path, in, out, &buf, &S);
+  return write_r1cs(path, in, out, o0_r1cs, &S);
 }
 
 int rs_write_constraints_json(const char *path, const rs_output *out) {

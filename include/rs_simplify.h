@@ -177,6 +177,7 @@ typedef struct rs_stats {
   double h2d_wait_ms;          /* host time the run spent waiting for input groups to land  */
   double d2h_ms;               /* D2H of the result into the engine's pinned buffers        */
   double host_total_ms;        /* rs_engine_simplify: host input -> host output             */
+  double write_ms;             /* ABI 5: the last rs_engine_write_r1cs (device image + file)  */
 } rs_stats;
 
 typedef struct rs_engine rs_engine;
@@ -208,6 +209,13 @@ void rs_engine_destroy(rs_engine *eng);
  * work too (HIP stages them), slower.
  */
 int rs_engine_simplify(rs_engine *eng, const rs_input *in, const rs_flags *fl, const rs_output **out);
+
+/* The engine's last result written as a .r1cs (constraint_list/src/r1cs_porting.rs:4-124; SURVEY
+ * 8(f) rank 2): byte-identical to rs_write_r1cs on the fetched output, with the constraint section
+ * (wire correspondence + LE-byte key order per row) built on the device and streamed to the file.
+ * o0_r1cs (may be NULL): copy its custom-gate sections like rs_write_r1cs_gates.  Time in
+ * rs_stats.write_ms. */
+int rs_engine_write_r1cs(rs_engine *eng, const char *path, const char *o0_r1cs);
 
 /* Page-locked host memory (hipHostMalloc) for the CSR blocks a caller marshals the Simplifier into,
  * so rs_engine_simplify's H2D runs at PCIe speed.  NULL without a device. */

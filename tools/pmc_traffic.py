@@ -16,7 +16,7 @@ import sys
 
 # bench.py KERNELS name -> substring of the rocprofv3 kernel name
 GROUPS = {
-    "k_big_main<512> (head)": "k_big_main<512u>",
+    "k_big_main_lds (head)": "k_big_main_lds",
     "k_big_main<256> (tail)": "k_big_main<256u>",
     "k_nl_fill": "rs::k_nl_fill(",
     "k_round_fill": "rs::k_round_fill(",
