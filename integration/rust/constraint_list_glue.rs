@@ -1,0 +1,158 @@
+// constraint_list_glue.rs -- goes into the reference's constraint_list crate as
+// `src/gpu_glue.rs` (with `rs-simplify-sys` as a dependency behind a `mi355x` feature).  It is the
+// body that replaces `constraint_simplification::simplification(&mut Simplifier)`
+// (constraint_list/src/constraint_simplification.rs:442) when the feature is on:
+//
+//     pub fn simplification(smp: &mut Simplifier) -> (ConstraintStorage, SignalMap, usize) {
+//         #[cfg(feature = "mi355x")]
+//         { return crate::gpu_glue::simplification_mi355x(smp); }
+//         // ... the reference body, unchanged ...
+//     }
+//
+// Marshalling: the three LinkedLists are already in the DFS order map_tree built them
+// (dag/src/map_to_constraint_list.rs:12-44); the non-linear rows come from the DAG encoding in the
+// EncodingIterator DFS (constraint_list/src/lib.rs:65-108), offsets applied.  The library takes
+// canonical 4 x u64 little-endian coefficients and returns the storage order with ORIGINAL signal
+// ids plus an int32 label -> wire map; the glue rebuilds ConstraintStorage and SignalMap from them.
+// A non-zero status panics with rs_last_error(), as the reference panics on its own invariants.
+use crate::{EncodingIterator, SignalMap, Simplifier};
+use circom_algebra::algebra::Constraint;
+use circom_algebra::constraint_storage::ConstraintStorage;
+use circom_algebra::num_bigint::BigInt;
+use rs_simplify_sys as ffi;
+use std::collections::HashMap;
+use std::ffi::CStr;
+
+type C = Constraint<usize>;
+
+/// One owned CSR block (the arrays an rs_lc points at).
+struct Csr {
+    ptr: Vec<u64>,
+    col: Vec<u32>,
+    val: Vec<u64>,
+}
+impl Csr {
+    fn new() -> Csr {
+        Csr { ptr: vec![0], col: Vec::new(), val: Vec::new() }
+    }
+    /// Appends one linear combination; keys ascending (the library sorts too, but sorted rows let
+    /// rs_engine_simplify start build_clusters before the values arrive).
+    fn push(&mut self, m: &HashMap<usize, BigInt>) {
+        let mut keys: Vec<_> = m.iter().filter(|(_, v)| !v.is_zero()).collect();
+        keys.sort_by_key(|(k, _)| **k);
+        for (k, v) in keys {
+            self.col.push(*k as u32);
+            let (_, digits) = v.to_u64_digits(); // canonical (< p)
+            for i in 0..4 {
+                self.val.push(*digits.get(i).unwrap_or(&0));
+            }
+        }
+        self.ptr.push(self.col.len() as u64);
+    }
+    fn lc(&mut self) -> ffi::rs_lc {
+        ffi::rs_lc {
+            n_rows: (self.ptr.len() - 1) as u64,
+            nnz: self.col.len() as u64,
+            ptr: self.ptr.as_mut_ptr(),
+            col: self.col.as_mut_ptr(),
+            val: self.val.as_mut_ptr(),
+        }
+    }
+}
+
+fn prime_id(field: &BigInt) -> (u32, [u64; 4]) {
+    // program_structure/src/utils/constants.rs:3-13 in ffi enum order; anything else is passed raw
+    let (_, d) = field.to_u64_digits();
+    let mut p = [0u64; 4];
+    for (i, x) in d.iter().take(4).enumerate() {
+        p[i] = *x;
+    }
+    (255, p) // RS_PRIME_CUSTOM: the library recognises the named primes from the value
+}
+
+fn non_linear_rows(iter: EncodingIterator, a: &mut Csr, b: &mut Csr, c: &mut Csr) {
+    let mut iter = iter;
+    let (_, non_linear) = EncodingIterator::take(&mut iter);
+    for row in non_linear {
+        a.push(row.a());
+        b.push(row.b());
+        c.push(row.c());
+    }
+    for edge in EncodingIterator::edges(&iter) {
+        let next = EncodingIterator::next(&iter, edge);
+        non_linear_rows(next, a, b, c);
+    }
+}
+
+pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, SignalMap, usize) {
+    let (mut ce, mut eq, mut lin) = (Csr::new(), Csr::new(), Csr::new());
+    for r in &smp.cons_equalities {
+        ce.push(r.c());
+    }
+    for r in &smp.equalities {
+        eq.push(r.c());
+    }
+    for r in &smp.linear {
+        lin.push(r.c());
+    }
+    let (mut na, mut nb, mut nc) = (Csr::new(), Csr::new(), Csr::new());
+    non_linear_rows(EncodingIterator::new(&smp.dag_encoding), &mut na, &mut nb, &mut nc);
+    let mut forbidden: Vec<u32> = smp.forbidden.iter().map(|s| *s as u32).collect();
+    forbidden.sort_unstable();
+    let (pid, prime) = prime_id(&smp.field);
+    let input = ffi::rs_input {
+        prime_id: pid,
+        prime,
+        max_signal: smp.max_signal as u64,
+        n_pub_out: smp.no_public_outputs as u64,
+        n_pub_in: smp.no_public_inputs as u64,
+        n_priv_in: smp.no_private_inputs as u64,
+        n_forbidden: forbidden.len() as u64,
+        forbidden: forbidden.as_mut_ptr(),
+        cons_eq: ce.lc(),
+        eq: eq.lc(),
+        linear: lin.lc(),
+        nl_a: na.lc(),
+        nl_b: nb.lc(),
+        nl_c: nc.lc(),
+    };
+    let flags = ffi::rs_flags {
+        flag_s: smp.flag_s as u32,
+        use_old_heuristics: smp.flag_old_heuristics as u32,
+        no_rounds: smp.no_rounds as u64,
+        emit_substitution_log: smp.port_substitution as u32,
+        device: 0,
+    };
+    let mut out: *mut ffi::rs_output = std::ptr::null_mut();
+    let rc = unsafe { ffi::rs_simplify(&input, &flags, &mut out) };
+    if rc != ffi::RS_OK {
+        let msg = unsafe { CStr::from_ptr(ffi::rs_last_error()) }.to_string_lossy().into_owned();
+        panic!("rs_simplify failed ({}): {}", rc, msg);
+    }
+    let o = unsafe { &*out };
+    let map_of = |lc: &ffi::rs_lc, r: usize| -> HashMap<usize, BigInt> {
+        let mut m = HashMap::new();
+        let (lo, hi) = unsafe { (*lc.ptr.add(r) as usize, *lc.ptr.add(r + 1) as usize) };
+        for e in lo..hi {
+            let k = unsafe { *lc.col.add(e) } as usize;
+            let limbs: Vec<u64> = (0..4).map(|i| unsafe { *lc.val.add(4 * e + i) }).collect();
+            m.insert(k, BigInt::from_slice_native(&limbs)); // canonical, non-negative
+        }
+        m
+    };
+    let mut storage = ConstraintStorage::new();
+    for r in 0..o.n_constraints as usize {
+        // Constraint::new is private (algebra.rs:1012): the shim adds `pub fn new_unchecked(a, b, c)`
+        storage.add_constraint(C::new_unchecked(map_of(&o.a, r), map_of(&o.b, r), map_of(&o.c, r)));
+    }
+    let mut signal_map = SignalMap::with_capacity(o.n_wires as usize);
+    for s in 0..o.n_labels as usize {
+        let w = unsafe { *o.label_to_wire.add(s) };
+        if w >= 0 {
+            signal_map.insert(s, w as usize);
+        }
+    }
+    let npiw = o.no_private_inputs_witness as usize;
+    unsafe { ffi::rs_output_free(out) };
+    (storage, signal_map, npiw)
+}
