@@ -25,6 +25,7 @@
 
 #include "host_common.hpp"
 #include "kernels.hpp"
+#include "frames_wave.hpp"
 #include "cluster.hpp"
 #include "writer.hpp"
 
@@ -1881,6 +1882,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   };
   unsigned long long *d_bytes = A.get<unsigned long long>("nl.bytes", 1);
   HC(hipMemsetAsync(d_bytes, 0, 8, st));
+  int *d_fw_err = A.get<int>("fw.err", 1);  // k_frames_wave batch bounds (checked with the input checks)
+  HC(hipMemsetAsync(d_fw_err, 0, 4, st));
   FrameArgs fr;
   fr.F = E->F;
   fr.eq_rep = eq_rep;
@@ -1910,7 +1913,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   // kernel time is read from (e0, e1) once the caller synchronises
   auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1) {
     stage_nl();
-    NLArgs a;
+    NLArgs a{};
     a.fr = fr;
     a.a = ia; a.b = ib; a.c = ic;
     a.cap_a = ca; a.cap_b = cb; a.cap_c = cc;
@@ -1936,9 +1939,55 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     sa.key = sb.key = sc.key = heap_k;
     sa.val = sb.val = sc.val = heap_v;
     a.oa = sa; a.ob = sb; a.oc = sc;
+    // whole waves on batches of rows (frames_wave.hpp); the rows too large for a batch, one lane each
+    FrameWaveArgs w{};
+    w.fr = fr;
+    w.in[0] = ia; w.in[1] = ib; w.in[2] = ic;
+    w.out[0] = sa; w.out[1] = sb; w.out[2] = sc;
+    w.cap[0] = ca; w.cap[1] = cb; w.cap[2] = cc;
+    w.ids = ids;
+    w.n = n;
+    w.late = phase == 1 ? nl_late : nullptr;
+    w.big = A.get<uint32_t>(phase == 1 ? "nl.big1" : "nl.big2", n);
+    w.n_big = A.get<unsigned>(phase == 1 ? "nl.nbig1" : "nl.nbig2", 1);
+    w.err = d_fw_err;
+    w.bytes = d_bytes;
+    HC(hipMemsetAsync(w.n_big, 0, 4, st));
+#ifdef RS_FWCLK
+    w.clk = A.get<unsigned long long>(phase == 1 ? "fw.clk1" : "fw.clk2", 32 + 8 * 64);
+    HC(hipMemsetAsync(w.clk, 0, 8 * (32 + 8 * 64), st));
+#endif
+    a.xlist = w.big;
+    a.n_xlist = w.n_big;
     HC(hipEventRecord(e0, st));
-    launch(st, k_nl_fill, n, a);
+    launch(st, k_frames_wave, n, w);
+    launch(st, k_nl_fill, n, a);  // a grid for every row: the list may be long, idle lanes leave at once
     HC(hipEventRecord(e1, st));
+    if (g_prof_env) {
+      unsigned nb = 0;
+      HC(hipMemcpyAsync(&nb, w.n_big, 4, hipMemcpyDeviceToHost, st));
+      HC(hipStreamSynchronize(st));
+      fprintf(stderr, "[rs-prof] nl phase %d: %u rows over a wave batch\n", phase, nb);
+      if (w.clk) {
+        unsigned long long c[32 + 8 * 64];
+        HC(hipMemcpy(c, w.clk, sizeof c, hipMemcpyDeviceToHost));
+        for (int q = 0; q < 0; ++q) {
+          const unsigned long long *d = c + 32 + q * 64;
+          fprintf(stderr, "[rs-prof] zero A row %llu: %llu entries:", d[0], d[1]);
+          for (unsigned i = 0; i < d[1] && i < 6; ++i)
+            fprintf(stderr, " (key/slot %llu kind %llu w %llu)", d[2 + i] >> 32, (d[2 + i] >> 16) & 0xff, d[2 + i] & 0xffff);
+          fprintf(stderr, " | %llu terms:", d[8]);
+          for (unsigned i = 0; i < d[8] && i < 24; ++i) fprintf(stderr, " %llu:%llx", d[9 + 2 * i] >> 32, d[10 + 2 * i]);
+          fprintf(stderr, "\n");
+        }
+        fprintf(stderr, "[rs-prof] frames clocks (Mcycles summed over waves): groups %.1f entries %.1f terms %.1f rank %.1f "
+                "heads %.1f emit %.1f rows %.1f plan %.1f | batches %llu, wave total %.1f over %llu waves\n",
+                c[0] / 1e6, c[1] / 1e6, c[2] / 1e6, c[3] / 1e6, c[4] / 1e6, c[5] / 1e6, c[6] / 1e6, c[7] / 1e6, c[8],
+                c[9] / 1e6, c[10]);
+        fprintf(stderr, "[rs-prof] frames fallbacks: A const %llu, B const %llu | emit: loads %.1f values %.1f sync %.1f stores %.1f\n",
+                c[12], c[13], c[16] / 1e6, c[17] / 1e6, c[18] / 1e6, c[19] / 1e6);
+      }
+    }
     E->stats.apply_kernel_launches++;
   };
   auto nl_ms = [&](hipEvent_t e0, hipEvent_t e1) {
@@ -2194,7 +2243,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       // apply to every storage row (apply_substitution_to_map, :345-396)
       std::vector<std::pair<uint64_t, uint32_t>> turned;  // (order key, storage id)
       if (n_st && nU) {
-        RoundArgs ra;
+        RoundArgs ra{};
         ra.F = E->F;
         ra.a = ta_; ra.b = tb_; ra.c = tc_;
         uint64_t *ca = A.get<uint64_t>("r.capa", n_st), *cb = A.get<uint64_t>("r.capb", n_st), *cc = A.get<uint64_t>("r.capc", n_st);
@@ -2240,9 +2289,39 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         ra.bytes = A.get<unsigned long long>("r.bytes", 1);
         HC(hipMemsetAsync(ra.bytes, 0, 8, st));
         if (ra.n_ids) {
+          FrameWaveArgs w{};
+          w.fr.F = E->F;
+          w.fr.sub_of = r_sub_of;
+          w.fr.h_off = ra.h_off; w.fr.h_len = ra.h_len; w.fr.pk = ra.pk; w.fr.pv = ra.pv;
+          w.in[0] = ta_; w.in[1] = tb_; w.in[2] = tc_;
+          w.out[0] = oa; w.out[1] = ob; w.out[2] = oc;
+          w.cap[0] = ca; w.cap[1] = cb; w.cap[2] = cc;
+          w.cap_by_row = 1;
+          w.ids = ra.ids;
+          w.n = ra.n_ids;
+          w.big = A.get<uint32_t>("r.big", ra.n_ids);
+          w.n_big = A.get<unsigned>("r.nbig", 2);
+          w.round = 1;
+          w.touched = ra.touched;
+          w.turn_list = A.get<uint32_t>("r.turnlist", ra.n_ids);
+          w.n_turn = w.n_big + 1;
+          w.err = d_fw_err;
+          w.bytes = ra.bytes;
+          HC(hipMemsetAsync(w.n_big, 0, 8, st));
+          RoundArgs rb = ra, rt = ra;
+          rb.rlist = w.big; rb.n_rlist = w.n_big;
+          rt.rlist = w.turn_list; rt.n_rlist = w.n_turn;
           HC(hipEventRecord(E->ev0, st));
-          launch(st, k_round_fill, ra.n_ids, ra);
+          launch(st, k_frames_wave, ra.n_ids, w);
+          launch(st, k_round_fill, ra.n_ids, rb);
+          launch(st, k_round_turn, ra.n_ids, rt);
           HC(hipEventRecord(E->ev1, st));
+          if (g_prof_env) {
+            unsigned nb[2] = {0, 0};
+            HC(hipMemcpyAsync(nb, w.n_big, 8, hipMemcpyDeviceToHost, st));
+            HC(hipStreamSynchronize(st));
+            fprintf(stderr, "[rs-prof] round: %llu rows, %u over a wave batch, %u turn\n", (unsigned long long)ra.n_ids, nb[0], nb[1]);
+          }
           float fm = 0;
           unsigned long long fb = 0;
           HC(hipMemcpyAsync(&fb, ra.bytes, 8, hipMemcpyDeviceToHost, st));
@@ -2488,10 +2567,12 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     E->out_host_tail = std::move(lconst);
   }
   load_wait_all(E);  // a group the path never needed (e.g. no non-linear rows) is still checked
-  int err = 0;
+  int err = 0, fw_err = 0;
   HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
+  HC(hipMemcpyAsync(&fw_err, d_fw_err, 4, hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
   if (err) throw RsError(RS_E_INVALID, "input rejected by the device checks (code " + std::to_string(err) + ")");
+  if (fw_err) throw RsError(RS_E_INTERNAL, "frames batch over its bounds (code " + std::to_string(fw_err) + ")");
   E->stats.final_ms = now_ms() - Tf;
   E->stats.total_ms = now_ms() - T0;
   E->stats.h2d_wait_ms = E->h2d_wait_ms;

@@ -3033,6 +3033,9 @@ struct NLArgs {
   int phase;
   const uint8_t *hmark;  // signal -> occurs in a row of a head cluster
   uint64_t *late;
+  // k_nl_fill only: the positions k_frames_wave left to it (rows too large for a wave's LDS batch)
+  const uint32_t *xlist;
+  const unsigned *n_xlist;
 };
 
 // Marks the signals of the head clusters' rows (signal 0 is never substituted).
@@ -3085,9 +3088,12 @@ __global__ void k_nl_count(NLArgs A) {
   }
 }
 
+// One lane per row: the rows k_frames_wave hands over (xlist), or every row when xlist is null.
 __global__ void k_nl_fill(NLArgs A) {
   unsigned long long bytes = 0;
-  for (uint64_t x = gtid(); x < A.n; x += gstride()) {
+  const uint64_t nx = A.xlist ? *A.n_xlist : A.n;
+  for (uint64_t xi = gtid(); xi < nx; xi += gstride()) {
+    const uint64_t x = A.xlist ? A.xlist[xi] : xi;
     const uint64_t r = A.ids ? A.ids[x] : x;
     if (A.phase == 1 && A.late[r]) continue;
     uint64_t oa = A.oa.off[r], ob = A.ob.off[r], oc = A.oc.off[r];
@@ -3132,6 +3138,9 @@ struct RoundArgs {
   uint64_t c_base;
   const uint32_t *ids;     // the rows a substitution touches (cap_c != 0), compacted
   uint64_t n_ids;
+  // k_round_fill / k_round_turn: the rows k_frames_wave left (rlist), or every id when null
+  const uint32_t *rlist;
+  const unsigned *n_rlist;
   unsigned long long *bytes;  // algorithmic bytes: 36 per entry read (row + right-hand sides) or written
 };
 __global__ void k_touch_flags(const uint64_t *cap_c, uint64_t n, uint64_t *flag) {
@@ -3155,24 +3164,91 @@ __global__ void k_round_count(RoundArgs A) {
 // is the (zero-free, sorted) map empty or constant-only?
 __device__ __forceinline__ bool d_const_or_empty(const uint32_t *k, uint32_t n) { return n == 0 || (n == 1 && k[0] == 0); }
 
-// One lane per touched row (the compacted list: untouched rows are neither read nor written here;
-// turn = -1 and touched = 0 were set for every row beforehand).
+// The rank (in the round's substitution order) of the first substitution after which the row's
+// A or B is constant or empty -- for a row whose final A or B is (the caller checked).  Replays the
+// substitutions one by one on copies of A and B held in the row's A / B output regions (their final
+// content is dropped anyway: fix_constraint clears A and B of such a row) with the row's scratch
+// [2 * (oc - c_base), + 2 * capc) for the ranks and merges.  Writes turn[r] (-2: linear on input).
+__device__ inline void d_round_turn(const RoundArgs &A, uint64_t r) {
+  const FieldP &F = A.F;
+  const uint64_t oa = A.oa.off[r], ob = A.ob.off[r], oc = A.oc.off[r];
+  const uint32_t capc = (uint32_t)A.cap_c[r];
+  // applicable ranks from A u B, ascending
+  uint32_t *rk_ = A.tmpk + 2 * (oc - A.c_base);
+  uint32_t nr = 0;
+  for (int part = 0; part < 2; ++part) {
+    const DRows &P = part ? A.b : A.a;
+    for (uint32_t i = 0; i < P.len[r]; ++i) {
+      int32_t q = A.rank_of[P.key[P.off[r] + i]];
+      if (q >= 0) rk_[nr++] = (uint32_t)q;
+    }
+  }
+  d_heap_sort_u32(rk_, nr);
+  uint32_t na = A.a.len[r], nb = A.b.len[r];
+  uint32_t *ak = A.oa.key + oa, *bk = A.ob.key + ob;
+  Fe *av = A.oa.val + oa, *bv = A.ob.val + ob;
+  for (uint32_t i = 0; i < na; ++i) { ak[i] = A.a.key[A.a.off[r] + i]; av[i] = A.a.val[A.a.off[r] + i]; }
+  for (uint32_t i = 0; i < nb; ++i) { bk[i] = A.b.key[A.b.off[r] + i]; bv[i] = A.b.val[A.b.off[r] + i]; }
+  if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = -2;  // already linear
+  for (uint32_t q = 0; q < nr && A.turn[r] == -1; ++q) {
+    if (q > 0 && rk_[q] == rk_[q - 1]) continue;
+    for (int part = 0; part < 2; ++part) {
+      uint32_t *pk_ = part ? bk : ak;
+      Fe *pv_ = part ? bv : av;
+      uint32_t &pn = part ? nb : na;
+      // find the signal with this rank in the part
+      uint32_t fi = RS_NONE;
+      for (uint32_t i = 0; i < pn; ++i)
+        if (A.rank_of[pk_[i]] == (int32_t)rk_[q]) { fi = i; break; }
+      if (fi == RS_NONE) continue;
+      int32_t s = A.sub_of[pk_[fi]];
+      Fe val = pv_[fi];
+      const uint32_t *hk = A.pk + A.h_off[s];
+      const Fe *hv = A.pv + A.h_off[s];
+      uint32_t hl = A.h_len[s];
+      // merge (pn - 1 + hl <= the part's capacity) via the scratch after the ranks
+      uint32_t *mk = A.tmpk + 2 * (oc - A.c_base) + capc;
+      Fe *mv = A.tmpv + 2 * (oc - A.c_base) + capc;
+      uint32_t i = 0, j = 0, w = 0;
+      while (i < pn || j < hl) {
+        if (i == fi) { ++i; continue; }
+        if (j >= hl || (i < pn && pk_[i] < hk[j])) { mk[w] = pk_[i]; mv[w] = pv_[i]; ++i; }
+        else if (i >= pn || hk[j] < pk_[i]) { mk[w] = hk[j]; mv[w] = fmul(F, val, hv[j]); ++j; }
+        else { mk[w] = pk_[i]; mv[w] = fadd(F, pv_[i], fmul(F, val, hv[j])); ++i; ++j; }
+        ++w;
+      }
+      w = d_drop_zeros(mk, mv, w);
+      for (uint32_t t = 0; t < w; ++t) { pk_[t] = mk[t]; pv_[t] = mv[t]; }
+      pn = w;
+    }
+    if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = (int32_t)rk_[q];
+  }
+}
+
+__device__ __forceinline__ FrameArgs d_round_frames(const RoundArgs &A) {
+  FrameArgs fr;
+  fr.F = A.F;
+  fr.eq_rep = nullptr;
+  fr.ce_has = nullptr;
+  fr.ce_val = nullptr;
+  fr.sub_of = A.sub_of;
+  fr.h_off = A.h_off;
+  fr.h_len = A.h_len;
+  fr.pk = A.pk;
+  fr.pv = A.pv;
+  return fr;
+}
+
+// One lane per touched row: the rows k_frames_wave left (rlist), or every id when rlist is null
+// (turn = -1 and touched = 0 were set for every row beforehand).
 __global__ void k_round_fill(RoundArgs A) {
   const FieldP &F = A.F;
   unsigned long long bytes = 0;
-  for (uint64_t i = gtid(); i < A.n_ids; i += gstride()) {
-    const uint64_t r = A.ids[i];
+  const uint64_t n = A.rlist ? *A.n_rlist : A.n_ids;
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint64_t r = A.rlist ? A.rlist[i] : A.ids[i];
     A.touched[r] = 1;
-    FrameArgs fr;
-    fr.F = F;
-    fr.eq_rep = nullptr;
-    fr.ce_has = nullptr;
-    fr.ce_val = nullptr;
-    fr.sub_of = A.sub_of;
-    fr.h_off = A.h_off;
-    fr.h_len = A.h_len;
-    fr.pk = A.pk;
-    fr.pv = A.pv;
+    const FrameArgs fr = d_round_frames(A);
     uint64_t oa = A.oa.off[r], ob = A.ob.off[r], oc = A.oc.off[r];
     uint32_t capa = (uint32_t)A.cap_a[r], capb = (uint32_t)A.cap_b[r], capc = (uint32_t)A.cap_c[r];
     uint32_t mx = capa > capb ? capa : capb;
@@ -3184,62 +3260,7 @@ __global__ void k_round_fill(RoundArgs A) {
     uint32_t na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
     uint32_t nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
     if (d_const_or_empty(A.oa.key + oa, na) || d_const_or_empty(A.ob.key + ob, nb)) {
-      // ---- first substitution (in round order) after which A or B is constant/empty
-      {
-        // applicable ranks from A u B, ascending; per-row scratch = [2*oc, 2*oc + 2*capc)
-        uint32_t *rk_ = A.tmpk + 2 * (oc - A.c_base);
-        uint32_t nr = 0;
-        for (int part = 0; part < 2; ++part) {
-          const DRows &P = part ? A.b : A.a;
-          for (uint32_t i = 0; i < P.len[r]; ++i) {
-            int32_t q = A.rank_of[P.key[P.off[r] + i]];
-            if (q >= 0) rk_[nr++] = (uint32_t)q;
-          }
-        }
-        d_heap_sort_u32(rk_, nr);
-        // incremental application on copies of A and B held in the output regions
-        uint32_t na = A.a.len[r], nb = A.b.len[r];
-        uint32_t *ak = A.oa.key + oa, *bk = A.ob.key + ob;
-        Fe *av = A.oa.val + oa, *bv = A.ob.val + ob;
-        for (uint32_t i = 0; i < na; ++i) { ak[i] = A.a.key[A.a.off[r] + i]; av[i] = A.a.val[A.a.off[r] + i]; }
-        for (uint32_t i = 0; i < nb; ++i) { bk[i] = A.b.key[A.b.off[r] + i]; bv[i] = A.b.val[A.b.off[r] + i]; }
-        if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = -2;  // already linear
-        for (uint32_t q = 0; q < nr && A.turn[r] == -1; ++q) {
-          if (q > 0 && rk_[q] == rk_[q - 1]) continue;
-          for (int part = 0; part < 2; ++part) {
-            uint32_t *pk_ = part ? bk : ak;
-            Fe *pv_ = part ? bv : av;
-            uint32_t &pn = part ? nb : na;
-            uint32_t pcap = part ? capb : capa;
-            // find the signal with this rank in the part
-            uint32_t fi = RS_NONE;
-            for (uint32_t i = 0; i < pn; ++i)
-              if (A.rank_of[pk_[i]] == (int32_t)rk_[q]) { fi = i; break; }
-            if (fi == RS_NONE) continue;
-            int32_t s = A.sub_of[pk_[fi]];
-            Fe val = pv_[fi];
-            const uint32_t *hk = A.pk + A.h_off[s];
-            const Fe *hv = A.pv + A.h_off[s];
-            uint32_t hl = A.h_len[s];
-            // merge (pn - 1 + hl <= pcap) via scratch tmp region after rk_
-            uint32_t *mk = A.tmpk + 2 * (oc - A.c_base) + capc;
-            Fe *mv = A.tmpv + 2 * (oc - A.c_base) + capc;
-            uint32_t i = 0, j = 0, w = 0;
-            while (i < pn || j < hl) {
-              if (i == fi) { ++i; continue; }
-              if (j >= hl || (i < pn && pk_[i] < hk[j])) { mk[w] = pk_[i]; mv[w] = pv_[i]; ++i; }
-              else if (i >= pn || hk[j] < pk_[i]) { mk[w] = hk[j]; mv[w] = fmul(F, val, hv[j]); ++j; }
-              else { mk[w] = pk_[i]; mv[w] = fadd(F, pv_[i], fmul(F, val, hv[j])); ++i; ++j; }
-              ++w;
-            }
-            w = d_drop_zeros(mk, mv, w);
-            (void)pcap;
-            for (uint32_t t = 0; t < w; ++t) { pk_[t] = mk[t]; pv_[t] = mv[t]; }
-            pn = w;
-          }
-          if (d_const_or_empty(ak, na) || d_const_or_empty(bk, nb)) A.turn[r] = (int32_t)rk_[q];
-        }
-      }
+      d_round_turn(A, r);
       // the replay used the A / B regions as scratch: final A and B again
       na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
       nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
@@ -3256,6 +3277,12 @@ __global__ void k_round_fill(RoundArgs A) {
              36ull * (na + nb + nc);
   }
   wave_atomic_add(A.bytes, bytes);
+}
+
+// The turn ranks of the rows k_frames_wave listed (their final content is already written).
+__global__ void k_round_turn(RoundArgs A) {
+  const uint64_t n = *A.n_rlist;
+  for (uint64_t i = gtid(); i < n; i += gstride()) d_round_turn(A, A.rlist[i]);
 }
 
 // ---------------------------------------------------------------- final assembly
