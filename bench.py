@@ -91,8 +91,8 @@ def shard_seed(seed: int, rank: int) -> int:
 KERNELS = (  # (name, stats fields: ms, bytes, launches)
     ("k_big_main_lds (head)", "head_main_ms", "head_main_bytes", "head_launches"),
     ("k_big_main<256> (tail)", "tail_main_ms", "tail_main_bytes", "tail_launches"),
-    ("k_nl_fill", "apply_kernel_ms", "apply_bytes", "apply_kernel_launches"),
-    ("k_round_fill", "round_fill_ms", "round_fill_bytes", "round_fill_launches"),
+    ("k_frames_wave<0> (non-linear)", "apply_kernel_ms", "apply_bytes", "apply_kernel_launches"),
+    ("k_frames_wave<1> (rounds)", "round_fill_ms", "round_fill_bytes", "round_fill_launches"),
 )
 
 

@@ -94,6 +94,13 @@ struct Arena {
   }
 };
 
+// grid of k_frames_wave: RS_FW_BLOCKS (diagnostic knob), else one 64-row chunk per wave up to 16384 blocks
+static uint64_t fw_blocks_env() {
+  static const uint64_t v = getenv("RS_FW_BLOCKS") ? strtoull(getenv("RS_FW_BLOCKS"), nullptr, 10) : 16384;
+  return v ? v : 16384;
+}
+#define fw_blocks(E) fw_blocks_env()
+
 // grid-stride kernels that end in per-wave atomics: a capped grid keeps the atomics few
 template <class K, class... Args>
 static void launch_capped(hipStream_t st, K kernel, uint64_t n, uint64_t max_blocks, Args... args) {
@@ -133,6 +140,7 @@ using namespace rs;
 struct rs_engine {
   uint64_t pool_want = 0;  // substitution pool size (entries) that fitted last time
   int device = 0;
+  uint32_t n_cu = 256;  // compute units (resident grids)
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // the largest clusters' elimination chain runs here, beside the rest
   hipEvent_t evx[11] = {};    // [0] join-in, [1..4] head chain, [5] after the lane kernel, [6..7] the
@@ -1960,7 +1968,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     a.xlist = w.big;
     a.n_xlist = w.n_big;
     HC(hipEventRecord(e0, st));
-    launch(st, k_frames_wave, n, w);
+    launch_capped(st, k_frames_wave<0>, n, fw_blocks(E), w);
     launch(st, k_nl_fill, n, a);  // a grid for every row: the list may be long, idle lanes leave at once
     HC(hipEventRecord(e1, st));
     if (g_prof_env) {
@@ -2312,7 +2320,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           rb.rlist = w.big; rb.n_rlist = w.n_big;
           rt.rlist = w.turn_list; rt.n_rlist = w.n_turn;
           HC(hipEventRecord(E->ev0, st));
-          launch(st, k_frames_wave, ra.n_ids, w);
+          launch_capped(st, k_frames_wave<1>, ra.n_ids, fw_blocks(E), w);
           launch(st, k_round_fill, ra.n_ids, rb);
           launch(st, k_round_turn, ra.n_ids, rt);
           HC(hipEventRecord(E->ev1, st));
@@ -2623,6 +2631,7 @@ int rs_engine_create(int device, rs_engine **eng) {
       uint32_t head_cus = 0;
       if (const char *hc = getenv("RS_HEAD_CUS")) head_cus = (uint32_t)std::min<unsigned long>(strtoul(hc, nullptr, 10), 64ul);
       const uint32_t n_cu = (uint32_t)prop.multiProcessorCount;
+      E->n_cu = n_cu;
       bool masked = false;
       if (head_cus && n_cu >= 4 * head_cus) {
         // mask bits go 32 to an XCD, and workgroups are dealt to the XCDs round-robin: the free CUs

@@ -36,6 +36,9 @@ constexpr uint32_t kFwG = 192;            // groups: 64 rows x 3 linear combinat
 constexpr uint32_t kFwPT = kFwT / 64;     // terms per lane
 constexpr uint32_t kFwPE = kFwE / 64;     // entries per lane
 constexpr uint32_t kFwWaves = 4;          // waves per workgroup (each with its own LDS slice)
+#ifndef FW_KB
+#define FW_KB 2                            // emit: sorted positions per lane whose loads go together
+#endif
 
 struct FrameWaveArgs {
   FrameArgs fr;             // frames 1-2 absent in rounds (eq_rep / ce_has null)
@@ -88,6 +91,12 @@ struct FwLds {
   uint64_t g_in[kFwG];      // the group's input / output offsets
   uint64_t g_out[kFwG];
   uint32_t g_k0[kFwG];      // the group's first emitted key
+  // rows waiting for the fix pass (A or B one constant term), gathered over the wave's batches
+  uint64_t fx_off[3][64];   // output offsets of A, B, C
+  uint32_t fx_row[64];
+  uint32_t fx_cc[64];       // the C region's expansion size: C' goes after it
+  uint32_t fx_len[3][64];   // written lengths of A, B, C
+  uint8_t fx_other[64];     // 1: C - s * B (A constant), 0: C - s * A
 };
 
 __device__ __forceinline__ uint32_t fw_scan(uint32_t x, uint32_t lane) {  // inclusive, over the wave
@@ -176,7 +185,7 @@ __device__ inline void fw_terms(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
     ent[k] = 0;
     jj[k] = 0;
     if (t < n_t) {
-      ent[k] = fw_find(L.e_t0, n_e, t);
+      ent[k] = L.perm[t];  // term -> entry, scattered by the entries' lanes (perm is free until fw_rank)
       jj[k] = t - L.e_t0[ent[k]];
     }
   }
@@ -247,7 +256,7 @@ __device__ inline void fw_emit(const FrameWaveArgs &A, FwLds &L, uint32_t lane, 
 #endif
 ) {
   const FieldP &F = A.fr.F;
-  constexpr uint32_t kB = 5;
+  constexpr uint32_t kB = FW_KB;
   static_assert(kFwPT % kB == 0, "emit blocks");
   uint32_t before = 0;  // non-zero heads in the blocks done
 #pragma unroll
@@ -286,12 +295,11 @@ __device__ inline void fw_emit(const FrameWaveArgs &A, FwLds &L, uint32_t lane, 
       for (uint32_t q = 1; q < runv; ++q) v = fadd(F, v, fw_term_value(A, L, L.perm[pv_ + q]));
       return !fe_is_zero(v);
     };
-    static_assert(kB == 5, "value() is applied to five slots");
-    nz[0] = __ballot(value(c[0], m[0], kd[0], run[0], pp[0]));
-    nz[1] = __ballot(value(c[1], m[1], kd[1], run[1], pp[1]));
-    nz[2] = __ballot(value(c[2], m[2], kd[2], run[2], pp[2]));
-    nz[3] = __ballot(value(c[3], m[3], kd[3], run[3], pp[3]));
-    nz[4] = __ballot(value(c[4], m[4], kd[4], run[4], pp[4]));
+    static_assert(kB <= 5, "value() is applied to at most five slots");
+#define FW_VALUE(i) \
+  if constexpr (kB > i) nz[i] = __ballot(value(c[i], m[i], kd[i], run[i], pp[i]));
+    FW_VALUE(0) FW_VALUE(1) FW_VALUE(2) FW_VALUE(3) FW_VALUE(4)
+#undef FW_VALUE
 #pragma unroll
     for (uint32_t k = 0; k < kB; ++k) {
       if (lane == 0) {
@@ -337,25 +345,96 @@ __device__ inline uint32_t fw_starts(FwLds &L, uint32_t lane, uint32_t n_e, cons
   for (uint32_t k = 0; k < kPer; ++k) sum += w[k];
   const uint32_t incl = fw_scan(sum, lane);
   uint32_t run = incl - sum;
+  const uint32_t n_t = __shfl(incl, 63);
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
     const uint32_t e = lane * kPer + k;
-    if (e < n_e) L.e_t0[e] = (uint16_t)run;
+    if (e < n_e) {
+      L.e_t0[e] = (uint16_t)run;
+      if (n_t <= kFwT)
+        for (uint32_t t = run; t < run + w[k]; ++t) L.perm[t] = (uint16_t)e;
+    }
     run += w[k];
   }
-  const uint32_t n_t = __shfl(incl, 63);
   if (lane == 63 && n_t <= kFwT) L.e_t0[n_e] = (uint16_t)n_t;
   wave_sync();
   for (uint32_t g = lane; g <= kFwG; g += 64) L.g_t0[g] = L.e_t0[L.g_e0[g]];
   return n_t;
 }
 
+// ---- fix pass: C' = C - s * other (fix_constraint with constant_linear_linear_reduction,
+// algebra.rs:1309-1344) for the n queued rows (lane = queued row), through the same stages: per row
+// one group of two sorted runs, the written C and the written other scaled by -s.  C' goes after the C
+// region's expansion part; A and B are cleared.
+__device__ inline void fw_fix(const FrameWaveArgs &A, FwLds &L, uint32_t lane, uint32_t n, unsigned long long &bytes
+#ifdef RS_FWCLK
+                              , unsigned long long *clk_acc, unsigned long long &clk_last
+#endif
+) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the queued rows were written by this wave
+  wave_sync();
+  const bool on = lane < n;
+  const uint32_t other = on ? L.fx_other[lane] : 0u;
+  const uint32_t lc = on ? L.fx_len[2][lane] : 0u, lo = on ? L.fx_len[other][lane] : 0u;
+  const uint32_t fe = on ? 2u : 0u, fincl = fw_scan(fe, lane), f0 = fincl - fe, nf = __shfl(fincl, 63);
+  const uint32_t tw = lc + lo, tincl = fw_scan(tw, lane), t0 = tincl - tw, nft = __shfl(tincl, 63);
+  {
+    const uint32_t g = 3 * lane;
+    L.g_e0[g] = L.g_e0[g + 1] = L.g_e0[g + 2] = (uint16_t)f0;
+    if (lane == 63) {
+      L.g_e0[kFwG] = (uint16_t)nf;
+      L.e_t0[nf] = (uint16_t)nft;
+    }
+    L.g_k0[g + 2] = RS_NONE;
+    if (on) {
+      L.g_out[g + 2] = L.fx_off[2][lane] + L.fx_cc[lane];
+      L.g_in[g + 2] = L.fx_off[1 - other][lane];  // s: the constant part's single entry
+      L.e_grp[f0] = L.e_grp[f0 + 1] = (uint8_t)(g + 2);
+      L.e_kind[f0] = (uint8_t)(3 | (2 << 4));
+      L.e_aux[f0] = L.fx_off[2][lane];
+      L.e_kind[f0 + 1] = (uint8_t)(4 | (other << 4));
+      L.e_aux[f0 + 1] = L.fx_off[other][lane];
+      L.e_t0[f0] = (uint16_t)t0;
+      L.e_t0[f0 + 1] = (uint16_t)(t0 + lc);
+      for (uint32_t t = t0; t < t0 + lc; ++t) L.perm[t] = (uint16_t)f0;
+      for (uint32_t t = t0 + lc; t < t0 + lc + lo; ++t) L.perm[t] = (uint16_t)(f0 + 1);
+    }
+  }
+  wave_sync();
+  for (uint32_t g = lane; g <= kFwG; g += 64) L.g_t0[g] = L.e_t0[L.g_e0[g]];
+  fw_terms(A, L, lane, nf, nft);
+  wave_sync();
+  fw_rank(L, lane, nft);
+  wave_sync();
+  FW_EMIT(nft);
+  wave_sync();
+  if (on) {
+    const uint32_t r = L.fx_row[lane], len = fw_glen(L, 3 * lane + 2);
+    A.out[0].len[r] = 0;
+    A.out[1].len[r] = 0;
+    A.out[2].off[r] = L.fx_off[2][lane] + L.fx_cc[lane];
+    A.out[2].len[r] = len;
+    bytes += 36ull * (L.fx_len[0][lane] + L.fx_len[1][lane] + lc + lo + len);
+    if (A.round) {  // fix_constraint cleared A and B: the row turns linear this round
+      const unsigned pos = atomicAdd(A.n_turn, 1u);
+      A.turn_list[pos] = r;
+    }
+  }
+  wave_sync();
+}
+
+#ifdef RS_FWCLK
+#define FW_CLK_ARGS , clk_acc, clk_last
+#else
+#define FW_CLK_ARGS
+#endif
+
 // One batch: rows [s, e) of the wave's 64 (lane = row in the row stages); ioff / ooff: the row's
 // input / output offsets of A, B, C; cc: the size of its C region's expansion part (fix pass output
 // goes after it).
 __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane, bool inb, uint64_t r, const uint32_t ln[3],
                                 const uint64_t ioff[3], const uint64_t ooff[3], uint32_t cc, uint64_t x_of_row,
-                                unsigned long long &bytes
+                                uint32_t &fx_n, uint32_t &fx_terms, unsigned long long &bytes
 #ifdef RS_FWCLK
                                 , unsigned long long *clk_acc
 #endif
@@ -377,6 +456,7 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
     L.g_e0[g + 2] = (uint16_t)(ex + n0 + n1);
     if (lane == 63) L.g_e0[kFwG] = (uint16_t)n_e;
     L.g_k0[g] = L.g_k0[g + 1] = L.g_k0[g + 2] = RS_NONE;
+    for (uint32_t q = 0; q < tot; ++q) L.e_grp[ex + q] = (uint8_t)(g + (q >= n0) + (q >= n0 + n1));
     if (inb) {
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -397,8 +477,7 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
       const uint32_t e = lane * kFwPE + k;
       key[k] = 0;
       if (e < n_e) {
-        const uint32_t g = fw_find(L.g_e0, kFwG, e);
-        L.e_grp[e] = (uint8_t)g;
+        const uint32_t g = L.e_grp[e];
         key[k] = fw_ikey(A, fw_part(g))[L.g_in[g] + (e - L.g_e0[g])];
       }
     }
@@ -477,63 +556,38 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
       }
     }
   }
-  // ---- fix pass: C' = C - s * other (constant_linear_linear_reduction, algebra.rs:1326-1344) of the
-  // rows with a constant A or B, through the same stages: per row one group of two sorted runs, the
-  // written C and the written other scaled by -s; C' goes after the C region's expansion part
-  if (__ballot(other >= 0)) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows are read back below
-    const uint32_t fe = other >= 0 ? 2u : 0u, fincl = fw_scan(fe, lane), f0 = fincl - fe, nf = __shfl(fincl, 63);
-    {
-      const uint32_t g = 3 * lane;
-      L.g_e0[g] = L.g_e0[g + 1] = L.g_e0[g + 2] = (uint16_t)f0;
-      if (lane == 63) L.g_e0[kFwG] = (uint16_t)nf;
-      L.g_k0[g + 2] = RS_NONE;
-      if (other >= 0) {
-        L.g_out[g + 2] = ooff[2] + cc;
-        L.g_in[g + 2] = ooff[1 - other];  // s: the constant part's single entry
-        L.e_grp[f0] = L.e_grp[f0 + 1] = (uint8_t)(g + 2);
-        L.e_kind[f0] = (uint8_t)(3 | (2 << 4));
-        L.e_aux[f0] = ooff[2];
-        L.e_kind[f0 + 1] = (uint8_t)(4 | ((uint32_t)other << 4));
-        L.e_aux[f0 + 1] = ooff[other];
+  // ---- rows with a constant A or B wait for the fix pass (fw_fix), which runs once enough gathered
+  const uint64_t fm = __ballot(other >= 0);
+  if (fm) {
+    const uint32_t nfix = (uint32_t)__popcll(fm);
+    const uint32_t tw = other >= 0 ? len[2] + len[other] : 0u, tsum = __shfl(fw_scan(tw, lane), 63);
+    if (fx_n + nfix > 64 || fx_terms + tsum > kFwT) {
+      fw_fix(A, L, lane, fx_n, bytes FW_CLK_ARGS);
+      fx_n = 0;
+      fx_terms = 0;
+    }
+    if (other >= 0) {
+      const uint32_t q = fx_n + (uint32_t)__popcll(fm & fw_below(lane));
+      L.fx_row[q] = (uint32_t)r;
+      L.fx_cc[q] = cc;
+      L.fx_other[q] = (uint8_t)other;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        L.fx_off[p][q] = ooff[p];
+        L.fx_len[p][q] = len[p];
       }
     }
-    wave_sync();
-    // weights: entry f0 (lane's first) = |C|, f0 + 1 = |other|; fw_starts wants them by entry
-    // position lane * 2 + k, which is f0 + k only for the fix rows -- so scan by row instead
-    const uint32_t tw = other >= 0 ? len[2] + len[other] : 0u, tincl = fw_scan(tw, lane), t0 = tincl - tw;
-    const uint32_t nft = __shfl(tincl, 63);
-    if (other >= 0) {
-      L.e_t0[f0] = (uint16_t)t0;
-      L.e_t0[f0 + 1] = (uint16_t)(t0 + len[2]);
-    }
-    if (lane == 63) L.e_t0[nf] = (uint16_t)nft;
-    wave_sync();
-    for (uint32_t g = lane; g <= kFwG; g += 64) L.g_t0[g] = L.e_t0[L.g_e0[g]];
-    fw_terms(A, L, lane, nf, nft);
-    wave_sync();
-    fw_rank(L, lane, nft);
-    wave_sync();
-    FW_EMIT(nft);
-    wave_sync();
-    if (other >= 0) {
-      const uint32_t lc = fw_glen(L, 3 * lane + 2);
-      A.out[0].len[r] = 0;
-      A.out[1].len[r] = 0;
-      A.out[2].off[r] = ooff[2] + cc;
-      A.out[2].len[r] = lc;
-      bytes += 36ull * (len[2] + len[other] + lc);
-      if (A.round) {  // fix_constraint cleared A and B: the row turns linear this round
-        const unsigned pos = atomicAdd(A.n_turn, 1u);
-        A.turn_list[pos] = (uint32_t)r;
-      }
-    }
+    fx_n += nfix;
+    fx_terms += tsum;
   }
   (void)x_of_row;
   wave_sync();
   FW_CLK(6);
 }
 
+// kRound: 0 = the non-linear rows of round 1, 1 = the storage rows of rounds >= 2 (separate symbols so
+// profiles tell the two apart)
+template <int kRound>
 __global__ __launch_bounds__(256, 2) void k_frames_wave(FrameWaveArgs A) {
   __shared__ FwLds lds[kFwWaves];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -543,6 +597,7 @@ __global__ __launch_bounds__(256, 2) void k_frames_wave(FrameWaveArgs A) {
   unsigned long long clk_last = clock64(), clk_k0 = clk_last, clk_acc[20] = {};
 #endif
   const uint64_t nw = (uint64_t)gridDim.x * kFwWaves;
+  uint32_t fx_n = 0, fx_terms = 0;  // the fix-pass queue (uniform)
   for (uint64_t base = ((uint64_t)blockIdx.x * kFwWaves + wv) * 64; base < A.n; base += nw * 64) {
     const uint64_t x = base + lane;
     bool act = x < A.n;
@@ -588,14 +643,22 @@ __global__ __launch_bounds__(256, 2) void k_frames_wave(FrameWaveArgs A) {
       const uint32_t e = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
       const bool inb = act && lane >= s && lane < e;
 #ifdef RS_FWCLK
-      if (__ballot(inb)) fw_batch(A, L, lane, inb, r, ln, ioff, ooff, cc, x, bytes, clk_acc);
+      if (__ballot(inb)) fw_batch(A, L, lane, inb, r, ln, ioff, ooff, cc, x, fx_n, fx_terms, bytes, clk_acc);
       clk_last = clock64();
       clk_acc[8] += 1;
 #else
-      if (__ballot(inb)) fw_batch(A, L, lane, inb, r, ln, ioff, ooff, cc, x, bytes);
+      if (__ballot(inb)) fw_batch(A, L, lane, inb, r, ln, ioff, ooff, cc, x, fx_n, fx_terms, bytes);
 #endif
       s = e;
     }
+  }
+  if (fx_n) {
+#ifdef RS_FWCLK
+    unsigned long long clk_last2 = clock64();
+    fw_fix(A, L, lane, fx_n, bytes, clk_acc, clk_last2);
+#else
+    fw_fix(A, L, lane, fx_n, bytes);
+#endif
   }
 #ifdef RS_FWCLK
   clk_acc[9] = clock64() - clk_k0;

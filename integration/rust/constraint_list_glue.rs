@@ -61,13 +61,13 @@ impl Csr {
 }
 
 fn prime_id(field: &BigInt) -> (u32, [u64; 4]) {
-    // program_structure/src/utils/constants.rs:3-13 in ffi enum order; anything else is passed raw
+    // every --prime of program_structure/src/utils/constants.rs:3-13 is passed as its value
     let (_, d) = field.to_u64_digits();
     let mut p = [0u64; 4];
     for (i, x) in d.iter().take(4).enumerate() {
         p[i] = *x;
     }
-    (255, p) // RS_PRIME_CUSTOM: the library recognises the named primes from the value
+    (255, p) // RS_PRIME_CUSTOM: the library derives its field constants from the value
 }
 
 fn non_linear_rows(iter: EncodingIterator, a: &mut Csr, b: &mut Csr, c: &mut Csr) {

@@ -18,8 +18,8 @@ import sys
 GROUPS = {
     "k_big_main_lds (head)": "k_big_main_lds",
     "k_big_main<256> (tail)": "k_big_main<256u>",
-    "k_nl_fill": "rs::k_nl_fill(",
-    "k_round_fill": "rs::k_round_fill(",
+    "k_frames_wave<0> (non-linear)": "k_frames_wave<0>",
+    "k_frames_wave<1> (rounds)": "k_frames_wave<1>",
 }
 
 
