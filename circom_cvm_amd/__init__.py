@@ -6,7 +6,8 @@ Simplifier -> ConstraintList interface (constraint_list/src/lib.rs:110-202) used
 the benchmark."""
 from .abi import (Engine, Group, Input, Output, PinnedInput, RsError, RsFlags, RsInput, RsOutput, RsStats, check,
                   comm_unique_id, lib, make_flags, simplify_multi)
+from .dag import Dag
 from .simplifier import ConstraintList, Simplifier
 
 __all__ = ["Engine", "Group", "PinnedInput", "comm_unique_id", "simplify_multi", "Input", "Output", "RsError", "RsFlags", "RsInput", "RsOutput", "RsStats",
-           "check", "lib", "make_flags", "Simplifier", "ConstraintList"]
+           "check", "lib", "make_flags", "Simplifier", "ConstraintList", "Dag"]

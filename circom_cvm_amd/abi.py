@@ -69,6 +69,19 @@ class RsStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class RsDag(C.Structure):
+    """rs_dag: the component DAG rs_flatten_dag expands."""
+    _fields_ = [("prime_id", C.c_uint32), ("prime", C.c_uint64 * 4),
+                ("n_pub_out", C.c_uint64), ("n_pub_in", C.c_uint64), ("n_priv_in", C.c_uint64),
+                ("n_forbidden", C.c_uint64), ("forbidden", C.POINTER(C.c_uint32)),
+                ("n_nodes", C.c_uint32), ("main_node", C.c_uint32),
+                ("cons_off", C.POINTER(C.c_uint64)), ("a", RsLc), ("b", RsLc), ("c", RsLc),
+                ("local_off", C.POINTER(C.c_uint64)), ("locals", C.POINTER(C.c_uint32)),
+                ("custom_gate", C.POINTER(C.c_uint8)),
+                ("edge_off", C.POINTER(C.c_uint64)), ("edge_to", C.POINTER(C.c_uint32)),
+                ("edge_in", C.POINTER(C.c_uint64))]
+
+
 # (name, restype, argtypes) of every symbol include/rs_simplify.h declares
 SYMBOLS = [
     ("rs_last_error", C.c_char_p, []),
@@ -101,6 +114,7 @@ SYMBOLS = [
     ("rs_write_constraints_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),
     ("rs_write_substitution_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),
     ("rs_synth", C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(RsInput))]),
+    ("rs_flatten_dag", C.c_int, [C.c_int, C.POINTER(RsDag), C.POINTER(C.POINTER(RsInput))]),
 ]
 
 _LIB = None

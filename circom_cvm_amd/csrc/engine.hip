@@ -393,6 +393,7 @@ static U3 excl_scan_u3(rs_engine *E, const U3 *in, U3 *out, uint64_t n, const ch
   HC(hipStreamSynchronize(E->st));
   return U3Plus()(li, lo);
 }
+#include "flatten.hpp"
 __global__ void k_pack3(const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n, U3 *out) {
   for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = U3{a[i], b[i], c[i]};
 }
@@ -3160,6 +3161,27 @@ int rs_simplify_multi(const rs_input *in, const rs_flags *fl, int n_dev, const i
       if (rcs[r]) { rc = rcs[r]; set_error("rank " + std::to_string(r) + ": " + errs[r]); }
   }
   for (auto *E : eng) rs_engine_destroy(E);
+  return rc;
+}
+
+int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in) {
+  if (!dag || !in) { set_error("rs_flatten_dag: null argument"); return RS_E_INVALID; }
+  *in = nullptr;
+  rs_engine *E = nullptr;
+  int rc = rs_engine_create(device, &E);
+  if (rc) return rc;
+  try {
+    HC(hipSetDevice(E->device));
+    *in = flatten_dag(E, dag);
+    rc = RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    rc = e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    rc = RS_E_INTERNAL;
+  }
+  rs_engine_destroy(E);
   return rc;
 }
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 5
+#define RS_ABI_VERSION 6
 
 enum rs_status {
   RS_OK = 0,
@@ -276,6 +276,37 @@ int rs_write_substitution_json(const char *path, const rs_output *out);
  * (configs[3] ECDSA stand-in: deep composition, 8 rounds), 3 = Poseidon(16) Merkle (configs[2]),
  * 4 = sha256-like bit gadgets (configs[0]). */
 int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id, rs_input **in);
+
+/* ---- the DAG -> constraint-list flattening that produces rs_input.
+ * Replaces dag::map_to_constraint_list::map's walk (dag/src/map_to_constraint_list.rs:12-44 map_tree,
+ * :111-150 map) and the non-linear rows of the EncodingIterator DFS (constraint_list/src/lib.rs:65-108,
+ * state_utils.rs:14-35): every component instance in DFS order from main (offset 0), its local
+ * signals appended to the witness list, its constraints with the instance offset applied (key 0 stays
+ * the constant) and classified like map_tree -- constant equality, equality, linear (empty
+ * constraints only in main; Tree::go_to_subtree drops them), else non-linear.  Custom-gate
+ * instances' signals join main's forbidden_if_main.  Instance expansion and the constraint copy run
+ * on the device (prefix sums over the instance tree); the per-template classification is a host
+ * pass over the templates.  The result is an ordinary rs_input (freed with rs_input_free). */
+typedef struct rs_dag {
+  uint32_t prime_id;           /* enum rs_prime                                                 */
+  uint64_t prime[4];           /* only read when prime_id == RS_PRIME_CUSTOM                     */
+  uint64_t n_pub_out, n_pub_in, n_priv_in;
+  uint64_t n_forbidden;        /* main's forbidden_if_main (main's offset is 0: global ids)      */
+  const uint32_t *forbidden;
+  uint32_t n_nodes;            /* DAG nodes (templates with their parameters)                   */
+  uint32_t main_node;
+  const uint64_t *cons_off;    /* [n_nodes + 1]: node -> its constraints, rows of a / b / c       */
+  rs_lc a, b, c;               /* every node's constraints, node-local ids (0 = the constant)     */
+  const uint64_t *local_off;   /* [n_nodes + 1]: node -> its local signals                        */
+  const uint32_t *locals;      /* node-local ids of the node's own signals, ascending             */
+  const uint8_t *custom_gate;  /* [n_nodes]                                                       */
+  const uint64_t *edge_off;    /* [n_nodes + 1]: node -> its edges, in adjacency order            */
+  const uint32_t *edge_to;     /* child node                                                      */
+  const uint64_t *edge_in;     /* the edge's in_number: the child's signal offset in the parent   */
+} rs_dag;
+/* device: the GPU to run on.  Rejects (RS_E_INVALID) a cyclic graph, out-of-range ids and a graph
+ * whose instances overflow 32-bit signal ids. */
+int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in);
 
 #ifdef __cplusplus
 }

@@ -4,7 +4,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const RS_ABI_VERSION: c_int = 5;
+pub const RS_ABI_VERSION: c_int = 6;
 pub const RS_COMM_ID_BYTES: usize = 128;
 
 pub const RS_OK: c_int = 0;
@@ -65,6 +65,30 @@ pub struct rs_output {
     pub n_log: u64,
     pub log_from: *mut u32,
     pub log_to: rs_lc,
+}
+
+/// the component DAG rs_flatten_dag expands (dag/src/lib.rs Node / Edge).
+#[repr(C)]
+pub struct rs_dag {
+    pub prime_id: u32,
+    pub prime: [u64; 4],
+    pub n_pub_out: u64,
+    pub n_pub_in: u64,
+    pub n_priv_in: u64,
+    pub n_forbidden: u64,
+    pub forbidden: *const u32,
+    pub n_nodes: u32,
+    pub main_node: u32,
+    pub cons_off: *const u64,
+    pub a: rs_lc,
+    pub b: rs_lc,
+    pub c: rs_lc,
+    pub local_off: *const u64,
+    pub locals: *const u32,
+    pub custom_gate: *const u8,
+    pub edge_off: *const u64,
+    pub edge_to: *const u32,
+    pub edge_in: *const u64,
 }
 
 #[repr(C)]
@@ -153,4 +177,5 @@ extern "C" {
     pub fn rs_write_constraints_json(path: *const c_char, out: *const rs_output) -> c_int;
     pub fn rs_write_substitution_json(path: *const c_char, out: *const rs_output) -> c_int;
     pub fn rs_synth(kind: u32, rows: u64, seed: u64, prime_id: u32, inp: *mut *mut rs_input) -> c_int;
+    pub fn rs_flatten_dag(device: c_int, dag: *const rs_dag, inp: *mut *mut rs_input) -> c_int;
 }

@@ -1067,6 +1067,62 @@ def read_r1cs_bytes(data: bytes) -> Tuple[System, dict]:
     return System(p, n_labels, n_out, n_pub, n_prv, forb, rows, gates), hdr
 
 
+# ---------------------------------------------------------------- DAG -> constraint lists (8(f) rank 1)
+@dataclass
+class DagNode:
+    """A DAG node as the flattening reads it (dag/src/lib.rs:141-176 Node): its constraints over
+    node-local ids (0 = the constant), its own signals (is_local_signal), the custom-gate flag, and
+    its edges in adjacency order as (goes_to, in_number) (dag/src/lib.rs:87-100 Edge)."""
+    constraints: List[Con]
+    locals: List[int]
+    custom_gate: bool = False
+    edges: List[Tuple[int, int]] = dc_field(default_factory=list)
+
+
+def _offset_map(m: Map, off: int) -> Map:
+    """apply_raw_offset (algebra.rs:1266-1277): every key but the constant moves by the offset."""
+    return {(k if k == CONST else k + off): v for k, v in m.items()}
+
+
+def flatten_dag(p: int, nodes: List[DagNode], main: int, n_pub_out: int, n_pub_in: int, n_priv_in: int,
+                forbidden_main) -> Tuple[System, dict]:
+    """dag/src/map_to_constraint_list.rs:111-150 (map) over the tree walk of map_tree (:12-44) with
+    Tree::new / Tree::go_to_subtree (dag/src/lib.rs:35-85: main at offset 0 keeps every constraint, a
+    subtree drops the empty ones and applies its offset), plus the non-linear rows in the
+    EncodingIterator's DFS (constraint_list/src/lib.rs:65-108, state_utils.rs:14-35 over
+    map_node_to_encoding's non_linear, map_to_constraint_list.rs:71-104).  Returns the System the
+    Simplifier is built from (rows in DFS order) and the blocks as map() fills them."""
+    ce, eq, lin, nl = [], [], [], []
+    witness = [0]
+    forbidden = set(forbidden_main)
+    rows = []
+    stack = [(main, 0, True)]
+    while stack:  # pre-order, children in adjacency order
+        nid, off, root = stack.pop()
+        node = nodes[nid]
+        for s in sorted(node.locals):
+            witness.append(s + off)
+            if node.custom_gate:
+                forbidden.add(s + off)
+        for c in node.constraints:
+            if not root and is_empty(c):
+                continue
+            c = Con(_offset_map(c.a, off), _offset_map(c.b, off), _offset_map(c.c, off))
+            rows.append(c)
+            if is_constant_equality(c):
+                ce.append(c)
+            elif is_equality(c, p):
+                eq.append(c)
+            elif is_linear(c):
+                lin.append(c)
+            else:
+                nl.append(c)
+        for child, inn in reversed(node.edges):
+            stack.append((child, off + inn, False))
+    sys_ = System(p, len(witness), n_pub_out, n_pub_in, n_priv_in, forbidden, rows)
+    return sys_, dict(cons_eq=ce, eq=eq, linear=lin, non_linear=nl, witness=witness)
+
+
 def to_json_constraints(constraints: List[Con], sm: Dict[int, int]) -> list:
     """json_porting.rs:8-48 (numeric key order, decimal strings)."""
     out = []

@@ -16,7 +16,7 @@ HDR = os.path.join(ROOT, "include", "rs_simplify.h")
 RS = os.path.join(ROOT, "integration", "rust", "src", "lib.rs")
 R = rsio.R
 
-C2RUST = {"uint32_t": "u32", "uint64_t": "u64", "int32_t": "i32", "double": "f64", "rs_lc": "rs_lc"}
+C2RUST = {"uint32_t": "u32", "uint64_t": "u64", "int32_t": "i32", "uint8_t": "u8", "double": "f64", "rs_lc": "rs_lc"}
 
 
 def _strip_c_comments(s):
@@ -32,6 +32,9 @@ def c_structs():
             decl = " ".join(decl.split())
             if not decl:
                 continue
+            const = decl.startswith("const ")
+            if const:
+                decl = decl[len("const "):]
             m = re.match(r"(\w+)\s*(\*?)\s*(.+)", decl)
             ty, star, names = m.group(1), m.group(2), m.group(3)
             for nm in names.split(","):
@@ -43,7 +46,7 @@ def c_structs():
                 if arr:
                     nm, rt = arr.group(1), f"[{rt}; {arr.group(2)}]"
                 elif ptr:
-                    rt = f"*mut {rt}"
+                    rt = f"*const {rt}" if const else f"*mut {rt}"
                 fields.append((nm, rt))
         out[name] = fields
     return out
@@ -79,7 +82,7 @@ def test_rust_bindings_cover_every_function():
 
 def test_rust_structs_match_header_layout():
     cs, rs = c_structs(), rust_structs()
-    for name in ("rs_lc", "rs_input", "rs_flags", "rs_output", "rs_stats"):
+    for name in ("rs_lc", "rs_input", "rs_flags", "rs_output", "rs_stats", "rs_dag"):
         assert cs[name] == rs[name], (name, [x for x in zip(cs[name], rs[name]) if x[0] != x[1]][:3])
 
 
