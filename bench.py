@@ -108,6 +108,85 @@ def pmc_traffic():
     return d.get("bytes_per_launch", {}), os.path.relpath(files[-1], ROOT)
 
 
+class _Con:  # the .a / .b / .c shape circom_cvm_amd.Dag reads
+    __slots__ = ("a", "b", "c")
+
+    def __init__(self, a, b, c):
+        self.a, self.b, self.c = a, b, c
+
+
+class _Node:  # DagNode's shape: constraints, locals, custom_gate, edges
+    __slots__ = ("constraints", "locals", "custom_gate", "edges")
+
+    def __init__(self, constraints, locals_, edges=()):
+        self.constraints, self.locals, self.custom_gate, self.edges = constraints, locals_, False, list(edges)
+
+
+def flatten_bench(seed: int, prime: str, mids: int = 12000, leaves: int = 20, reps: int = 3):
+    """SURVEY 8(f) rank 1 measured: rs_flatten_dag on a 3-level synthetic component DAG (main -> `mids`
+    mid templates -> `leaves` leaf templates each; ~9.8 M instance constraints, 252 k instances) --
+    the DAG a circuit of the metric's size hands to map().  Checked by a size-independent property:
+    every block's row count equals the templates' class counts times their instance counts."""
+    import random
+
+    import circom_cvm_amd as M
+    p = _prime_value(prime)
+    rng = random.Random(seed)
+
+    def coef():
+        return rng.randrange(1, p)
+    L_LEAF, L_MID = 30, 10
+    lc = []
+    for _ in range(4):  # constant equalities
+        lc.append(_Con({}, {}, {rng.randint(1, L_LEAF): 1, 0: coef()}))
+    for _ in range(10):  # equalities
+        x, y = rng.sample(range(1, L_LEAF + 1), 2)
+        c = coef()
+        lc.append(_Con({}, {}, {x: c, y: p - c}))
+    for _ in range(14):  # linear
+        lc.append(_Con({}, {}, {k: coef() for k in rng.sample(range(1, L_LEAF + 1), 4)}))
+    for _ in range(12):  # quadratic
+        x, y, z = rng.sample(range(1, L_LEAF + 1), 3)
+        lc.append(_Con({x: coef()}, {y: coef()}, {z: 1}))
+    leaf = _Node(lc, list(range(1, L_LEAF + 1)))
+    s_mid = L_MID + leaves * L_LEAF
+    mc = []
+    for k in range(leaves):
+        c = coef()
+        mc.append(_Con({}, {}, {1 + k % L_MID: c, L_MID + L_LEAF * k + 1: p - c}))
+    mid = _Node(mc, list(range(1, L_MID + 1)), [(0, L_MID + L_LEAF * k) for k in range(leaves)])
+    main = _Node([_Con({}, {}, {1: 1, 2: 1, 3: 1, 4: 1}), _Con({}, {}, {1: 2, 2: 3, 3: 1, 5: 1})], [1, 2, 3],
+                 [(1, 3 + s_mid * j) for j in range(mids)])
+    dag = M.Dag(p, [leaf, mid, main], 2, 1, 1, 1, {0, 1, 2}, prime)
+    n_leaf = mids * leaves
+    want = {"cons_eq": 4 * n_leaf, "eq": 10 * n_leaf + leaves * mids, "linear": 14 * n_leaf + 2,
+            "nl": 12 * n_leaf}
+    times, ok = [], True
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        inp = dag.flatten(0)
+        times.append(time.perf_counter() - t0)
+        c = inp.c
+        got = {"cons_eq": c.cons_eq.n_rows, "eq": c.eq.n_rows, "linear": c.linear.n_rows, "nl": c.nl_a.n_rows}
+        ok &= got == want and c.max_signal == 1 + 3 + mids * (L_MID + leaves * L_LEAF)
+        inp.free()
+    n = sum(want.values())
+    best = min(times)
+    return {"ms": round(best * 1e3, 2), "constraints": n, "instances": 1 + mids * (1 + leaves),
+            "value": round(n / best, 1), "unit": "constraints/s", "counts_ok": bool(ok),
+            "what": "rs_flatten_dag host DAG -> host rs_input (templates up, every instance's rows classified "
+                    "and offset on the device, blocks back over PCIe), best of %d" % reps}
+
+
+def _prime_value(name: str) -> int:
+    """The field's modulus as the library knows it (a 1-row synthetic input carries it)."""
+    import circom_cvm_amd as M
+    inp = M.Input.synth(1, 1, 0, name)
+    v = sum(int(inp.c.prime[i]) << (64 * i) for i in range(4))
+    inp.free()
+    return v
+
+
 def timed_steps(eng, inp_c, fl, steps, barrier):
     """K host -> host steps between barriers; per-kernel device time/bytes summed over them."""
     acc = {k: [0.0, 0, 0] for k, *_ in KERNELS}
@@ -140,6 +219,7 @@ def main():
     ap.add_argument("--cpu-j1-rows", type=int, default=2_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the independent-shard extra run")
+    ap.add_argument("--no-flatten", action="store_true", help="skip the rs_flatten_dag extra measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,6 +268,8 @@ def main():
             write = {"ms": round(ms_w, 2), "bytes": os.path.getsize(path),
                      "what": "rs_engine_write_r1cs: the last step's result as a .r1cs file (constraint section "
                              "built on the device, streamed to a file in a temporary directory)"}
+    # the DAG flattening that produces such an input, timed on its own
+    flat = flatten_bench(args.seed, args.prime) if rank == 0 and not args.no_flatten else None
     # ---- extra: the same engine with the input resident in HBM (rs_engine_run only)
     eng.load(pin.c)
     barrier()
@@ -264,6 +346,8 @@ def main():
         }
         if write is not None:
             line["write_r1cs"] = write
+        if flat is not None:
+            line["flatten_dag"] = flat
         if weak is not None:
             line["weak_shards"] = weak
         if not args.no_cpu:
