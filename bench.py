@@ -220,6 +220,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the independent-shard extra run")
     ap.add_argument("--no-flatten", action="store_true", help="skip the rs_flatten_dag extra measurement")
+    ap.add_argument("--no-templated", action="store_true", help="skip the template-replicated extra circuit")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -270,6 +271,25 @@ def main():
                              "built on the device, streamed to a file in a temporary directory)"}
     # the DAG flattening that produces such an input, timed on its own
     flat = flatten_bench(args.seed, args.prime) if rank == 0 and not args.no_flatten else None
+    # SURVEY 8(d) config 5's template replication (64-row instances sharing coefficients, wired
+    # into chains): the same metric on that circuit, host -> host (parity: tests/test_gpu_configs.py)
+    tmpl = None
+    if rank == 0 and world == 1 and not args.no_templated:
+        tinp = M.Input.synth(5, args.rows, args.seed, args.prime)
+        tpin = M.PinnedInput(tinp.c)
+        for _ in range(2):
+            eng.simplify(tpin.c, fl)
+        k_t = min(args.steps, 20)
+        tdt, _, _, _, tst = timed_steps(eng, tpin.c, fl, k_t, lambda: None)
+        tmpl = {"value": round(tinp.rows() * k_t / tdt, 1), "unit": "constraints/s",
+                "ms_per_step": round(tdt * 1000.0 / k_t, 3), "steps": k_t, "constraints": tinp.rows(),
+                "max_cluster": int(tst.max_cluster), "rounds": int(tst.rounds),
+                "elim_ms": round(tst.elim_ms, 2),
+                "workload": f"synth_templated rows={args.rows} seed={args.seed} {args.prime} --O2: 16 templates "
+                            f"of 64 rows replicated with signal offsets, instances wired into log-normal chains "
+                            f"(SURVEY 8(d) config 5's replication), host -> host"}
+        tpin.free()
+        tinp.free()
     # ---- extra: the same engine with the input resident in HBM (rs_engine_run only)
     eng.load(pin.c)
     barrier()
@@ -348,6 +368,8 @@ def main():
             line["write_r1cs"] = write
         if flat is not None:
             line["flatten_dag"] = flat
+        if tmpl is not None:
+            line["templated"] = tmpl
         if weak is not None:
             line["weak_shards"] = weak
         if not args.no_cpu:

@@ -3,7 +3,8 @@
 // Replaces circom_algebra/src/modular_arithmetic.rs:9-91 (num-bigint-dig BigInt + double
 // remainder per op) with residues stored as 4 x 64-bit limbs in Montgomery form (R = 2^261): one
 // radix-2^29 Montgomery product per field multiplication, carry-propagating add/sub with a single
-// conditional correction.
+// conditional correction.  Primes below 2^64 (goldilocks) take a one-word path (two 64-bit
+// Montgomery reductions) in the same representation.
 // Results are canonical residues, identical to the reference's ((a % p) + p) % p.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -29,6 +30,9 @@ struct FieldP {
   Fe r2;        // R^2 mod p  (R = 2^261)
   Fe one;       // R mod p
   Fe pm2;       // p - 2 (Fermat exponent)
+  uint64_t np64;  // -p^-1 mod 2^64 (one-word primes)
+  uint64_t k133;  // 2^-133 mod p (one-word primes): folds the 2^64 word radix into R = 2^261
+  uint32_t w64;   // p < 2^64 (goldilocks): products take the one-word Montgomery path
 };
 
 __host__ __device__ __forceinline__ bool fe_is_zero(const Fe &a) {
@@ -96,12 +100,32 @@ __host__ __device__ __forceinline__ void to_limbs(const Fe &x, uint32_t *a) {
     a[i] = (uint32_t)v & kLimbMask;
   }
 }
+// One-word Montgomery reduction for p < 2^64 (goldilocks, constants.rs:7): a*b*2^-64 mod p from
+// the 128-bit product and one reduction word.  a, b < p, so hi(ab) < p and hi(mp) < p; lo(ab) +
+// lo(mp) = 0 mod 2^64 carries iff lo(ab) != 0; the sum < 2p may exceed 2^64 (128-bit compare).
+__host__ __device__ __forceinline__ uint64_t mont64(const FieldP &F, uint64_t a, uint64_t b) {
+  const u128 t = (u128)a * b;
+  const uint64_t lo = (uint64_t)t, m = lo * F.np64;
+  const u128 mp = (u128)m * F.p[0];
+  u128 u = (t >> 64) + (mp >> 64) + (lo != 0);
+  if (u >= F.p[0]) u -= F.p[0];
+  return (uint64_t)u;
+}
+// The same Montgomery product as fmul256 (a*b*2^-261 mod p, so the representation, r2 and one are
+// shared and kernels may mix the two paths) in two one-word reductions: mont64(mont64(a, b),
+// 2^-133) = a*b*2^-64*2^-133*2^-64.  Eight 32-bit multiply-add pairs instead of 162 limb products.
+__host__ __device__ __forceinline__ Fe fmul64(const FieldP &F, uint64_t a, uint64_t b) {
+  Fe o;
+  o.l[0] = mont64(F, mont64(F, a, b), F.k133);
+  o.l[1] = o.l[2] = o.l[3] = 0;
+  return o;
+}
 // Montgomery product a*b*2^-261 mod p, radix 2^29: the 81 limb products of each half go into
 // 64-bit column accumulators with independent multiply-adds (no carry chain inside a column; a
 // column holds at most 18 products < 2^58), then 9 reduction steps and one carry pass.  44 % lower
 // dependent latency than a 8 x 32-bit CIOS on gfx950 (tools/micro/fmul28.hip: 0.60 vs 1.09 us
 // per product for one wave), which is what the ordered elimination loop waits on.
-__host__ __device__ __forceinline__ Fe fmul(const FieldP &F, const Fe &A, const Fe &B) {
+__host__ __device__ __forceinline__ Fe fmul256(const FieldP &F, const Fe &A, const Fe &B) {
   uint32_t a[kLimbs], b[kLimbs];
   to_limbs(A, a);
   to_limbs(B, b);
@@ -147,9 +171,18 @@ __host__ __device__ __forceinline__ Fe fmul(const FieldP &F, const Fe &A, const 
   }
   return o;
 }
+// The field product every kernel uses: the one-word path for p < 2^64 (the prime is uniform over a
+// launch, so the branch never diverges a wave), else fmul256.  The tail's ordered loop calls fmul256
+// directly: the branch costs it 18 VGPRs and ~5 % of its time on the 256-bit primes, and a goldilocks
+// circuit gets the same residues either way.
+__host__ __device__ __forceinline__ Fe fmul(const FieldP &F, const Fe &A, const Fe &B) {
+  if (F.w64) return fmul64(F, A.l[0], B.l[0]);
+  return fmul256(F, A, B);
+}
 // Montgomery square: the product half is symmetric (45 limb products instead of 81: off-diagonal
 // ones doubled; a column still sums below 2^63), the reduction is fmul's.
 __host__ __device__ __forceinline__ Fe fsqr(const FieldP &F, const Fe &A) {
+  if (F.w64) return fmul64(F, A.l[0], A.l[0]);
   uint32_t a[kLimbs], a2[kLimbs];
   to_limbs(A, a);
 #pragma unroll
@@ -247,6 +280,13 @@ inline FieldP make_field(const uint64_t prime[4]) {
   uint32_t inv = 1;  // p^-1 mod 2^29 (Newton)
   for (int i = 0; i < 5; ++i) inv *= 2 - F.pl[0] * inv;
   F.np = (0u - inv) & kLimbMask;
+  F.w64 = prime[1] == 0 && prime[2] == 0 && prime[3] == 0;
+  uint64_t inv64 = 1;  // p^-1 mod 2^64 (Newton: each step doubles the correct bits)
+  for (int i = 0; i < 6; ++i) inv64 *= 2 - prime[0] * inv64;
+  F.np64 = 0 - inv64;
+  u128 h = 1;  // 2^-133 mod p by 133 halvings (p odd)
+  for (int i = 0; i < 133 && F.w64; ++i) h = (h & 1) ? (h + prime[0]) >> 1 : h >> 1;
+  F.k133 = (uint64_t)h;
   uint64_t x[4] = {1, 0, 0, 0};
   const int rb = kLimbBits * kLimbs;  // R = 2^rb
   for (int i = 0; i < 2 * rb; ++i) {

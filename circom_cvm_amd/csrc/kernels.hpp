@@ -1573,7 +1573,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           const uint32_t on = isw ? rl : (isr ? len : 0u);
           bool hit;
           const uint32_t lb = lds_lb64(ok, on, key, hit);
-          val = fmul(F, isw ? c2 : coef, val);
+          val = fmul256(F, isw ? c2 : coef, val);
           const unsigned long long tq1 = clk();
           if (isr) rv[j] = val;
           wave_sync();
@@ -1619,8 +1619,8 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           Fe wval = fe_zero(), rval = fe_zero();
           if (l < rl) { rkey = A.pk[roff + l]; rval = A.pv[roff + l]; }
           if (l < len) { wkey = wk[cur][l]; wval = wv[cur][l]; }
-          if (l < len) wval = fmul(F, c2, wval);   // one product per entry, both lists at once
-          if (l < rl) rval = fmul(F, coef, rval);
+          if (l < len) wval = fmul256(F, c2, wval);   // one product per entry, both lists at once
+          if (l < rl) rval = fmul256(F, coef, rval);
           if (l < rl) { rk[l] = rkey; rv[l] = rval; }
           __syncthreads();
           bool keep_w = false, keep_r = false;
@@ -1662,8 +1662,8 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
         __syncthreads();
         // one product per entry, all lanes at once: work entries c2*v, RHS entries coef*rv
         for (uint32_t q = tid; q < len + rl; q += nt) {
-          if (q < len) wv[cur][q] = fmul(F, c2, wv[cur][q]);
-          else rv[q - len] = fmul(F, coef, rv[q - len]);
+          if (q < len) wv[cur][q] = fmul256(F, c2, wv[cur][q]);
+          else rv[q - len] = fmul256(F, coef, rv[q - len]);
         }
         __syncthreads();
         for (uint32_t i = tid; i < len; i += nt) {  // work keys: -c2*v (+ coef*rv when the RHS has the key)

@@ -17,6 +17,8 @@
 //          4-limb big-integer products (see gen_chain).
 //  kind 3  poseidon (config 3 stand-in): Poseidon(16) (t = 17) 16-ary Merkle paths of depth 20.
 //  kind 4  sha (config 1 stand-in): sha256 compression gadgets (XOR3, Ch, Maj, BinSum, Num2Bits).
+//  kind 5  templated (config 5 as SURVEY 8(d) words it): 64-row template instances replicated with
+//          signal offsets, wired into chains of log-normal length (see gen_templated).
 //
 // Coefficients: 60% from {1, p-1, 2^k}, 40% uniform in [1, p) (splitmix64 stream).
 #include <algorithm>
@@ -656,13 +658,158 @@ static void gen_sha(Gen &g, uint64_t R, uint32_t n_pub) {
   }
 }
 
+// kind 5 (SURVEY 8(d) config 5 as written: "rows are replicated per template instance of 64 rows,
+// to mimic DAG replication"): 16 templates of 64 rows each (19 eq / 3 const-eq / 22 linear / 20
+// quadratic), generated once over local signal ids with fixed coefficients; every instance is a
+// template with its signals offset (dag/src/lib.rs:73-78 apply_offset), so instances of a template
+// share coefficients exactly as a compiled circuit's do.  Instances form wiring chains of
+// log-normal length (median 2 instances, up to ~9,000 = 2e5 linear rows): instance k's 4 inputs
+// are tied to instance k-1's 4 outputs by equalities (`c.in <== d.out`), so after eq renaming the
+// linear rows of a chain form one cluster.  Inside a template the linear rows define internal
+// signals from earlier ones (a DAG, 2-4 terms), the quadratic rows multiply defined signals (one in
+// 25 with a constant selector in A: those rows turn linear and feed round 2), the equalities
+// alias defined signals for the quadratic rows.
+static void gen_templated(Gen &g, uint64_t R, uint32_t n_pub) {
+  // templates, interface, locals per instance (1-4 inputs, 5-46 definitions, 47-61 aliases, 63-65
+  // selectors)
+  constexpr uint32_t kT = 16, kIn = 4, kOut = 4, kL = 66;
+  struct LRow {
+    uint8_t blk;  // 0 eq, 1 const-eq, 2 linear, 3 quadratic
+    std::vector<std::pair<uint32_t, std::array<uint64_t, 4>>> a, b, c;  // local ids (0 = constant)
+  };
+  std::vector<std::vector<LRow>> tpl(kT);
+  const uint64_t one[4] = {1, 0, 0, 0};
+  auto term = [&](uint32_t s) {
+    std::array<uint64_t, 4> c;
+    g.coef(c.data());
+    return std::make_pair(s, c);
+  };
+  for (uint32_t t = 0; t < kT; ++t) {
+    // locals: 1..4 inputs, then 22 linear-defined, 20 quadratic-defined, 3 selectors, 15 aliases
+    std::vector<uint32_t> defd = {1, 2, 3, 4};
+    uint32_t nx = kIn + 1;
+    std::vector<LRow> rows;
+    std::vector<uint32_t> sels;
+    for (int j = 0; j < 3; ++j) {  // selectors fixed to a constant
+      LRow r;
+      r.blk = 1;
+      const uint32_t s = kL - 1 - j;
+      sels.push_back(s);
+      std::array<uint64_t, 4> o;
+      memcpy(o.data(), one, 32);
+      r.c.push_back({s, o});
+      if (g.rng.uni() < 0.8) r.c.push_back(term(0));
+      rows.push_back(r);
+    }
+    auto pick = [&]() { return defd[defd.size() - 1 - g.rng.below(std::min<size_t>(defd.size(), 12))]; };
+    uint32_t last_lin = 0, n_lin = 0;
+    for (int j = 0; j < 22 + 20; ++j) {  // linear (even j and the last two) and quadratic (odd j)
+      LRow r;
+      const uint32_t x = nx++;
+      if ((j & 1) == 0 || j >= 40) {  // linear: x = previous linear definition + 0-2 others (+ c)
+        r.blk = 2;
+        r.c.push_back(term(x));
+        if (last_lin) r.c.push_back(term(last_lin));  // the backbone: inputs -> ... -> outputs
+        if (n_lin < kIn) r.c.push_back(term(1 + n_lin));
+        const int nt = (int)g.rng.below(3);
+        for (int u = 0; u < nt; ++u) r.c.push_back(term(pick()));
+        if (g.rng.uni() < 0.3) r.c.push_back(term(0));
+        last_lin = x;
+        ++n_lin;
+      } else {  // quadratic: x = (a) * (b) (+ c)
+        r.blk = 3;
+        if (g.rng.uni() < 0.04 * 2) {
+          std::array<uint64_t, 4> o;
+          memcpy(o.data(), one, 32);
+          r.a.push_back({sels[g.rng.below(sels.size())], o});
+        } else {
+          r.a.push_back(term(pick()));
+          if (g.rng.uni() < 0.3) r.a.push_back(term(0));
+        }
+        r.b.push_back(term(pick()));
+        if (g.rng.uni() < 0.4) r.b.push_back(term(pick()));
+        std::array<uint64_t, 4> o;
+        memcpy(o.data(), one, 32);
+        r.c.push_back({x, o});
+        if (g.rng.uni() < 0.3) r.c.push_back(term(pick()));
+      }
+      rows.push_back(r);
+      defd.push_back(x);
+    }
+    for (int j = 0; j < 15; ++j) {  // aliases of defined signals
+      LRow r;
+      r.blk = 0;
+      const uint32_t y = nx++;
+      const uint32_t s = defd[kIn + g.rng.below(defd.size() - kIn)];
+      std::array<uint64_t, 4> c, nc_;
+      g.coef(c.data());
+      g.neg(c.data(), nc_.data());
+      r.c.push_back({y, c});
+      r.c.push_back({s, nc_});
+      rows.push_back(r);
+      defd.push_back(y);
+    }
+    tpl[t] = std::move(rows);
+  }
+  // outputs of a template: linear-defined locals (definitions j = 40, 41, 38, 36)
+  const uint32_t out_local[kOut] = {kIn + 1 + 40, kIn + 1 + 41, kIn + 1 + 38, kIn + 1 + 36};
+  uint64_t made = 0;
+  uint32_t pub_used = 0;
+  Terms t, a, b, c;
+  while (made < R) {
+    double z = std::sqrt(-2.0 * std::log(std::max(g.rng.uni(), 1e-300))) * std::cos(6.283185307179586 * g.rng.uni());
+    uint64_t len = (uint64_t)std::llround(2.0 * std::exp(1.3 * z));
+    len = std::max<uint64_t>(1, std::min<uint64_t>(len, 9000));
+    uint32_t prev = 0;  // base of the previous instance of the chain (0: none)
+    for (uint64_t k = 0; k < len && made < R; ++k) {
+      const std::vector<LRow> &T = tpl[g.rng.below(kT)];
+      const uint32_t base = g.next_sig - 1;  // local l -> base + l
+      g.next_sig += kL - 1;
+      for (uint32_t q = 0; q < kIn; ++q) {  // wiring: in_q <== prev.out_q (or a public input)
+        uint32_t src = 0;
+        if (prev) src = prev + out_local[q];
+        else if (pub_used < n_pub && g.rng.uni() < 1.0 / 512) src = 2 + (pub_used++);
+        if (!src) continue;
+        t.clear();
+        uint64_t cc[4], nn[4];
+        g.coef(cc);
+        g.neg(cc, nn);
+        add_v(t, base + 1 + q, cc);
+        add_v(t, src, nn);
+        g.row(g.eq, t);
+        g.n_eq++;
+        ++made;
+      }
+      for (const LRow &r : T) {
+        auto off = [&](const Terms &src, Terms &dst) {
+          dst.clear();
+          for (auto &e : src) dst.push_back({e.first ? base + e.first : 0u, e.second});
+        };
+        off(r.c, c);
+        if (r.blk == 3) {
+          off(r.a, a);
+          off(r.b, b);
+          g.row(g.na, a);
+          g.row(g.nb, b);
+          g.row(g.nc, c);
+          g.n_q++;
+        } else {
+          g.linear_row(c);  // classified as map_tree would (eq / const-eq / linear)
+        }
+        ++made;
+      }
+      prev = base;
+    }
+  }
+}
+
 }  // namespace rs
 
 using namespace rs;
 
 extern "C" int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id,
                         rs_input **out) {
-  if (prime_id >= 8 || kind > 4) { set_error("rs_synth: bad kind/prime"); return RS_E_INVALID; }
+  if (prime_id >= 8 || kind > 5) { set_error("rs_synth: bad kind/prime"); return RS_E_INVALID; }
   Gen g;
   g.rng.s = seed;
   memcpy(g.p, kPrimes[prime_id], 32);
@@ -673,7 +820,8 @@ extern "C" int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t pr
   else if (kind == 1) gen_linear(g, rows, n_pub);
   else if (kind == 2) gen_chain(g, rows, n_pub);
   else if (kind == 3) gen_poseidon(g, rows, n_pub);
-  else gen_sha(g, rows, n_pub);
+  else if (kind == 4) gen_sha(g, rows, n_pub);
+  else gen_templated(g, rows, n_pub);
   rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
   in->prime_id = prime_id;
   memcpy(in->prime, g.p, 32);

@@ -59,6 +59,15 @@ def test_config4_bls12381_20M():
     run_and_check(0, 20_000_000, 42, "bls12381", "bls12381 20M")
 
 
+def test_config4_templated_10M():
+    """configs[4] with SURVEY 8(d) config 5's replication: 64-row template instances (16 templates,
+    coefficients shared by every instance) wired into log-normal chains; 2M and the full 10M."""
+    got, st = run_and_check(5, 2_000_000, 7, "bn128", "templated 2M")
+    assert st.max_cluster >= 350 and st.rounds >= 2
+    got, st = run_and_check(5, 10_000_000, 42, "bn128", "templated 10M")
+    assert st.max_cluster >= 5_000
+
+
 @pytest.mark.parametrize("prime", ["grumpkin", "pallas", "vesta", "bls12377", "goldilocks", "secq256r1"])
 def test_every_prime_1M(prime):
     run_and_check(0, 1_000_000, 9, prime, f"mixed 1M {prime}")
