@@ -334,16 +334,30 @@ __global__ __launch_bounds__(64) void k_cl_replay_wave(const uint64_t *cl_off, c
   }
 }
 
-// cluster-size classes for the elimination kernels: sorted by (size desc, index)
-__global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, uint64_t *skey, uint32_t *sidx,
+// cluster-size classes for the elimination kernels, sorted by (workgroup kernels first, size desc,
+// index).  The workgroup kernels take every cluster of kWaveMin rows or more, and also the smaller
+// ones holding kHeavyNnz entries or more: rounds >= 2 cluster rows that substitution made long (a
+// chain's composed right-hand sides), which one lane would merge serially for tens of ms.  Both
+// kernels run the same process_3 / process_4 rules, and results are collected by cluster index, so
+// the routing changes no output.
+constexpr uint32_t kHeavyNnz = 256;
+__global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, const uint32_t *srow, const uint32_t *len,
+                             uint64_t *skey, uint32_t *sidx,
                              unsigned long long *cnt /* [0] >= 1e6, [1] workgroup kernels, [2] LDS replay, [3] > LDS, [4] large LDS replay */) {
   unsigned long long k[5] = {0, 0, 0, 0, 0};
   for (uint64_t c = gtid(); c < n_cl; c += gstride()) {
-    uint64_t sz = cl_off[c + 1] - cl_off[c];
-    skey[c] = ((uint64_t)(0xffffffffu - (uint32_t)sz) << 32) | c;
+    const uint64_t b = cl_off[c], sz = cl_off[c + 1] - b;
+    bool wg = sz >= kWaveMin;
+    if (!wg) {
+      uint64_t nnz = 0;
+      for (uint64_t i = b; i < b + sz; ++i) nnz += len[srow[i]];
+      wg = nnz >= kHeavyNnz;
+    }
+    const uint64_t rank = wg ? (1ull << 31) + sz : sz;  // sz < 2^31
+    skey[c] = ((0xffffffffull - rank) << 32) | c;
     sidx[c] = (uint32_t)c;
     k[0] += sz >= 1000000;
-    k[1] += sz >= kWaveMin;
+    k[1] += wg;
     k[2] += sz > kClSmall && sz <= kClLds;
     k[3] += sz > kClLds;
     k[4] += sz > kClMid && sz <= kClLds;

@@ -750,6 +750,27 @@ static void fetch_pool_maps(rs_engine *E, const std::vector<uint64_t> &off, cons
   HC(hipStreamSynchronize(E->st));
 }
 
+// D2H keys of pool maps (no values)
+static void fetch_pool_keys(rs_engine *E, const std::vector<uint64_t> &off, const std::vector<uint32_t> &len,
+                            const uint32_t *pk, std::vector<uint32_t> &keys, std::vector<uint64_t> &optr) {
+  const uint64_t n = off.size();
+  optr.assign(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) optr[i + 1] = optr[i] + len[i];
+  const uint64_t tot = optr[n];
+  keys.resize(tot);
+  if (tot == 0) return;
+  uint64_t *d_off = E->A.get<uint64_t>("fp.off", n);
+  uint32_t *d_len = E->A.get<uint32_t>("fp.len", n);
+  uint64_t *d_optr = E->A.get<uint64_t>("fp.optr", n + 1);
+  uint32_t *d_k = E->A.get<uint32_t>("fp.k", tot);
+  h2d(E, d_off, off.data(), 8 * n);
+  h2d(E, d_len, len.data(), 4 * n);
+  h2d(E, d_optr, optr.data(), 8 * (n + 1));
+  launch(E->st, k_pool_keys, 64 * n, (const uint64_t *)d_off, (const uint32_t *)d_len, (const uint64_t *)d_optr, n, pk, d_k);
+  HC(hipMemcpyAsync(keys.data(), d_k, 4 * tot, hipMemcpyDeviceToHost, E->st));
+  HC(hipStreamSynchronize(E->st));
+}
+
 static bool is_zero4(const uint64_t *v) { return (v[0] | v[1] | v[2] | v[3]) == 0; }
 
 // fix_constraint for a host lconst row (always linear: only zero removal)
@@ -878,11 +899,11 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   launch(st, k_cl_stream, n_act, (const uint32_t *)srow, (const uint64_t *)poff, (const uint32_t *)prevrow,
          (const uint32_t *)gpos, (const uint32_t *)cid, (const uint64_t *)D.cl_off, (const uint64_t *)q_off, n_act,
          stream);
-  // size order: (size desc, index asc)
+  // sort order: (workgroup-kernel clusters first, size desc, index asc)
   uint64_t *sk = A.get<uint64_t>("cl.sk", n_cl), *sk2 = A.get<uint64_t>("cl.sk2", n_cl);
   uint32_t *si = A.get<uint32_t>("cl.si", n_cl), *sorted = A.get<uint32_t>("el.big", n_cl);
   unsigned long long *cnt = stat + 2;
-  launch_capped(st, k_cl_sizekey, n_cl, 1024, (const uint64_t *)D.cl_off, n_cl, sk, si, cnt);
+  launch_capped(st, k_cl_sizekey, n_cl, 1024, (const uint64_t *)D.cl_off, n_cl, (const uint32_t *)srow, (const uint32_t *)V.len, sk, si, cnt);
   sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
   unsigned long long hc[5];
   uint64_t first = 0;
@@ -931,8 +952,9 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
     if (!sharded && hc[3] + hc[4] <= head_limit()) D.join_pending = true;
     else HC(hipStreamWaitEvent(st, E->evx[7], 0));
   }
-  // elimination split: clusters of kWaveMin rows or more (a prefix of the size order) go to the
-  // workgroup kernels (process_3 or process_4 per cluster), the rest one lane each
+  // elimination split: clusters of kWaveMin rows or more and the heavy small ones (a prefix of the
+  // sort order, k_cl_sizekey) go to the workgroup kernels (process_3 or process_4 per cluster), the
+  // rest one lane each
   const uint64_t h = 0, nb = hc[1];
   D.big = sorted + h;
   D.n_big = nb;
@@ -946,7 +968,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   HC(hipMemcpyAsync(eo.cl_off.data(), D.cl_off, 8 * (n_cl + 1), hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
   E->stats.n_clusters += n_cl;
-  E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, 0xffffffffull - (first >> 32));
+  E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, (0xffffffffull - (first >> 32)) & 0x7fffffffull);
   return D;
 }
 
@@ -2160,7 +2182,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       HC(hipMemcpyAsync(ic0.len, tc_.len, 4 * n_st, hipMemcpyDeviceToDevice, st));
     }
     std::unordered_map<uint32_t, std::vector<uint32_t>> minit;  // queried signals only
-    std::unordered_map<uint32_t, std::vector<uint32_t>> mext;
     uint8_t *qflag = A.get<uint8_t>("m.qflag", S);
     HC(hipMemsetAsync(qflag, 0, S, st));
     auto query_initial = [&](const std::vector<uint32_t> &sigs) {
@@ -2193,6 +2214,52 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       }
       launch(st, k_unmark_list, q.size(), (const uint32_t *)d_q, (uint64_t)q.size(), qflag);
     };
+    // The appends of apply_substitution_to_map (:369-377) -- every key of a substitution's RHS gets
+    // the row list of its `from` -- kept lazily: per round that another round follows, its
+    // substitutions' `from` and RHS keys (a batch).  A signal's appended list is materialised only
+    // when a later round orders the rows it turned linear by their positions in that list
+    // (resolve_ext); most appended lists are never read, and building them all costs
+    // sum |RHS| x |rows| host appends per round.
+    struct MapBatch {
+      std::vector<uint32_t> from, keys;
+      std::vector<uint64_t> ptr;
+    };
+    std::vector<MapBatch> batches;
+    std::vector<uint8_t> hmark;  // membership marks over the signals, all zero between uses
+    // the appended lists of the signals X from batches [0, upto), in append order: batch, then
+    // substitution, then RHS position (a substitution's `from` is in no RHS of its own round, so a
+    // batch's appends never depend on each other; a visit list depends on earlier batches only)
+    std::function<std::unordered_map<uint32_t, std::vector<uint32_t>>(const std::vector<uint32_t> &, size_t)> resolve_ext =
+        [&](const std::vector<uint32_t> &X, size_t upto) {
+          std::unordered_map<uint32_t, std::vector<uint32_t>> res;
+          if (X.empty() || upto == 0) return res;
+          if (hmark.empty()) hmark.assign(S, 0);
+          for (size_t bi = 0; bi < upto; ++bi) {
+            const MapBatch &B = batches[bi];
+            std::vector<std::pair<uint32_t, uint32_t>> hits;  // (substitution, key)
+            for (uint32_t x : X) hmark[x] = 1;
+            for (uint64_t j = 0; j < B.from.size(); ++j)
+              for (uint64_t t = B.ptr[j]; t < B.ptr[j + 1]; ++t)
+                if (hmark[B.keys[t]]) hits.push_back({(uint32_t)j, B.keys[t]});
+            for (uint32_t x : X) hmark[x] = 0;
+            if (hits.empty()) continue;
+            std::vector<uint32_t> Fr;
+            for (auto &h : hits) Fr.push_back(B.from[h.first]);
+            std::sort(Fr.begin(), Fr.end());
+            Fr.erase(std::unique(Fr.begin(), Fr.end()), Fr.end());
+            query_initial(Fr);
+            const auto prior = resolve_ext(Fr, bi);  // the visit lists' appended parts
+            for (auto &h : hits) {
+              const uint32_t f = B.from[h.first];
+              std::vector<uint32_t> &dst = res[h.second];
+              const std::vector<uint32_t> &L0 = minit[f];
+              dst.insert(dst.end(), L0.begin(), L0.end());
+              auto it = prior.find(f);
+              if (it != prior.end()) dst.insert(dst.end(), it->second.begin(), it->second.end());
+            }
+          }
+          return res;
+        };
     E->stats.subst_ms += now_ms() - Tm;
     E->stats.map_ms += now_ms() - Tm;
     int32_t *rank_of = A.get<int32_t>("rank_of", S);
@@ -2360,6 +2427,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           HC(hipStreamSynchronize(st));
           need_usig();
         }
+        std::unordered_map<uint32_t, std::vector<uint32_t>> ext;  // appended lists of those signals
         {  // initial map lists of the turning substitutions' signals only
           double Tq = now_ms();
           std::vector<uint32_t> qs;
@@ -2367,6 +2435,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           std::sort(qs.begin(), qs.end());
           qs.erase(std::unique(qs.begin(), qs.end()), qs.end());
           query_initial(qs);
+          ext = resolve_ext(qs, batches.size());
           E->stats.map_ms += now_ms() - Tq;
         }
         // order key: (rank of the turning substitution, first position in map[from])
@@ -2379,8 +2448,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           auto lb = std::lower_bound(L0.begin(), L0.end(), r);  // initial lists are ascending
           if (lb != L0.end() && *lb == r) pos = lb - L0.begin();
           if (pos == UINT64_MAX) {
-            auto it = mext.find(from);
-            if (it != mext.end())
+            auto it = ext.find(from);
+            if (it != ext.end())
               for (uint64_t t = 0; t < it->second.size(); ++t)
                 if (it->second[t] == r) { pos = L0.size() + t; break; }
           }
@@ -2428,29 +2497,17 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (another) {
         double Tq = now_ms();
         need_usig();
-        // RHS keys of the substitutions (the map appends of the next round's ordering)
-        std::vector<uint64_t> uoff(nU), uvals, uptr;
-        std::vector<uint32_t> ulen(nU), ukeys;
+        // this round's batch of appends: every substitution's `from` and RHS keys (no values)
+        MapBatch B;
+        std::vector<uint64_t> uoff(nU);
+        std::vector<uint32_t> ulen(nU);
         HC(hipMemcpyAsync(uoff.data(), d_uoff, 8 * nU, hipMemcpyDeviceToHost, st));
         HC(hipMemcpyAsync(ulen.data(), d_ulen, 4 * nU, hipMemcpyDeviceToHost, st));
         HC(hipStreamSynchronize(st));
-        fetch_pool_maps(E, uoff, ulen, P.pk, P.pv, ukeys, uvals, uptr);
-        query_initial(usig);
+        fetch_pool_keys(E, uoff, ulen, P.pk, B.keys, B.ptr);
+        B.from = usig;
+        batches.push_back(std::move(B));
         E->stats.map_ms += now_ms() - Tq;
-        for (uint64_t i = 0; i < nU; ++i) {
-          uint32_t from = usig[i];
-          const std::vector<uint32_t> &L0 = minit[from];
-          uint64_t n0 = L0.size();
-          auto it = mext.find(from);
-          uint64_t n1 = it == mext.end() ? 0 : it->second.size();
-          if (n0 + n1 == 0) continue;
-          std::vector<uint32_t> visit(L0.begin(), L0.end());
-          if (n1) visit.insert(visit.end(), it->second.begin(), it->second.end());
-          for (uint64_t t = uptr[i]; t < uptr[i + 1]; ++t) {
-            std::vector<uint32_t> &dst = mext[ukeys[t]];
-            dst.insert(dst.end(), visit.begin(), visit.end());
-          }
-        }
       }
       MK.mark("appends2");
       lv.n = nn;

@@ -2129,7 +2129,7 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
               pf_st = pst;
             }
           }
-          val = fmul(F, isw ? c2 : coef, val);
+          val = fmul256(F, isw ? c2 : coef, val);
           if (isr) rv[j] = val;
           wave_sync();
           bool keep = false;
@@ -2171,8 +2171,8 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
         __syncthreads();
         // one product per entry, all lanes at once: work entries c2*v, RHS entries coef*rv
         for (uint32_t q = tid; q < len + rl; q += nt) {
-          if (q < len) wv[cur][q] = fmul(F, c2, wv[cur][q]);
-          else rv[q - len] = fmul(F, coef, rv[q - len]);
+          if (q < len) wv[cur][q] = fmul256(F, c2, wv[cur][q]);
+          else rv[q - len] = fmul256(F, coef, rv[q - len]);
         }
         __syncthreads();
         for (uint32_t i = tid; i < len; i += nt) {  // work keys: -c2*v (+ coef*rv when the RHS has the key)
@@ -3329,6 +3329,17 @@ __global__ void k_pool_to_canon(FieldP F, const uint64_t *off, const uint32_t *l
       Fe c = ffrom_mont(F, pv[off[i] + t]);
       for (int q = 0; q < 4; ++q) ov[4 * (o + t) + q] = c.l[q];
     }
+  }
+}
+
+// keys only (the rounds' map appends read no value): one wave per map, consecutive lanes copy
+// consecutive keys
+__global__ __launch_bounds__(256) void k_pool_keys(const uint64_t *off, const uint32_t *len, const uint64_t *optr, uint64_t n,
+                                                   const uint32_t *pk, uint32_t *ok) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t i = gtid() >> 6; i < n; i += gstride() >> 6) {
+    const uint64_t o = optr[i], b = off[i];
+    for (uint32_t t = lane; t < len[i]; t += 64) ok[o + t] = pk[b + t];
   }
 }
 
