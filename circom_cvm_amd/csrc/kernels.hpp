@@ -36,18 +36,48 @@ __device__ __forceinline__ void wave_atomic_add(unsigned long long *p, unsigned 
 // ---------------------------------------------------------------- small sequential helpers
 // insertion sort by key + combine duplicate keys (sum); zeros are kept (HashMap semantics).
 __device__ inline uint32_t d_sort_combine(const FieldP &F, uint32_t *k, Fe *v, uint32_t n) {
-  for (uint32_t i = 1; i < n; ++i) {
-    uint32_t kk = k[i];
-    Fe vv = v[i];
-    uint32_t j = i;
-    while (j > 0 && k[j - 1] > kk) {
-      k[j] = k[j - 1];
-      v[j] = v[j - 1];
-      --j;
+  if (n <= 32) {  // short lists: insertion sort
+    for (uint32_t i = 1; i < n; ++i) {
+      uint32_t kk = k[i];
+      Fe vv = v[i];
+      uint32_t j = i;
+      while (j > 0 && k[j - 1] > kk) {
+        k[j] = k[j - 1];
+        v[j] = v[j - 1];
+        --j;
+      }
+      k[j] = kk;
+      v[j] = vv;
     }
-    k[j] = kk;
-    v[j] = vv;
+  } else {  // in-place heap sort: n log n moves (a frame-3 expansion of a long row is thousands of
+            // entries; insertion sort moved O(n^2) 36-byte entries on one lane)
+    auto sift = [&](uint32_t i, uint32_t m) {
+      const uint32_t kk = k[i];
+      const Fe vv = v[i];
+      for (;;) {
+        uint32_t c = 2 * i + 1;
+        if (c >= m) break;
+        if (c + 1 < m && k[c + 1] > k[c]) ++c;
+        if (k[c] <= kk) break;
+        k[i] = k[c];
+        v[i] = v[c];
+        i = c;
+      }
+      k[i] = kk;
+      v[i] = vv;
+    };
+    for (uint32_t i = n / 2; i-- > 0;) sift(i, n);
+    for (uint32_t m = n; m-- > 1;) {
+      const uint32_t tk = k[0];
+      const Fe tv = v[0];
+      k[0] = k[m];
+      v[0] = v[m];
+      k[m] = tk;
+      v[m] = tv;
+      sift(0, m);
+    }
   }
+  // equal keys are summed (field addition is commutative: the order among them does not matter)
   uint32_t w = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (w > 0 && k[w - 1] == k[i]) v[w - 1] = fadd(F, v[w - 1], v[i]);
