@@ -75,7 +75,9 @@ struct Arena {
     void *p = nullptr;
     size_t cap = 0;
   };
-  std::map<std::string, B> bufs;
+  // named, grow-only device buffers (a few hundred names, each looked up a few times per run):
+  // one hash probe per lookup
+  std::unordered_map<std::string, B> bufs{512};
   template <class T>
   T *get(const std::string &name, size_t n) {
     size_t bytes = std::max<size_t>(n, 1) * sizeof(T);

@@ -12,14 +12,14 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- \
-  python3 bench.py --steps 5 --warmup 2 --no-cpu > $OUT/trace_bench.log 2>&1
+  python3 bench.py --steps 5 --warmup 2 --no-cpu --no-flatten --no-templated > $OUT/trace_bench.log 2>&1
 echo "trace done"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o f -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu > $OUT/pmc_fetch.log 2>&1
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-flatten --no-templated > $OUT/pmc_fetch.log 2>&1
 echo "fetch done"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o w -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu > $OUT/pmc_write.log 2>&1
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-flatten --no-templated > $OUT/pmc_write.log 2>&1
 echo "write done"
 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/pmc_wrreq -o q -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu > $OUT/pmc_wrreq.log 2>&1
+  python3 bench.py --steps 1 --warmup 0 --no-cpu --no-flatten --no-templated > $OUT/pmc_wrreq.log 2>&1
 echo "wrreq done"
