@@ -2391,6 +2391,33 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           rt.rlist = w.turn_list; rt.n_rlist = w.n_turn;
           HC(hipEventRecord(E->ev0, st));
           launch_capped(st, k_frames_wave<1>, ra.n_ids, fw_blocks(E), w);
+          {  // the rows too long for a wave's LDS batch: A / B / C expanded by one device-wide sort
+            unsigned nbig = 0;
+            HC(hipMemcpyAsync(&nbig, w.n_big, 4, hipMemcpyDeviceToHost, st));
+            HC(hipStreamSynchronize(st));
+            if (nbig) {
+              const uint64_t nseg = 3ull * nbig;
+              uint64_t *xc = A.get<uint64_t>("x.cnt", nseg), *xo = A.get<uint64_t>("x.off", nseg + 1);
+              launch(st, k_xrow_count, nseg, rb, nseg, xc);
+              const uint64_t T = excl_scan_u64(E, xc, xo, nseg, "xrow");
+              h2d(E, xo + nseg, &T, 8);
+              if (T) {
+                uint64_t *xk = A.get<uint64_t>("x.k", T), *xk2 = A.get<uint64_t>("x.k2", T);
+                uint32_t *xi = A.get<uint32_t>("x.i", T), *xi2 = A.get<uint32_t>("x.i2", T);
+                Fe *xv = A.get<Fe>("x.v", T);
+                launch(st, k_xrow_expand, 64 * nseg, rb, nseg, (const uint64_t *)xo, xk, xv, xi);
+                int sb = 1;
+                while (sb < 32 && (1ull << sb) <= nseg) ++sb;
+                sort_pairs(E, (const uint64_t *)xk, xk2, (const uint32_t *)xi, xi2, T, 32 + sb, "xrow");
+                launch(st, k_xrow_combine, 64 * nseg, rb, nseg, (const uint64_t *)xo, (const uint64_t *)xk2,
+                       (const uint32_t *)xi2, (const Fe *)xv);
+              } else {
+                launch(st, k_xrow_combine, 64 * nseg, rb, nseg, (const uint64_t *)xo, (const uint64_t *)nullptr,
+                       (const uint32_t *)nullptr, (const Fe *)nullptr);
+              }
+              rb.pre_expanded = 1;
+            }
+          }
           launch(st, k_round_fill, ra.n_ids, rb);
           launch(st, k_round_turn, ra.n_ids, rt);
           HC(hipEventRecord(E->ev1, st));

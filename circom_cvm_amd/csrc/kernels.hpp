@@ -3172,6 +3172,9 @@ struct RoundArgs {
   const uint32_t *rlist;
   const unsigned *n_rlist;
   unsigned long long *bytes;  // algorithmic bytes: 36 per entry read (row + right-hand sides) or written
+  // k_round_fill: A / B / C were already expanded into oa / ob / oc (lengths in their len arrays) by
+  // k_xrow_count / k_xrow_expand / k_xrow_combine -- the rows too long for a wave's LDS batch
+  int pre_expanded;
 };
 __global__ void k_touch_flags(const uint64_t *cap_c, uint64_t n, uint64_t *flag) {
   for (uint64_t r = gtid(); r < n; r += gstride()) flag[r] = cap_c[r] != 0;
@@ -3287,8 +3290,14 @@ __global__ void k_round_fill(RoundArgs A) {
     // touch C), so it turns iff its final A or B -- all of the round's substitutions applied -- is
     // constant or empty.  The final A and B come first; only the rows that turn (few) replay the
     // substitutions one by one to find the rank at which they turn.
-    uint32_t na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
-    uint32_t nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
+    uint32_t na, nb;
+    if (A.pre_expanded) {
+      na = A.oa.len[r];
+      nb = A.ob.len[r];
+    } else {
+      na = d_apply_frames(fr, A.a.key + A.a.off[r], A.a.val + A.a.off[r], A.a.len[r], A.oa.key + oa, A.oa.val + oa, capa);
+      nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
+    }
     if (d_const_or_empty(A.oa.key + oa, na) || d_const_or_empty(A.ob.key + ob, nb)) {
       d_round_turn(A, r);
       // the replay used the A / B regions as scratch: final A and B again
@@ -3296,7 +3305,9 @@ __global__ void k_round_fill(RoundArgs A) {
       nb = d_apply_frames(fr, A.b.key + A.b.off[r], A.b.val + A.b.off[r], A.b.len[r], A.ob.key + ob, A.ob.val + ob, capb);
     }
     // ---- final content: fix(all substitutions applied)
-    uint32_t nc = d_apply_frames(fr, A.c.key + A.c.off[r], A.c.val + A.c.off[r], A.c.len[r], A.oc.key + oc, A.oc.val + oc, cc);
+    uint32_t nc = A.pre_expanded ? A.oc.len[r]
+                                       : d_apply_frames(fr, A.c.key + A.c.off[r], A.c.val + A.c.off[r], A.c.len[r], A.oc.key + oc,
+                                                        A.oc.val + oc, cc);
     d_fix(F, A.oa.key + oa, A.oa.val + oa, na, A.ob.key + ob, A.ob.val + ob, nb, A.oc.key + oc, A.oc.val + oc, nc,
           A.oc.key + oc + cc, A.oc.val + oc + cc);
     A.oa.len[r] = na;
@@ -3307,6 +3318,113 @@ __global__ void k_round_fill(RoundArgs A) {
              36ull * (na + nb + nc);
   }
   wave_atomic_add(A.bytes, bytes);
+}
+
+// ---- rows too long for a wave's LDS batch (k_frames_wave lists them in rlist): their A, B and C
+// through the round's substitutions as a device-wide sort instead of one lane per row.  Segment
+// s = 3 * i + part (part 0 / 1 / 2 = A / B / C of rlist[i]):
+//   k_xrow_count   entries after expansion (a substituted entry -> its right-hand side),
+//   k_xrow_expand  (s, key) keys + coefficient x RHS values, one wave per segment,
+//   one radix sort of (s, key), then
+//   k_xrow_combine equal keys summed, zero sums dropped, written in key order into the row's output
+//                  region -- what d_apply_frames (frame 3: sort_combine + drop_zeros) produces.
+__device__ __forceinline__ const DRows &d_part(const RoundArgs &A, uint32_t p) { return p == 0 ? A.a : (p == 1 ? A.b : A.c); }
+__global__ void k_xrow_count(RoundArgs A, uint64_t nseg, uint64_t *cnt) {
+  for (uint64_t sg = gtid(); sg < nseg; sg += gstride()) {
+    const uint64_t r = A.rlist[sg / 3];
+    const DRows &P = d_part(A, (uint32_t)(sg % 3));
+    uint64_t c = 0;
+    for (uint32_t i = 0; i < P.len[r]; ++i) {
+      const int32_t s = A.sub_of[P.key[P.off[r] + i]];
+      c += s >= 0 ? A.h_len[s] : 1;
+    }
+    cnt[sg] = c;
+  }
+}
+__global__ __launch_bounds__(256) void k_xrow_expand(RoundArgs A, uint64_t nseg, const uint64_t *soff, uint64_t *xk, Fe *xv,
+                                                     uint32_t *xi) {
+  const FieldP &F = A.F;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t sg = gtid() >> 6; sg < nseg; sg += gstride() >> 6) {
+    const uint64_t r = A.rlist[sg / 3];
+    const DRows &P = d_part(A, (uint32_t)(sg % 3));
+    const uint64_t ro = P.off[r];
+    const uint32_t n = P.len[r];
+    uint64_t base = soff[sg];
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+      const uint32_t i = c0 + lane;
+      uint32_t k = 0, m = 0;
+      int32_t s = -1;
+      if (i < n) {
+        k = P.key[ro + i];
+        s = A.sub_of[k];
+        m = s >= 0 ? A.h_len[s] : 1;
+      }
+      uint32_t x = m;  // inclusive scan of the counts over the wave
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += y;
+      }
+      const uint64_t o = base + x - m;
+      if (i < n) {
+        const Fe vv = P.val[ro + i];
+        if (s < 0) {
+          xk[o] = ((uint64_t)sg << 32) | k;
+          xv[o] = vv;
+          xi[o] = (uint32_t)(o - soff[sg]);
+        } else {
+          const uint64_t hb = A.h_off[s];
+          for (uint32_t t = 0; t < m; ++t) {
+            xk[o + t] = ((uint64_t)sg << 32) | A.pk[hb + t];
+            xv[o + t] = fmul(F, vv, A.pv[hb + t]);
+            xi[o + t] = (uint32_t)(o + t - soff[sg]);
+          }
+        }
+      }
+      base += __shfl(x, 63);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_xrow_combine(RoundArgs A, uint64_t nseg, const uint64_t *soff, const uint64_t *xk,
+                                                      const uint32_t *xi, const Fe *xv) {
+  const FieldP &F = A.F;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t sg = gtid() >> 6; sg < nseg; sg += gstride() >> 6) {
+    const uint64_t r = A.rlist[sg / 3];
+    const uint32_t p = (uint32_t)(sg % 3);
+    const DRows &O = p == 0 ? A.oa : (p == 1 ? A.ob : A.oc);
+    uint32_t *ok = O.key + O.off[r];
+    Fe *ov = O.val + O.off[r];
+    const uint64_t b = soff[sg], e = soff[sg + 1];
+    uint32_t w = 0;
+    for (uint64_t q0 = b; q0 < e; q0 += 64) {
+      const uint64_t q = q0 + lane;
+      bool keep = false;
+      uint32_t key = 0;
+      Fe sum = fe_zero();
+      if (q < e) {
+        key = (uint32_t)xk[q];
+        if (q == b || (uint32_t)xk[q - 1] != key) {  // the head of a run of equal keys sums it
+          sum = xv[b + xi[q]];
+          for (uint64_t t = q + 1; t < e && (uint32_t)xk[t] == key; ++t) sum = fadd(F, sum, xv[b + xi[t]]);
+          keep = !fe_is_zero(sum);
+        }
+      }
+      const uint64_t km = __ballot(keep);
+      if (keep) {
+        const uint32_t at = w + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+        ok[at] = key;
+        ov[at] = sum;
+      }
+      w += (uint32_t)__popcll(km);
+    }
+    if (lane == 0) {
+      if (p == 0) A.oa.len[r] = w;
+      else if (p == 1) A.ob.len[r] = w;
+      else A.oc.len[r] = w;
+    }
+  }
 }
 
 // The turn ranks of the rows k_frames_wave listed (their final content is already written).
