@@ -340,7 +340,7 @@ __global__ __launch_bounds__(64) void k_cl_replay_wave(const uint64_t *cl_off, c
 // chain's composed right-hand sides), which one lane would merge serially for tens of ms.  Both
 // kernels run the same process_3 / process_4 rules, and results are collected by cluster index, so
 // the routing changes no output.
-constexpr uint32_t kHeavyNnz = 256;
+constexpr uint32_t kHeavyNnz = 128;  // MI355X sweep: templated round-2 small clusters 21.8 -> 7.4 ms vs 256, metric device time unchanged
 __global__ void k_cl_sizekey(const uint64_t *cl_off, uint64_t n_cl, const uint32_t *srow, const uint32_t *len,
                              uint64_t *skey, uint32_t *sidx,
                              unsigned long long *cnt /* [0] >= 1e6, [1] workgroup kernels, [2] LDS replay, [3] > LDS, [4] large LDS replay */) {
