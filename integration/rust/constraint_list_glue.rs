@@ -15,15 +15,42 @@
 // canonical 4 x u64 little-endian coefficients and returns the storage order with ORIGINAL signal
 // ids plus an int32 label -> wire map; the glue rebuilds ConstraintStorage and SignalMap from them.
 // A non-zero status panics with rs_last_error(), as the reference panics on its own invariants.
+//
+// BigInt <-> limbs goes through the byte conversions the reference itself uses: `to_bytes_le`
+// (constraint_writers/src/r1cs_writer.rs:25-28) and `BigInt::from_bytes_le(Sign::Plus, ..)`
+// (constraint_writers/src/r1cs_reader.rs:41); `is_zero` comes from num_traits::Zero as in
+// circom_algebra/src/algebra.rs:4.  tests/test_integration.py rejects any other BigInt method.
+// Not compiled in this repository (no cargo in the build image); the bindings it uses are checked
+// against include/rs_simplify.h by tests/test_integration.py.
 use crate::{EncodingIterator, SignalMap, Simplifier};
 use circom_algebra::algebra::Constraint;
 use circom_algebra::constraint_storage::ConstraintStorage;
-use circom_algebra::num_bigint::BigInt;
+use circom_algebra::num_bigint::{BigInt, Sign};
+use circom_algebra::num_traits::Zero;
 use rs_simplify_sys as ffi;
 use std::collections::HashMap;
-use std::ffi::CStr;
+use std::ffi::{CStr, CString};
 
 type C = Constraint<usize>;
+
+/// A canonical (non-negative, < 2^256) field element as 4 little-endian u64 limbs.
+fn to_limbs(v: &BigInt) -> [u64; 4] {
+    let (_, bytes) = v.to_bytes_le();
+    let mut limbs = [0u64; 4];
+    for (i, b) in bytes.iter().enumerate().take(32) {
+        limbs[i / 8] |= (*b as u64) << (8 * (i % 8));
+    }
+    limbs
+}
+
+/// The inverse of `to_limbs` (the library returns canonical values).
+fn from_limbs(limbs: &[u64]) -> BigInt {
+    let mut bytes = Vec::with_capacity(32);
+    for l in limbs {
+        bytes.extend_from_slice(&l.to_le_bytes());
+    }
+    BigInt::from_bytes_le(Sign::Plus, &bytes)
+}
 
 /// One owned CSR block (the arrays an rs_lc points at).
 struct Csr {
@@ -42,10 +69,7 @@ impl Csr {
         keys.sort_by_key(|(k, _)| **k);
         for (k, v) in keys {
             self.col.push(*k as u32);
-            let (_, digits) = v.to_u64_digits(); // canonical (< p)
-            for i in 0..4 {
-                self.val.push(*digits.get(i).unwrap_or(&0));
-            }
+            self.val.extend_from_slice(&to_limbs(v)); // canonical (< p)
         }
         self.ptr.push(self.col.len() as u64);
     }
@@ -62,12 +86,7 @@ impl Csr {
 
 fn prime_id(field: &BigInt) -> (u32, [u64; 4]) {
     // every --prime of program_structure/src/utils/constants.rs:3-13 is passed as its value
-    let (_, d) = field.to_u64_digits();
-    let mut p = [0u64; 4];
-    for (i, x) in d.iter().take(4).enumerate() {
-        p[i] = *x;
-    }
-    (255, p) // RS_PRIME_CUSTOM: the library derives its field constants from the value
+    (255, to_limbs(field)) // RS_PRIME_CUSTOM: the library derives its field constants from the value
 }
 
 fn non_linear_rows(iter: EncodingIterator, a: &mut Csr, b: &mut Csr, c: &mut Csr) {
@@ -136,7 +155,7 @@ pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, Signal
         for e in lo..hi {
             let k = unsafe { *lc.col.add(e) } as usize;
             let limbs: Vec<u64> = (0..4).map(|i| unsafe { *lc.val.add(4 * e + i) }).collect();
-            m.insert(k, BigInt::from_slice_native(&limbs)); // canonical, non-negative
+            m.insert(k, from_limbs(&limbs)); // canonical, non-negative
         }
         m
     };
@@ -153,6 +172,17 @@ pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, Signal
         }
     }
     let npiw = o.no_private_inputs_witness as usize;
+    if smp.port_substitution {
+        // --simplification_substitution: the reference opens SubstitutionJSON at json_substitutions
+        // and logs every substitution (constraint_simplification.rs:448-453, 9-17); the library
+        // returned the same log in out->log_* and writes the same file.
+        let path = CString::new(smp.json_substitutions.clone()).expect("path without NUL");
+        let rc = unsafe { ffi::rs_write_substitution_json(path.as_ptr(), out) };
+        if rc != ffi::RS_OK {
+            let msg = unsafe { CStr::from_ptr(ffi::rs_last_error()) }.to_string_lossy().into_owned();
+            panic!("rs_write_substitution_json failed ({}): {}", rc, msg);
+        }
+    }
     unsafe { ffi::rs_output_free(out) };
     (storage, signal_map, npiw)
 }

@@ -1,4 +1,4 @@
-//! Raw bindings of `include/rs_simplify.h` (ABI 5), one item per C declaration, same order and
+//! Raw bindings of `include/rs_simplify.h` (ABI 6), one item per C declaration, same order and
 //! layout.  The safe wrapper a caller uses is `constraint_list_glue.rs` (the body that replaces
 //! `constraint_list::constraint_simplification::simplification`, constraint_simplification.rs:442).
 #![allow(non_camel_case_types)]

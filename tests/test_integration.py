@@ -119,3 +119,42 @@ def test_r1cs_diff_tool():
         open(c, "wb").write(R.result_to_r1cs(sys_, R.Result(cons, res.signal_map, res.no_private_inputs_witness)))
         r = _tool(a, c)
         assert r.returncode == 1 and "constraint" in r.stdout, r.stdout + r.stderr
+
+
+GLUE = os.path.join(ROOT, "integration", "rust", "constraint_list_glue.rs")
+# num-bigint(-dig) BigInt API the reference itself calls on the path's data (file:line in
+# /root/reference): to_bytes_le (constraint_writers/src/r1cs_writer.rs:26), from_bytes_le
+# (r1cs_reader.rs:41), to/from_signed_bytes_le (circom_algebra/src/constraint_storage/logic.rs:7,25),
+# is_zero via num_traits::Zero (circom_algebra/src/algebra.rs:4), BigInt::from (algebra.rs passim).
+BIGINT_ALLOWED = {"to_bytes_le", "from_bytes_le", "to_signed_bytes_le", "from_signed_bytes_le", "is_zero", "from"}
+# other BigInt / BigUint methods of num-bigint: none may appear in the glue (the pinned
+# num-bigint-dig 0.8.4 is not vendored, so only calls the reference makes are known to exist)
+BIGINT_API = {"to_u64_digits", "to_u32_digits", "from_slice", "from_slice_native", "from_biguint", "to_biguint",
+              "from_radix_be", "from_radix_le", "to_radix_be", "to_radix_le", "to_str_radix", "parse_bytes",
+              "magnitude", "into_parts", "bits", "from_bytes_be", "to_bytes_be", "from_signed_bytes_be",
+              "to_signed_bytes_be", "modpow", "sqrt", "cbrt", "nth_root", "trailing_zeros", "set_bit", "bit",
+              "mod_inverse", "to_u64", "to_i64", "from_u64", "new", "assign_from_slice", "iter_u64_digits",
+              "iter_u32_digits", "to_usize"}
+
+
+def test_rust_glue_uses_only_reference_bigint_calls():
+    src = re.sub(r"//[^\n]*", "", open(GLUE).read())
+    calls = set(re.findall(r"\.(\w+)\(", src)) | set(re.findall(r"BigInt::(\w+)\(", src))
+    bad = (calls & BIGINT_API) - BIGINT_ALLOWED
+    assert not bad, f"BigInt methods the reference never calls: {sorted(bad)}"
+    for m in re.findall(r"BigInt::(\w+)\(", src):
+        assert m in BIGINT_ALLOWED, m
+    if ".is_zero(" in src:
+        assert re.search(r"use circom_algebra::num_traits::Zero;", src), "is_zero needs num_traits::Zero in scope"
+    if "Sign::" in src:
+        assert re.search(r"use circom_algebra::num_bigint::\{[^}]*\bSign\b", src)
+    # every ffi call in the glue is a function the header declares
+    for f in re.findall(r"ffi::(rs_\w+)\(", src):
+        assert f in c_functions(), f
+    # --simplification_substitution writes the log file (constraint_simplification.rs:448-453)
+    assert "rs_write_substitution_json" in src and "json_substitutions" in src
+
+
+def test_rust_lib_doc_abi_matches_header():
+    ver = re.search(r"#define RS_ABI_VERSION (\d+)", open(HDR).read()).group(1)
+    assert f"(ABI {ver})" in open(RS).read().splitlines()[0]
