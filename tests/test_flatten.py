@@ -2,9 +2,14 @@
 oracle/pyref.py flatten_dag (a restatement of dag/src/map_to_constraint_list.rs:12-44 / :111-150
 and the EncodingIterator DFS, constraint_list/src/lib.rs:65-108): the rs_input blocks, the forbidden
 set and max_signal array for array, then the flattened input through the simplifier against pyref.
-Parity unpinned beyond the oracle: the reference holds no DAG fixtures (its DAGs come from the
-compiler front end)."""
+Pinned to reference data by the docs' basic.circom (Main + one Internal multiplier): flattening its
+two-node DAG must give the --O0 constraint list of mkdocs/docs/circom-language/formats/
+constraints-json.md:77-81 and the --O0 witness / component columns of formats/sym.md:65-70, and the
+flattened input simplified must give the O1 / O2 texts (constraints-json.md:57-59, 95-96; sym.md:46-51,
+81-86).  Random DAGs beyond that are checked against pyref alone."""
 import ctypes as C
+import os
+import sys
 
 import numpy as np
 import pytest
@@ -14,6 +19,56 @@ import rsio
 import circom_cvm_amd as M
 
 R = rsio.R
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+import make_golden as G  # noqa: E402
+
+
+def docs_basic_dag():
+    """basic.circom / symbols.circom of the docs as the DAG constraint_generation builds: node 0 =
+    Internal (locals out=1, in[0]=2, in[1]=3; `out <== in[0]*in[1]` with C negated,
+    algebra.rs:113-145), node 1 = Main (locals out=1, in[0]=2, in[1]=3; its component c at
+    in_number 3, so c's signals are 4..6; the three `<==` of Main).  Node ids are the sym.md #c
+    column: main.* -> 1, main.c.* -> 0."""
+    p = R.PRIMES["bn128"]
+    m = p - 1
+    internal = R.DagNode([R.Con({2: m}, {3: 1}, {1: m})], [1, 2, 3])
+    main = R.DagNode([R.Con({}, {}, {2: 1, 5: m}), R.Con({}, {}, {0: 1, 2: 2, 3: 1, 6: m}),
+                      R.Con({}, {}, {1: m, 4: 1})], [1, 2, 3], edges=[(0, 3)])
+    d = G.DOCS
+    return p, [internal, main], 1, d["n_pub_out"], d["n_pub_in"], d["n_priv_in"], {0, 1}
+
+
+def _docs_o0_classes():
+    """constraints-json.md:77-81 split the way map_tree classifies (map_to_constraint_list.rs:12-44),
+    each class keeping the docs' (DFS) order."""
+    sys_ = G.docs_system()
+    ce, eq, lin, nl = R.classify(sys_)
+    return sys_, {"cons_eq": ce, "eq": eq, "linear": lin, "non_linear": nl}
+
+
+def _sym_o0():
+    return [tuple(int(x) if i < 3 else x for i, x in enumerate(l.split(",", 3))) for l in G.DOCS["sym_o0"]]
+
+
+def test_docs_basic_flatten_oracle():
+    """pyref.flatten_dag on the docs DAG = the reference's published --O0 export."""
+    p, nodes, main, no, npb, npr, forb = docs_basic_dag()
+    sys_, b = R.flatten_dag(p, nodes, main, no, npb, npr, forb)
+    # the --O0 constraint list, in DFS order (constraints-json.md:77-81)
+    assert G.rows_to_json(sys_.rows) == G.DOCS["constraints"]["O0"]
+    ref_sys, classes = _docs_o0_classes()
+    for k in classes:
+        assert [(c.a, c.b, c.c) for c in b[k]] == [(c.a, c.b, c.c) for c in classes[k]], k
+    assert (sys_.max_signal, sys_.forbidden) == (ref_sys.max_signal, ref_sys.forbidden)
+    # sym.md:65-70: --O0 witness = signal order; the #c column names the instance's node
+    assert b["witness"] == [0] + [ln[1] for ln in _sym_o0()]
+    owner = {s: (1 if s <= 3 else 0) for s in range(1, 7)}
+    assert all(ln[2] == owner[ln[0]] for ln in _sym_o0())
+    # and simplified: the O1 / O2 texts of the docs
+    for lvl in ("O1", "O2"):
+        res = R.simplification(sys_, G.flags_of(lvl))
+        assert R.to_json_constraints(res.constraints, res.signal_map) == G.DOCS["constraints"][lvl]
+        assert R.result_to_sym(_sym_o0(), res).splitlines() == G.DOCS["sym"][lvl]
 
 
 def blocks_of(inp):
@@ -84,6 +139,30 @@ def test_flatten_parity_random(prime):
         sys_, b = R.flatten_dag(p, nodes, main, no, npb, npr, forb)
         inp = M.Dag(p, nodes, main, no, npb, npr, forb, prime).flatten(0)
         _eq_blocks(blocks_of(inp.c), b, sys_)
+
+
+@pytest.mark.gpu
+def test_docs_basic_flatten_device():
+    """rs_flatten_dag on the docs DAG = the --O0 export of constraints-json.md:77-81 (class by class,
+    DFS order), then the device simplifier on that input = the docs' O1 / O2 constraints and
+    witness columns (constraints-json.md:57-59, 95-96; sym.md:46-51, 81-86)."""
+    p, nodes, main, no, npb, npr, forb = docs_basic_dag()
+    inp = M.Dag(p, nodes, main, no, npb, npr, forb, "bn128").flatten(0)
+    ce, eq, lin, nl, fb, ms = blocks_of(inp.c)
+    ref_sys, classes = _docs_o0_classes()
+    for name, got in (("cons_eq", ce), ("eq", eq), ("linear", lin), ("non_linear", nl)):
+        assert [(c.a, c.b, c.c) for c in got] == [(c.a, c.b, c.c) for c in classes[name]], name
+    assert (ms, fb) == (ref_sys.max_signal, ref_sys.forbidden)
+    eng = M.Engine(0)
+    for lvl in ("O1", "O2"):
+        eng.load(inp.c)
+        eng.run(rsio.flags(lvl))
+        out = eng.fetch()
+        cons, sm, _, npiw = rsio.output_to_py(out.c)
+        res = R.Result(cons, sm, npiw)
+        assert R.to_json_constraints(res.constraints, res.signal_map) == G.DOCS["constraints"][lvl], lvl
+        assert R.result_to_sym(_sym_o0(), res).splitlines() == G.DOCS["sym"][lvl], lvl
+    eng.close()
 
 
 @pytest.mark.gpu
