@@ -16,6 +16,7 @@
 #include <thread>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <functional>
 #include <vector>
 
@@ -2227,41 +2228,75 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       std::vector<uint64_t> ptr;
     };
     std::vector<MapBatch> batches;
-    std::vector<uint8_t> hmark;  // membership marks over the signals, all zero between uses
     // the appended lists of the signals X from batches [0, upto), in append order: batch, then
     // substitution, then RHS position (a substitution's `from` is in no RHS of its own round, so a
-    // batch's appends never depend on each other; a visit list depends on earlier batches only)
-    std::function<std::unordered_map<uint32_t, std::vector<uint32_t>>(const std::vector<uint32_t> &, size_t)> resolve_ext =
-        [&](const std::vector<uint32_t> &X, size_t upto) {
-          std::unordered_map<uint32_t, std::vector<uint32_t>> res;
-          if (X.empty() || upto == 0) return res;
-          if (hmark.empty()) hmark.assign(S, 0);
-          for (size_t bi = 0; bi < upto; ++bi) {
-            const MapBatch &B = batches[bi];
-            std::vector<std::pair<uint32_t, uint32_t>> hits;  // (substitution, key)
-            for (uint32_t x : X) hmark[x] = 1;
-            for (uint64_t j = 0; j < B.from.size(); ++j)
-              for (uint64_t t = B.ptr[j]; t < B.ptr[j + 1]; ++t)
-                if (hmark[B.keys[t]]) hits.push_back({(uint32_t)j, B.keys[t]});
-            for (uint32_t x : X) hmark[x] = 0;
-            if (hits.empty()) continue;
-            std::vector<uint32_t> Fr;
-            for (auto &h : hits) Fr.push_back(B.from[h.first]);
-            std::sort(Fr.begin(), Fr.end());
-            Fr.erase(std::unique(Fr.begin(), Fr.end()), Fr.end());
-            query_initial(Fr);
-            const auto prior = resolve_ext(Fr, bi);  // the visit lists' appended parts
-            for (auto &h : hits) {
-              const uint32_t f = B.from[h.first];
-              std::vector<uint32_t> &dst = res[h.second];
-              const std::vector<uint32_t> &L0 = minit[f];
-              dst.insert(dst.end(), L0.begin(), L0.end());
-              auto it = prior.find(f);
-              if (it != prior.end()) dst.insert(dst.end(), it->second.begin(), it->second.end());
-            }
+    // batch's appends never depend on each other; a visit list depends on earlier batches only).
+    // list(x, u) = concat over batches b < u, over the substitutions j of b whose RHS holds x (in
+    // order): minit[from_j] ++ list(from_j, b) -- memoised per (signal, batch bound), so chains of
+    // rounds cost one evaluation per pair instead of one per path.
+    std::vector<std::unordered_map<uint32_t, std::vector<uint32_t>>> bidx;  // per batch: key -> j's
+    auto batch_index = [&](size_t bi) -> const std::unordered_map<uint32_t, std::vector<uint32_t>> & {
+      if (bidx.size() < batches.size()) bidx.resize(batches.size());
+      auto &ix = bidx[bi];
+      if (ix.empty() && !batches[bi].keys.empty()) {
+        const MapBatch &B = batches[bi];
+        for (uint64_t j = 0; j < B.from.size(); ++j)
+          for (uint64_t t = B.ptr[j]; t < B.ptr[j + 1]; ++t) ix[B.keys[t]].push_back((uint32_t)j);
+      }
+      return ix;
+    };
+    std::unordered_map<uint64_t, std::vector<uint32_t>> ext_memo;
+    auto memo_key = [&](uint32_t x, size_t u) { return (uint64_t)x * (batches.size() + 1) + u; };
+    std::function<const std::vector<uint32_t> &(uint32_t, size_t)> ext_list = [&](uint32_t x, size_t u) -> const std::vector<uint32_t> & {
+      const uint64_t key = memo_key(x, u);
+      auto it = ext_memo.find(key);
+      if (it != ext_memo.end()) return it->second;
+      std::vector<uint32_t> out;
+      for (size_t bi = 0; bi < u; ++bi) {
+        const auto &ix = batch_index(bi);
+        auto h = ix.find(x);
+        if (h == ix.end()) continue;
+        for (uint32_t j : h->second) {
+          const uint32_t f = batches[bi].from[j];
+          const std::vector<uint32_t> &L0 = minit[f];
+          out.insert(out.end(), L0.begin(), L0.end());
+          const std::vector<uint32_t> &pr = ext_list(f, bi);
+          out.insert(out.end(), pr.begin(), pr.end());
+        }
+      }
+      return ext_memo.emplace(key, std::move(out)).first->second;
+    };
+    auto resolve_ext = [&](const std::vector<uint32_t> &X, size_t upto) {
+      std::unordered_map<uint32_t, std::vector<uint32_t>> res;
+      if (X.empty() || upto == 0) return res;
+      // every `from` the lists reach, fetched from the device in one query
+      std::vector<uint32_t> froms;
+      std::unordered_set<uint64_t> seen;
+      std::vector<std::pair<uint32_t, size_t>> work;
+      for (uint32_t x : X) work.push_back({x, upto});
+      while (!work.empty()) {
+        auto [x, u] = work.back();
+        work.pop_back();
+        if (!seen.insert(memo_key(x, u)).second || ext_memo.count(memo_key(x, u))) continue;
+        for (size_t bi = 0; bi < u; ++bi) {
+          const auto &ix = batch_index(bi);
+          auto h = ix.find(x);
+          if (h == ix.end()) continue;
+          for (uint32_t j : h->second) {
+            froms.push_back(batches[bi].from[j]);
+            work.push_back({batches[bi].from[j], bi});
           }
-          return res;
-        };
+        }
+      }
+      std::sort(froms.begin(), froms.end());
+      froms.erase(std::unique(froms.begin(), froms.end()), froms.end());
+      query_initial(froms);
+      for (uint32_t x : X) {
+        const std::vector<uint32_t> &L = ext_list(x, upto);
+        if (!L.empty()) res[x] = L;
+      }
+      return res;
+    };
     E->stats.subst_ms += now_ms() - Tm;
     E->stats.map_ms += now_ms() - Tm;
     int32_t *rank_of = A.get<int32_t>("rank_of", S);
@@ -3000,6 +3035,24 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
     hipStream_t st = E->st;
     const uint32_t fs = (uint32_t)field_size_bytes(E->prime);
     const uint64_t n = E->out_n_dev, S = E->S;
+    if (getenv("RS_WRITER_HOST") || n >= (1ull << (64 - kLeKeyBits)) || E->out_nnz[0] >> 32 || E->out_nnz[1] >> 32 || E->out_nnz[2] >> 32) {
+      // the device sort key holds the row in 64 - 36 = 28 bits and the entry index in 32: beyond
+      // that, the host writer over the fetched result (same bytes, no such limits)
+      rs_output *o = nullptr;
+      int rc = rs_engine_fetch(E, &o);
+      if (rc != RS_OK) return rc;
+      rs_input hin{};
+      hin.prime_id = RS_PRIME_CUSTOM;
+      memcpy(hin.prime, E->prime, sizeof(hin.prime));
+      hin.max_signal = S;
+      hin.n_pub_out = E->n_pub_out;
+      hin.n_pub_in = E->n_pub_in;
+      hin.n_priv_in = E->n_priv_in;
+      rc = o0_r1cs ? rs_write_r1cs_gates(path, &hin, o, o0_r1cs) : rs_write_r1cs(path, &hin, o);
+      rs_output_free(o);
+      E->stats.write_ms = now_ms() - t0;
+      return rc;
+    }
     const char *nm[3] = {"out.a", "out.b", "out.c"};
     const uint64_t *pq[3];
     for (int q = 0; q < 3; ++q) pq[q] = A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1);

@@ -183,6 +183,20 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
       throw RsError(RS_E_INVALID, "rs_flatten_dag: offsets decrease");
   for (uint64_t e = 0; e < n_edges; ++e)
     if (D->edge_to[e] >= N) throw RsError(RS_E_INVALID, "rs_flatten_dag: edge to a missing node");
+  // the CSR blocks: every row's entries inside [0, nnz) (the host classification and the device
+  // copy read col / val up to ptr[T])
+  for (const rs_lc *b : {&D->a, &D->b, &D->c}) {
+    if (b->ptr[0] != 0 || b->ptr[T] != b->nnz) throw RsError(RS_E_INVALID, "rs_flatten_dag: ptr[0] != 0 or ptr[T] != nnz");
+    for (uint64_t t = 0; t < T; ++t)
+      if (b->ptr[t] > b->ptr[t + 1]) throw RsError(RS_E_INVALID, "rs_flatten_dag: row pointers decrease");
+  }
+  // the largest node-local id of every node (its constraints' keys, its own signals)
+  std::vector<uint64_t> maxkey(N, 0);
+  for (uint32_t v = 0; v < N; ++v) {
+    for (uint64_t i = D->local_off[v]; i < D->local_off[v + 1]; ++i) maxkey[v] = std::max<uint64_t>(maxkey[v], D->locals[i]);
+    for (const rs_lc *b : {&D->a, &D->b, &D->c})
+      for (uint64_t e = b->ptr[D->cons_off[v]]; e < b->ptr[D->cons_off[v + 1]]; ++e) maxkey[v] = std::max<uint64_t>(maxkey[v], b->col[e]);
+  }
   // ---- templates (host): classes, ranks and entry prefixes within the class, counts
   std::vector<uint8_t> cls(T);
   std::vector<uint32_t> rank(T), rank_ne(T);
@@ -241,6 +255,7 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
   }
   // subtree sizes (instances) in reverse topological order; per edge, the earlier siblings' subtrees
   std::vector<uint64_t> sz(N, 0), epre(n_edges);
+  std::vector<uint32_t> post;  // DFS post-order of the nodes reachable from main
   {
     std::vector<uint8_t> state(N, 0);  // 0 new, 1 on the stack, 2 done
     std::vector<std::pair<uint32_t, uint64_t>> stk;
@@ -266,10 +281,23 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
       }
       sz[v] = s;
       state[v] = 2;
+      post.push_back(v);
       stk.pop_back();
     }
   }
   const uint64_t n_inst = sz[D->main_node];
+  {  // the largest instance offset of every reachable node (reverse post-order is topological):
+     // every offset id (offset + local id) must stay below the engine's 2^31 signal bound
+    std::vector<uint64_t> maxoff(N, 0);
+    for (size_t i = post.size(); i-- > 0;) {
+      const uint32_t v = post[i];
+      if (maxoff[v] + maxkey[v] >= (1ull << 31)) throw RsError(RS_E_INVALID, "rs_flatten_dag: signal ids overflow 2^31");
+      for (uint64_t e = D->edge_off[v]; e < D->edge_off[v + 1]; ++e) {
+        if (D->edge_in[e] >= (1ull << 31)) throw RsError(RS_E_INVALID, "rs_flatten_dag: signal ids overflow 2^31");
+        maxoff[D->edge_to[e]] = std::max(maxoff[D->edge_to[e]], maxoff[v] + D->edge_in[e]);
+      }
+    }
+  }
   // ---- device: upload the templates, expand the instance tree level by level
   FlArgs A{};
   A.cons_off = fl_up(E, "cons_off", D->cons_off, N + 1);
@@ -331,7 +359,7 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
   HC(hipMemcpyAsync(&last_p, A.pre + n_inst - 1, sizeof(FlCnt), hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
   for (int k = 0; k < kFlN; ++k) tot.v[k] = last_c.v[k] + last_p.v[k];
-  if (tot.v[12] + 1 > 0xffffffffull) throw RsError(RS_E_INVALID, "rs_flatten_dag: more than 2^32 signals");
+  if (tot.v[12] + 1 >= (1ull << 31)) throw RsError(RS_E_INVALID, "rs_flatten_dag: 2^31 signals or more");
   // ---- emit the blocks
   const uint64_t rows[6] = {tot.v[0], tot.v[1], tot.v[2], tot.v[3], tot.v[3], tot.v[3]};
   const uint64_t nnz[6] = {tot.v[4], tot.v[5], tot.v[6], tot.v[7], tot.v[8], tot.v[9]};

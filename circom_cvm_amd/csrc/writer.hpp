@@ -32,8 +32,10 @@ __global__ void k_w_keys(const uint64_t *ptr, uint64_t n_rows, const uint32_t *c
     for (uint64_t e = ptr[r]; e < ptr[r + 1]; ++e) {
       const uint32_t c = col[e];
       const int32_t w = c == 0 ? 0 : l2w[c];
-      if (w < 0) { atomicOr(err, 1); continue; }  // apply_raw_correspondence would panic
-      key[e] = (r << kLeKeyBits) | d_le_order_key((uint32_t)w);
+      // apply_raw_correspondence would panic: flagged, and the entry keeps a key inside its own row
+      // (the largest one) so the sort and k_w_entries stay in bounds until the host reads `err`
+      if (w < 0) atomicOr(err, 1);
+      key[e] = (r << kLeKeyBits) | (w < 0 ? (1ull << kLeKeyBits) - 1 : d_le_order_key((uint32_t)w));
       idx[e] = (uint32_t)e;
     }
   }
@@ -69,7 +71,7 @@ __global__ void k_w_entries(const uint64_t *skey, const uint32_t *sidx, uint64_t
     if (q >= 2) base += (pb[r + 1] - pb[r]) * es + 1;
     uint32_t *o = out + base + t * es;
     const uint32_t c = col[e];
-    o[0] = c == 0 ? 0u : (uint32_t)l2w[c];
+    o[0] = c == 0 ? 0u : (uint32_t)l2w[c];  // a removed signal (-1) only reaches here when err is set
     const uint32_t *v = (const uint32_t *)(val + 4 * (uint64_t)e);
     for (uint32_t i = 0; i < fs / 4; ++i) o[1 + i] = v[i];
   }

@@ -305,8 +305,9 @@ typedef struct rs_dag {
   const uint32_t *edge_to;     /* child node                                                      */
   const uint64_t *edge_in;     /* the edge's in_number: the child's signal offset in the parent   */
 } rs_dag;
-/* device: the GPU to run on.  Rejects (RS_E_INVALID) a cyclic graph, out-of-range ids and a graph
- * whose instances overflow 32-bit signal ids. */
+/* device: the GPU to run on.  Rejects (RS_E_INVALID) a cyclic graph, an edge to a missing node,
+ * malformed CSR blocks (ptr[0] != 0, decreasing pointers, ptr[T] != nnz) and a graph whose offset
+ * signal ids (instance offset + node-local id) or signal count reach 2^31. */
 int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in);
 
 #ifdef __cplusplus

@@ -204,3 +204,24 @@ def test_flatten_rejects_cycle_and_bad_edge():
     c = R.DagNode([R.Con({}, {}, {1: 1})], [1], edges=[(7, 1)])
     with pytest.raises(M.RsError):
         M.Dag(p, [c], 0, 0, 0, 0, {0}, "bn128").flatten(0)
+
+
+@pytest.mark.gpu
+def test_flatten_rejects_malformed_blocks():
+    """Row pointers that leave [0, nnz) and offsets past the 2^31 signal bound are RS_E_INVALID,
+    before anything is read out of bounds (host classification or device copy)."""
+    p = R.PRIMES["bn128"]
+    leaf = R.DagNode([R.Con({}, {}, {1: 1, 2: 3})], [1, 2])
+    main = R.DagNode([R.Con({1: 1}, {2: 1}, {3: 1})], [1, 2], edges=[(0, 2)])
+    d = M.Dag(p, [leaf, main], 1, 1, 0, 1, {0, 1}, "bn128")
+    d.flatten(0).free()  # well-formed: accepted
+    d.parts[2].ptr[-1] += 1  # C's ptr[T] past nnz
+    with pytest.raises(M.RsError):
+        d.flatten(0)
+    d.parts[2].ptr[-1] -= 1
+    d.edge_in[0] = 1 << 31  # the leaf's ids past 2^31
+    with pytest.raises(M.RsError):
+        d.flatten(0)
+    d.edge_in[0] = (1 << 31) - 2  # leaf id 2 + offset reaches 2^31
+    with pytest.raises(M.RsError):
+        d.flatten(0)

@@ -85,3 +85,20 @@ def test_device_writer_custom_gates():
             assert a == b
             assert b == R.result_to_r1cs(sys_, R.simplification(sys_, rsio.py_flags(rsio.flags(lvl))))
     eng.close()
+
+
+def test_writer_host_fallback_same_bytes(monkeypatch):
+    """Outputs past the device sort key's range (2^28 rows or 2^32 entries of a part) are written by
+    the host writer over the fetched result; forced here (RS_WRITER_HOST), the bytes are the device
+    writer's."""
+    p = R.PRIMES["bn128"]
+    eng = M.Engine(0)
+    with tempfile.TemporaryDirectory() as tmp:
+        sys_ = rsio.gen_system(977, p, n_sig=900, n_rows=700, density=2.5)
+        h = rsio.InputHolder(sys_, "bn128")
+        eng.simplify(h.inp, rsio.flags("O2"))
+        a = device_bytes(eng, os.path.join(tmp, "d.r1cs"))
+        monkeypatch.setenv("RS_WRITER_HOST", "1")
+        b = device_bytes(eng, os.path.join(tmp, "h.r1cs"))
+        assert a == b
+    eng.close()
