@@ -27,6 +27,7 @@
 #include "host_common.hpp"
 #include "kernels.hpp"
 #include "frames_wave.hpp"
+#include "spec_loop.hpp"
 #include "cluster.hpp"
 #include "writer.hpp"
 
@@ -1176,9 +1177,14 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipEventRecord(E->evx[2], E->st2));
         HC(hipEventRecord(E->evx[10], E->st2));
         // the ordered loop with LDS-resident signal state (RS_NO_LDS_HEAD: k_big_main<512>, diagnostic)
-        static const bool no_lds = getenv("RS_NO_LDS_HEAD") != nullptr;
-        if (no_lds) hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        else hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        // (RS_HEAD_KERNEL=lds: the one-wave k_big_main_lds; =plain: k_big_main<512>; diagnostics)
+        static const char *hk = getenv("RS_HEAD_KERNEL");
+        static const int spec_nw = getenv("RS_SPEC_NW") ? atoi(getenv("RS_SPEC_NW")) : 8;
+        if (hk && !strcmp(hk, "plain")) hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        else if (hk && !strcmp(hk, "lds")) hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        else if (spec_nw == 16) hipLaunchKernelGGL(k_big_spec<16>, dim3(g), dim3(1024), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        else if (spec_nw == 4) hipLaunchKernelGGL(k_big_spec<4>, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        else hipLaunchKernelGGL(k_big_spec<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
         hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);

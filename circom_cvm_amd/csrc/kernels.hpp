@@ -1303,7 +1303,14 @@ __device__ inline bool d_treat_scalar(const ElimArgs &A, Alloc &al, uint64_t b, 
   }
 }
 
-// exclusive scan of a[0..n) (LDS) by one 64-lane workgroup; returns the total
+// LDS barrier of ONE wave (the workgroup barrier of a 64-lane workgroup, and what a single wave of a
+// larger workgroup runs the same code with: d_big_main_cluster, wave_excl_scan)
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// exclusive scan of a[0..n) (LDS) by one 64-lane wave; returns the total
 __device__ inline uint32_t wave_excl_scan(uint32_t *a, uint32_t n) {
   const uint32_t lane = threadIdx.x;
   uint32_t per = (n + 63) / 64, lo = min(n, lane * per), hi = min(n, lo + per);
@@ -1318,7 +1325,9 @@ __device__ inline uint32_t wave_excl_scan(uint32_t *a, uint32_t n) {
   uint32_t acc = x - sum;
   for (uint32_t i = lo; i < hi; ++i) { uint32_t t = a[i]; a[i] = acc; acc += t; }
   uint32_t total = __shfl(x, 63);
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   return total;
 }
 // Per-signal state of a work-list entry, loaded once when the entry enters the list: a row's
@@ -1412,7 +1421,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
 #endif
     t_1 = prof ? wall_clock64() : 0ull;
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
-    __syncthreads();
+    wave_sync_lds();
     const uint32_t n_loop = A.big_alive[ci];
     uint64_t nx_off = n_loop ? A.row_off[b + n_loop - 1] : 0;  // descriptor of the next row, one ahead
     uint32_t nx_len = n_loop ? A.row_len[b + n_loop - 1] : 0;
@@ -1431,14 +1440,14 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
         if (!A.forb[s] && A.occ[s] >= 0) A.occ[s]--;
       }
       if (len > kBigCap) {
-        __syncthreads();
+        wave_sync_lds();
         if (tid == 0) {
           uint32_t m = s_m, nl = s_nl;
           if (!d_treat_scalar(A, al0, b, k, v, len, m, nl, p4)) s_ok = 0;
           s_m = m;
           s_nl = nl;
         }
-        __syncthreads();
+        wave_sync_lds();
         continue;
       }
       for (uint32_t i = tid; i < len; i += nt) {
@@ -1449,7 +1458,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
       }
       uint32_t cur = 0;
       bool st_ok = true;  // ws[cur] holds the states of wk[cur]
-      __syncthreads();
+      wave_sync_lds();
       tp_row += clk() - tp_r0;
       while (len > 0) {
         tp_x = clk();
@@ -1488,7 +1497,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           }
         } else {
           if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
-          __syncthreads();
+          wave_sync_lds();
           for (uint32_t i = tid; i < len; i += nt) {
             uint32_t s = wk[cur][i];
             if (A.forb[s]) continue;
@@ -1498,7 +1507,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
             if (o < 0) { atomicOr(A.err, 16); o = 0; }
             atomicMin(&s_best, ((unsigned long long)(uint32_t)o << 32) | (0xffffffffu - i));  // sorted keys
           }
-          __syncthreads();
+          wave_sync_lds();
           const uint32_t fdel = s_fdel;
           const unsigned long long best = s_best;
           if (fdel != RS_NONE || best != ~0ull) {
@@ -1509,14 +1518,14 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
         }
         if (oi == RS_NONE) {  // nothing takeable: leftover
           if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
-          __syncthreads();
+          wave_sync_lds();
           by += 36ull * len;
           if (s_ok) {
             const uint64_t o = s_o;
             for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
             if (tid == 0) { A.l_off[b + s_nl] = o; A.l_len[b + s_nl] = len; s_nl = s_nl + 1; }
           }
-          __syncthreads();
+          wave_sync_lds();
           break;
         }
         const uint32_t p = wk[cur][oi];
@@ -1526,7 +1535,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           const uint32_t mm = len - 1 + sh;
           by += 36ull * mm;
           if (tid == 0) { s_o = pool_alloc(A, al0, mm); if (s_o == RS_NONE) s_ok = 0; }
-          __syncthreads();
+          wave_sync_lds();
           if (s_ok) {
             const uint64_t o = s_o;
             for (uint32_t i = tid; i < len; i += nt) {
@@ -1543,7 +1552,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
               A.del[p] = 1;
             }
           }
-          __syncthreads();
+          wave_sync_lds();
           tp_new += clk() - tn0;
           break;
         }
@@ -1557,11 +1566,11 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
         mwork += len + rl;
         if (rl > kBigCap || len + rl > kBigCap + 1) {  // spill, finish the row on lane 0
           if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
-          __syncthreads();
+          wave_sync_lds();
           if (s_ok) {
             const uint64_t o = s_o;
             for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
-            __syncthreads();
+            wave_sync_lds();
             if (tid == 0) {
               uint32_t m = s_m, nl = s_nl;
               if (!d_treat_scalar(A, al0, b, A.pk + o, A.pv + o, len, m, nl, p4)) s_ok = 0;
@@ -1569,7 +1578,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
               s_nl = nl;
             }
           }
-          __syncthreads();
+          wave_sync_lds();
           break;
         }
         { unsigned long long t = clk(); tp_hold += t - tp_x; tp_x = t; }
@@ -1652,7 +1661,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           if (l < len) wval = fmul256(F, c2, wval);   // one product per entry, both lists at once
           if (l < rl) rval = fmul256(F, coef, rval);
           if (l < rl) { rk[l] = rkey; rv[l] = rval; }
-          __syncthreads();
+          wave_sync_lds();
           bool keep_w = false, keep_r = false;
           uint32_t lb_w = 0, lb_r = 0;
           if (l < len && l != oi) {  // -c2*v (+ coef*rv when the RHS has the key)
@@ -1679,7 +1688,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
             wk[nx][q] = rkey;
             wv[nx][q] = rval;
           }
-          __syncthreads();
+          wave_sync_lds();
           const uint32_t nlen = (uint32_t)(__popcll(wmk) + __popcll(rmk));
           cur = nx;
           st_ok = false;
@@ -1689,13 +1698,13 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           continue;
         }
         for (uint32_t j = tid; j < rl; j += nt) { rk[j] = A.pk[roff + j]; rv[j] = A.pv[roff + j]; }
-        __syncthreads();
+        wave_sync_lds();
         // one product per entry, all lanes at once: work entries c2*v, RHS entries coef*rv
         for (uint32_t q = tid; q < len + rl; q += nt) {
           if (q < len) wv[cur][q] = fmul256(F, c2, wv[cur][q]);
           else rv[q - len] = fmul256(F, coef, rv[q - len]);
         }
-        __syncthreads();
+        wave_sync_lds();
         for (uint32_t i = tid; i < len; i += nt) {  // work keys: -c2*v (+ coef*rv when the RHS has the key)
           if (i == oi) { fw[i] = 0; continue; }
           const uint32_t key = wk[cur][i];
@@ -1713,7 +1722,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           lbr[j] = lb;
           fr[j] = fe_is_zero(rv[j]) ? 0 : 1;
         }
-        __syncthreads();
+        wave_sync_lds();
         const uint32_t tw = wave_excl_scan(fw, len);
         const uint32_t tr = wave_excl_scan(fr, rl);
         for (uint32_t i = tid; i < len; i += nt) {
@@ -1730,7 +1739,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
           wk[nx][q] = rk[j];
           wv[nx][q] = rv[j];
         }
-        __syncthreads();
+        wave_sync_lds();
         cur = nx;
         st_ok = false;
         by += 36ull * (len + rl + tw + tr);
@@ -1755,7 +1764,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
         (void)merges; (void)mwork;
       }
     }
-    __syncthreads();
+    wave_sync_lds();
   }
 }
 template <uint32_t CAP>

@@ -41,6 +41,16 @@
 #include <thread>
 #include <vector>
 
+// Optional instrumentation of the ordered loop (tools/elim_trace.cpp defines these; no-ops here).
+#ifndef RC_TRACE_CLUSTER
+#define RC_TRACE_CLUSTER(n_rows, n_uniq)
+#define RC_TRACE_ROW(len)
+#define RC_TRACE_MERGE(key, wlen, hidx, hlen)
+#define RC_TRACE_INSERT(key, hidx, len)
+#define RC_TRACE_LEFT(len)
+#define RC_TRACE_END()
+#endif
+
 namespace refcpu {
 
 struct Term {
@@ -430,6 +440,7 @@ static void process_4(Ctx &X, std::vector<Map> &vec, Simplified &res) {
   for (size_t i = 0; i < touched.size(); ++i)
     if (X.occ[touched[i]] == 1) uniques.push_back({touched[i], (uint32_t)repv[i]});
   std::sort(uniques.begin(), uniques.end());
+  RC_TRACE_CLUSTER(vec.size(), uniques.size());
   auto remove_constraint = [&](const Map &c) {
     for (const Term &t : c)
       if (!X.forbidden[t.k] && X.occ[t.k] >= 0) X.occ[t.k]--;
@@ -451,12 +462,14 @@ static void process_4(Ctx &X, std::vector<Map> &vec, Simplified &res) {
     actual.swap(vec[u.second]);
     remove_constraint(actual);
     clear_nn(F, actual, u.first, coef, to);
+    RC_TRACE_INSERT(u.first, H.sig.size(), to.size());
     insert(u.first, coef, to);
   }
   while (!vec.empty()) {
     work.swap(vec.back());
     vec.pop_back();
     remove_constraint(work);
+    RC_TRACE_ROW(work.size());
     for (;;) {
       if (work.empty()) break;
       // take_signal_4 (simplification_utils.rs:379-411), HashMap order := ascending
@@ -470,13 +483,15 @@ static void process_4(Ctx &X, std::vector<Map> &vec, Simplified &res) {
         if (occ_ret < 0 || n < occ_ret) { ret = t.k; occ_ret = n; }
         else if (n == occ_ret && ret < (int64_t)t.k) ret = t.k;
       }
-      if (ret < 0) { res.lconst.push_back(work); break; }
+      if (ret < 0) { RC_TRACE_LEFT(work.size()); res.lconst.push_back(work); break; }
       clear_nn(F, work, (uint32_t)ret, coef, to);
       int32_t hi = X.holder_idx[ret];
-      if (hi < 0) { insert((uint32_t)ret, coef, to); break; }
+      if (hi < 0) { RC_TRACE_INSERT((uint32_t)ret, H.sig.size(), to.size()); insert((uint32_t)ret, coef, to); break; }
+      RC_TRACE_MERGE((uint32_t)ret, work.size(), hi, H.to[hi].size());
       merge_conflict(F, coef, to, H.coef[hi], H.to[hi], work);
     }
   }
+  RC_TRACE_END();
   for (uint32_t s : touched) X.occ[s] = -1;
   for (uint32_t s : order) X.del[s] = 0;
   normalize_and_compose(X, H, &order, res);

@@ -19,6 +19,7 @@ CONFIGS = {  # name: (kind, rows, seed, prime)
     "chain1.5M": (2, 1_500_000, 3, "bn128"),
     "mixed10M": (0, 10_000_000, 42, "bn128"),
     "bls20M": (0, 20_000_000, 42, "bls12381"),
+    "templated10M": (5, 10_000_000, 42, "bn128"),
 }
 
 ap = argparse.ArgumentParser()
