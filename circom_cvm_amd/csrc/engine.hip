@@ -1130,6 +1130,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     // time is the critical path of the largest cluster, and everything else overlaps it.
     const uint64_t n_head = std::min<uint64_t>(n_big, head_limit()), n_tail = n_big - n_head;
     a.wide = 1;       // the head's largest process_4 clusters go through the k_wide_* grid
+    a.skip = nullptr;
     ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
     at.wide = 0;
     at.bytes_main = a.bytes + 3;
@@ -1182,7 +1183,6 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         static const int spec_nw = getenv("RS_SPEC_NW") ? atoi(getenv("RS_SPEC_NW")) : 8;
         if (hk && !strcmp(hk, "plain")) hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         else if (hk && !strcmp(hk, "lds")) hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        else if (spec_nw == 16) hipLaunchKernelGGL(k_big_spec<16>, dim3(g), dim3(1024), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         else if (spec_nw == 4) hipLaunchKernelGGL(k_big_spec<4>, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         else hipLaunchKernelGGL(k_big_spec<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -1207,6 +1207,14 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[10], 0));
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
+        // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast)
+        static const bool no_p3_fast = getenv("RS_NO_P3_FAST") != nullptr;
+        if (!no_p3_fast) {
+          at.skip = E->A.get<uint8_t>("el.skip", n_tail);
+          HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
+          hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
+          HC(hipGetLastError());
+        }
         HC(hipEventRecord(E->ev5, E->st));
         hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
@@ -1371,6 +1379,15 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 16); ++q)
           fprintf(stderr, " %llu:%.0f/%.0f", (unsigned long long)pf[kProfWords * q],
                   pf[kProfWords * q + 22] ? (pf[kProfWords * q + 22] - t0m) / 100.0 : -1.0, pf[kProfWords * q + 5] / 100.0);
+        fprintf(stderr, "\n");
+        // k_big_spec counters (spec_loop.hpp): rows, conflicts, rows on lane 0, merges kept / thrown
+        // away, turn time (of it: exact passes), turns that waited for their row's speculation
+        fprintf(stderr, "[rs-prof] head spec (rows conf serial merges redo | turn us exact us | late n us | wall us):");
+        for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 16); ++q) {
+          const unsigned long long *P = &pf[kProfWords * q];
+          fprintf(stderr, " [%llu %llu %llu %llu %llu | %.0f %.0f | %llu %.0f | %.0f]", P[2], P[8], P[9], P[10], P[11],
+                  P[12] / 100.0, P[13] / 100.0, P[14], P[15] / 100.0, P[5] / 100.0);
+        }
         fprintf(stderr, "\n");
       }
       std::vector<uint64_t> ix(n_big);

@@ -540,6 +540,7 @@ struct ElimArgs {
   uint64_t *row_off;          // per slot: (offset, length) of those rows in loop order (k_big_prep)
   uint32_t *row_len;
   int wide;                   // the k_wide_* kernels prepared this launch's largest p4 clusters
+  uint8_t *skip = nullptr;    // per cluster (launch order): k_p3_fast finished it, the ordered loop skips it
   // split composition (the head's clusters): k_big_finish only normalises and builds each cluster's
   // dependency DAG, k_compose_level composes one Kahn level of every cluster at a time over the
   // whole GPU, k_big_emit finishes
@@ -1253,6 +1254,104 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
   }
 }
 
+// ---- process_3 without a merge, row-parallel (substitution_process_3 / treat_constraint_3 /
+// take_signal_3, simplification_utils.rs:143-154, 259-294, 368-377).  A process_3 row's pivot is its
+// largest takeable key; it merges only if that key was already deleted, i.e. only if an earlier-popped
+// row has the same pivot.  When no two rows of a cluster share a pivot (checked here with one atomic
+// per row), the sequential loop makes every row with a takeable key a new substitution for its pivot
+// and every other row a leftover, in pop order -- which this kernel writes directly, every row at
+// once: slot = its rank among the pivot rows popped before it, leftover index likewise.  A cluster
+// with a shared pivot is left to the ordered loop (skip stays 0).  One workgroup per cluster, grid-
+// stride over the tail; the per-signal occurrence slots (unused by process_3, -1) count the pivots
+// and are reset.
+__global__ __launch_bounds__(256) void k_p3_fast(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  __shared__ uint32_t s_dirty, s_ph[256], s_pl[256];
+  __shared__ unsigned long long s_by;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  Alloc al;
+  al.chunk = 256;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b);
+    if (d_is_p4(A, n)) continue;
+    if (tid == 0) { s_dirty = 0; s_by = 0; }
+    __syncthreads();
+    for (uint32_t pos = tid; pos < n; pos += nt) {  // take_signal_3 of every row; shared pivots?
+      const uint64_t ro = A.row_off[b + pos];
+      const uint32_t rl = A.row_len[b + pos];
+      uint32_t mi = RS_NONE;
+      for (uint32_t i = rl; i-- > 0;)
+        if (!A.forb[A.rows.key[ro + i]]) { mi = i; break; }
+      A.tmp[b + pos] = mi;
+      if (mi != RS_NONE && atomicAdd(&A.occ[A.rows.key[ro + mi]], 1) != -1) s_dirty = 1;
+    }
+    __syncthreads();
+    for (uint32_t pos = tid; pos < n; pos += nt) {
+      const uint32_t mi = A.tmp[b + pos];
+      if (mi != RS_NONE) A.occ[A.rows.key[A.row_off[b + pos] + mi]] = -1;
+    }
+    const bool dirty = s_dirty != 0;
+    __syncthreads();
+    if (dirty) continue;
+    // ranks in pop order (descending position): per thread a contiguous segment, segments scanned
+    // from the last thread down
+    const uint32_t per = (n + nt - 1) / nt, lo = min(n, tid * per), hi = min(n, lo + per);
+    uint32_t ch = 0, cl = 0;
+    for (uint32_t pos = lo; pos < hi; ++pos) {
+      if (A.tmp[b + pos] != RS_NONE) ++ch;
+      else ++cl;
+    }
+    s_ph[tid] = ch;
+    s_pl[tid] = cl;
+    __syncthreads();
+    uint32_t rh = 0, rlft = 0, th = 0, tl = 0;
+    for (uint32_t q = 0; q < nt; ++q) {
+      if (q > tid) { rh += s_ph[q]; rlft += s_pl[q]; }
+      th += s_ph[q];
+      tl += s_pl[q];
+    }
+    unsigned long long by = 0;
+    bool ok = true;
+    for (uint32_t pos = hi; pos-- > lo;) {
+      const uint64_t ro = A.row_off[b + pos];
+      const uint32_t len = A.row_len[b + pos];
+      const uint32_t *k = A.rows.key + ro;
+      const Fe *v = A.rows.val + ro;
+      const uint32_t mi = A.tmp[b + pos];
+      by += 36ull * len;
+      if (mi != RS_NONE) {  // clear_signal_not_normalized: a new substitution, slot = its pop rank
+        Fe coef;
+        uint64_t to_off;
+        uint32_t to_len;
+        if (!d_clear_nn(A, al, k, v, len, mi, coef, to_off, to_len)) { ok = false; continue; }
+        d_set_holder(A, k[mi], b + rh, coef, to_off, to_len);
+        A.del[k[mi]] = 1;
+        by += 36ull * to_len;
+        ++rh;
+      } else {  // nothing takeable: leftover, as popped
+        const uint64_t o = pool_alloc(A, al, len);
+        if (o == RS_NONE) { ok = false; continue; }
+        for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
+        A.l_off[b + rlft] = o;
+        A.l_len[b + rlft] = len;
+        by += 36ull * len;
+        ++rlft;
+      }
+    }
+    if (!ok) atomicOr(A.err, 8);
+    atomicAdd(&s_by, by);
+    __syncthreads();
+    if (tid == 0) {
+      A.n_sub[c] = th;
+      A.n_left[c] = tl;
+      A.skip[ci] = 1;
+      atomicAdd(A.bytes_main, s_by);
+    }
+    __syncthreads();
+  }
+}
+
 // The rest of one row's treat_constraint_3/4 loop on a work list in the pool (single lane; used
 // when a list does not fit the LDS buffers of k_big_main).
 __device__ inline bool d_treat_scalar(const ElimArgs &A, Alloc &al, uint64_t b, const uint32_t *k, const Fe *v,
@@ -1419,6 +1518,7 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
 #else
     auto clk = []() -> unsigned long long { return 0ull; };
 #endif
+    if (A.skip && A.skip[ci]) return;  // k_p3_fast did this cluster's loop
     t_1 = prof ? wall_clock64() : 0ull;
     if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
     wave_sync_lds();

@@ -44,6 +44,7 @@
 // Optional instrumentation of the ordered loop (tools/elim_trace.cpp defines these; no-ops here).
 #ifndef RC_TRACE_CLUSTER
 #define RC_TRACE_CLUSTER(n_rows, n_uniq)
+#define RC_TRACE_CLUSTER3(n_rows)
 #define RC_TRACE_ROW(len)
 #define RC_TRACE_MERGE(key, wlen, hidx, hlen)
 #define RC_TRACE_INSERT(key, hidx, len)
@@ -399,18 +400,22 @@ static void process_3(Ctx &X, std::vector<Map> &cons, Simplified &res) {
   Holder H;
   Map to, work;
   Fe coef;
+  RC_TRACE_CLUSTER3(cons.size());
   while (!cons.empty()) {
     work.swap(cons.back());
     cons.pop_back();
+    RC_TRACE_ROW(work.size());
     for (;;) {
       if (work.empty()) break;
       int64_t out = -1;
       for (size_t i = work.size(); i-- > 0;)
         if (!X.forbidden[work[i].k]) { out = work[i].k; break; }
-      if (out < 0) { res.lconst.push_back(work); break; }
+      if (out < 0) { RC_TRACE_LEFT(work.size()); res.lconst.push_back(work); break; }
       clear_nn(F, work, (uint32_t)out, coef, to);
       int32_t hi = X.holder_idx[out];
+      if (hi >= 0) RC_TRACE_MERGE((uint32_t)out, work.size(), hi, H.to[hi].size());
       if (hi < 0) {
+        RC_TRACE_INSERT((uint32_t)out, H.sig.size(), to.size());
         X.holder_idx[out] = (int32_t)H.sig.size();
         H.sig.push_back((uint32_t)out);
         H.coef.push_back(coef);
@@ -420,6 +425,7 @@ static void process_3(Ctx &X, std::vector<Map> &cons, Simplified &res) {
       merge_conflict(F, coef, to, H.coef[hi], H.to[hi], work);
     }
   }
+  RC_TRACE_END();
   normalize_and_compose(X, H, nullptr, res);
 }
 

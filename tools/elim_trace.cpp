@@ -20,7 +20,8 @@ struct Cl {
   std::set<uint32_t> row_keys;           // keys of the popped row (before any merge)
   size_t cur_merges = 0;
   std::map<size_t, size_t> merges_per_row, age_hist, hlen_hist, wlen_hist, sum_hist;
-  size_t over64 = 0, max_sum = 0, max_row = 0, nonempty_rows = 0;
+  size_t over64 = 0, max_sum = 0, max_row = 0, nonempty_rows = 0, over128 = 0, len_over64 = 0;
+  bool p3 = false, agg = false;
   size_t from_row = 0, introduced = 0, uniq_holder = 0, sum_h = 0, sum_w = 0, max_chain = 0;
   // speculation distance: non-empty loop rows back to the latest row whose pivot this row's work saw
   std::map<uint32_t, long> del_at;       // signal -> non-empty loop row index that deleted it
@@ -40,14 +41,26 @@ struct Cl {
 };
 thread_local Cl C;
 size_t g_min = 2000;
+size_t g_tail_min = 32;  // clusters in [g_tail_min, g_min): one aggregate line (the "tail")
+struct Agg { size_t clusters = 0, rows = 0, merges = 0, over64 = 0, over128 = 0, len_over64 = 0; std::map<size_t, size_t> sum_hist; };
+Agg g_agg[2];  // [0] process_4, [1] process_3
 std::mutex g_mu;
 inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; return b; }
 }  // namespace tr
 
+#define RC_TRACE_CLUSTER3(n_rows)                                                   \
+  do {                                                                              \
+    tr::C = tr::Cl();                                                               \
+    tr::C.p3 = true;                                                                \
+    tr::C.agg = (n_rows) >= tr::g_tail_min;                                         \
+    tr::C.on = tr::C.agg;                                                           \
+    tr::C.rows = (n_rows);                                                          \
+  } while (0)
 #define RC_TRACE_CLUSTER(n_rows, n_uniq)                                            \
   do {                                                                              \
     tr::C = tr::Cl();                                                               \
-    tr::C.on = (n_rows) >= tr::g_min;                                               \
+    tr::C.agg = (n_rows) >= tr::g_tail_min && (n_rows) < tr::g_min;                 \
+    tr::C.on = (n_rows) >= tr::g_tail_min;                                          \
     tr::C.rows = (n_rows);                                                          \
     tr::C.uniq = (n_uniq);                                                          \
   } while (0)
@@ -56,7 +69,8 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
     if (!tr::C.on) break;                                                           \
     if (tr::C.row_i) { tr::C.merges_per_row[tr::C.cur_merges]++; }                  \
     if (!work.empty()) { tr::C.row_end(); tr::C.ne_i++; tr::C.dep = -1; tr::C.nonempty_rows++; \
-      tr::C.max_row = std::max<size_t>(tr::C.max_row, work.size()); }               \
+      tr::C.max_row = std::max<size_t>(tr::C.max_row, work.size());                 \
+      if (work.size() > 64) tr::C.len_over64++; }                                   \
     tr::C.max_chain = std::max(tr::C.max_chain, tr::C.cur_merges);                  \
     tr::C.cur_merges = 0;                                                           \
     tr::C.row_i++;                                                                  \
@@ -76,6 +90,7 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
     tr::C.wlen_hist[tr::bucket(wlen)]++;                                            \
     tr::C.sum_hist[tr::bucket((wlen) + (hl))]++;                                    \
     if ((wlen) + (hl) > 65) tr::C.over64++;                                         \
+    if ((wlen) + (hl) > 129) tr::C.over128++;                                       \
     tr::C.max_sum = std::max<size_t>(tr::C.max_sum, (wlen) + (hl));                 \
     tr::C.sum_h += (hl);                                                            \
     tr::C.sum_w += (wlen);                                                          \
@@ -96,6 +111,15 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
 #define RC_TRACE_END()                                                              \
   do {                                                                              \
     if (!tr::C.on) break;                                                           \
+    if (tr::C.agg) {                                                                \
+      std::lock_guard<std::mutex> lk_(tr::g_mu);                                    \
+      tr::Agg &a_ = tr::g_agg[tr::C.p3 ? 1 : 0];                                    \
+      a_.clusters++; a_.rows += tr::C.nonempty_rows; a_.merges += tr::C.merges;     \
+      a_.over64 += tr::C.over64; a_.over128 += tr::C.over128;                       \
+      a_.len_over64 += tr::C.len_over64;                                            \
+      for (auto &kv : tr::C.sum_hist) a_.sum_hist[kv.first] += kv.second;           \
+      break;                                                                        \
+    }                                                                               \
     tr::C.merges_per_row[tr::C.cur_merges]++;                                       \
     tr::C.row_end();                                                                \
     std::lock_guard<std::mutex> lk_(tr::g_mu);                                      \
@@ -137,5 +161,12 @@ int main(int argc, char **argv) {
   rs_output *out = nullptr;
   int rc = refcpu_simplify(in, &fl, 8, &out, nullptr, nullptr);
   printf("rc=%d\n", rc);
+  for (int q = 0; q < 2; ++q) {
+    const tr::Agg &a = tr::g_agg[q];
+    printf("tail %s: clusters=%zu rows=%zu merges=%zu len+rl>64: %zu  >128: %zu  rows>64: %zu  len+rl(log2):", q ? "p3" : "p4",
+           a.clusters, a.rows, a.merges, a.over64, a.over128, a.len_over64);
+    for (auto &kv : a.sum_hist) printf(" %zu:%zu", kv.first, kv.second);
+    printf("\n");
+  }
   return rc;
 }
