@@ -1209,15 +1209,32 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast)
         static const bool no_p3_fast = getenv("RS_NO_P3_FAST") != nullptr;
-        if (!no_p3_fast) {
+        static const bool p3_verify = getenv("RS_P3_VERIFY") != nullptr;
+        if (p3_verify) {  // diagnostic: the fast path's pivots checked against the ordered loop's
+          at.skip = E->A.get<uint8_t>("el.skip", n_tail);
+          at.p3_shadow = E->A.get<uint32_t>("el.p3_shadow", n_slots);
+          HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
+          hipLaunchKernelGGL(k_p3_shadow, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
+          HC(hipGetLastError());
+        } else if (!no_p3_fast) {
           at.skip = E->A.get<uint8_t>("el.skip", n_tail);
           HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
           hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
           HC(hipGetLastError());
         }
         HC(hipEventRecord(E->ev5, E->st));
-        hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
-        HC(hipGetLastError());
+        {
+          ElimArgs am = at;
+          if (p3_verify) am.skip = nullptr;  // the ordered loop does every cluster, then the check
+          hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, am, ids, n_tail);
+          HC(hipGetLastError());
+          if (p3_verify) {
+            unsigned int *nb = E->A.get<unsigned int>("el.p3_bad", 1);
+            HC(hipMemsetAsync(nb, 0, 4, E->st));
+            launch(E->st, k_p3_check, n_tail, at, ids, n_tail, nb);
+            HC(hipStreamSynchronize(E->st));
+          }
+        }
         HC(hipEventRecord(E->ev6, E->st));
         {  // tail clusters flagged in cls, then one inversion per 64 slots across clusters
           uint8_t *cls = E->A.get<uint8_t>("el.cls", eo.n_clusters);

@@ -541,6 +541,7 @@ struct ElimArgs {
   uint32_t *row_len;
   int wide;                   // the k_wide_* kernels prepared this launch's largest p4 clusters
   uint8_t *skip = nullptr;    // per cluster (launch order): k_p3_fast finished it, the ordered loop skips it
+  uint32_t *p3_shadow = nullptr;  // RS_P3_VERIFY diagnostic: k_p3_fast's pivots per slot, checked after the loop
   // split composition (the head's clusters): k_big_finish only normalises and builds each cluster's
   // dependency DAG, k_compose_level composes one Kahn level of every cluster at a time over the
   // whole GPU, k_big_emit finishes
@@ -588,13 +589,25 @@ __device__ __forceinline__ uint64_t pool_alloc(const ElimArgs &A, Alloc &al, uin
 // Every substitution created before or inside the ordered loop is preceded in the pool by a header
 // entry (key = RHS length, value = the coefficient): k_big_main_lds reads a holder's header and its
 // right-hand side in one round trip.
+__device__ __forceinline__ uint32_t d_clear_nn_len(const uint32_t *k, uint32_t n, uint32_t oi) {  // RHS entries
+  const bool has0 = n > 0 && k[0] == 0 && oi != 0;
+  return n - 1 + (has0 ? 0 : 1);
+}
+__device__ inline void d_clear_nn_at(const ElimArgs &A, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
+                                     uint64_t o, Fe &coef, uint64_t &to_off, uint32_t &to_len);
 __device__ inline bool d_clear_nn(const ElimArgs &A, Alloc &al, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
                                   Fe &coef, uint64_t &to_off, uint32_t &to_len) {
-  coef = fneg(A.F, v[oi]);
-  bool has0 = n > 0 && k[0] == 0 && oi != 0;
-  uint32_t m = n - 1 + (has0 ? 0 : 1);
-  uint64_t o = pool_alloc(A, al, (uint64_t)m + 1);
+  const uint64_t o = pool_alloc(A, al, (uint64_t)d_clear_nn_len(k, n, oi) + 1);
   if (o == RS_NONE) return false;
+  d_clear_nn_at(A, k, v, n, oi, o, coef, to_off, to_len);
+  return true;
+}
+// the same at a given pool offset o (header at o, the RHS from o + 1)
+__device__ inline void d_clear_nn_at(const ElimArgs &A, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
+                                     uint64_t o, Fe &coef, uint64_t &to_off, uint32_t &to_len) {
+  coef = fneg(A.F, v[oi]);
+  const bool has0 = n > 0 && k[0] == 0 && oi != 0;
+  const uint32_t m = n - 1 + (has0 ? 0 : 1);
   A.pk[o] = m;
   A.pv[o] = coef;
   ++o;
@@ -604,7 +617,6 @@ __device__ inline bool d_clear_nn(const ElimArgs &A, Alloc &al, const uint32_t *
     if (i != oi) { A.pk[o + w] = k[i]; A.pv[o + w] = v[i]; ++w; }
   to_off = o;
   to_len = m;
-  return true;
 }
 // treat_constraint_3/4 conflict: work = coef*R - c2*L, zeros dropped; L = row minus key (+{0:0}).
 __device__ inline bool d_merge(const ElimArgs &A, Alloc &al, const uint32_t *k, const Fe *v, uint32_t n, uint32_t oi,
@@ -1266,10 +1278,9 @@ __global__ __launch_bounds__(256) void k_big_prep(ElimArgs A, const uint32_t *id
 // and are reset.
 __global__ __launch_bounds__(256) void k_p3_fast(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
   __shared__ uint32_t s_dirty, s_ph[256], s_pl[256];
+  __shared__ uint64_t s_pz[256], s_base;
   __shared__ unsigned long long s_by;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  Alloc al;
-  al.chunk = 256;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
@@ -1294,25 +1305,39 @@ __global__ __launch_bounds__(256) void k_p3_fast(ElimArgs A, const uint32_t *ids
     const bool dirty = s_dirty != 0;
     __syncthreads();
     if (dirty) continue;
-    // ranks in pop order (descending position): per thread a contiguous segment, segments scanned
-    // from the last thread down
+    // ranks in pop order (descending position) and the pool space of every row: per thread a
+    // contiguous segment, segments counted from the last thread down; one allocation per cluster
     const uint32_t per = (n + nt - 1) / nt, lo = min(n, tid * per), hi = min(n, lo + per);
     uint32_t ch = 0, cl = 0;
+    uint64_t cz = 0;
     for (uint32_t pos = lo; pos < hi; ++pos) {
-      if (A.tmp[b + pos] != RS_NONE) ++ch;
-      else ++cl;
+      const uint32_t mi = A.tmp[b + pos], len = A.row_len[b + pos];
+      if (mi != RS_NONE) {
+        ++ch;
+        cz += 1 + d_clear_nn_len(A.rows.key + A.row_off[b + pos], len, mi);
+      } else if (len) {
+        ++cl;
+        cz += len;
+      }
     }
     s_ph[tid] = ch;
     s_pl[tid] = cl;
+    s_pz[tid] = cz;
     __syncthreads();
     uint32_t rh = 0, rlft = 0, th = 0, tl = 0;
+    uint64_t oz = 0, tz = 0;
     for (uint32_t q = 0; q < nt; ++q) {
-      if (q > tid) { rh += s_ph[q]; rlft += s_pl[q]; }
+      if (q > tid) { rh += s_ph[q]; rlft += s_pl[q]; oz += s_pz[q]; }
       th += s_ph[q];
       tl += s_pl[q];
+      tz += s_pz[q];
     }
+    if (tid == 0) s_base = pool_alloc_global(A, tz);
+    __syncthreads();
+    const uint64_t base = s_base;
+    if (base == RS_NONE) continue;  // pool exhausted (err 8 set, the run is retried): left to the loop
+    uint64_t o = base + oz;
     unsigned long long by = 0;
-    bool ok = true;
     for (uint32_t pos = hi; pos-- > lo;) {
       const uint64_t ro = A.row_off[b + pos];
       const uint32_t len = A.row_len[b + pos];
@@ -1324,22 +1349,21 @@ __global__ __launch_bounds__(256) void k_p3_fast(ElimArgs A, const uint32_t *ids
         Fe coef;
         uint64_t to_off;
         uint32_t to_len;
-        if (!d_clear_nn(A, al, k, v, len, mi, coef, to_off, to_len)) { ok = false; continue; }
+        d_clear_nn_at(A, k, v, len, mi, o, coef, to_off, to_len);
         d_set_holder(A, k[mi], b + rh, coef, to_off, to_len);
         A.del[k[mi]] = 1;
         by += 36ull * to_len;
+        o += 1 + to_len;
         ++rh;
-      } else {  // nothing takeable: leftover, as popped
-        const uint64_t o = pool_alloc(A, al, len);
-        if (o == RS_NONE) { ok = false; continue; }
+      } else if (len) {  // nothing takeable: leftover, as popped (an empty row is dropped, :267)
         for (uint32_t i = 0; i < len; ++i) { A.pk[o + i] = k[i]; A.pv[o + i] = v[i]; }
         A.l_off[b + rlft] = o;
         A.l_len[b + rlft] = len;
         by += 36ull * len;
+        o += len;
         ++rlft;
       }
     }
-    if (!ok) atomicOr(A.err, 8);
     atomicAdd(&s_by, by);
     __syncthreads();
     if (tid == 0) {
@@ -1349,6 +1373,65 @@ __global__ __launch_bounds__(256) void k_p3_fast(ElimArgs A, const uint32_t *ids
       atomicAdd(A.bytes_main, s_by);
     }
     __syncthreads();
+  }
+}
+// RS_P3_VERIFY diagnostic: the pivots k_p3_fast would give every row (pop order) into p3_shadow,
+// the clusters it would take flagged in skip (2); nothing else written
+__global__ __launch_bounds__(256) void k_p3_shadow(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  __shared__ uint32_t s_dirty;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b);
+    if (d_is_p4(A, n)) continue;
+    if (tid == 0) s_dirty = 0;
+    __syncthreads();
+    for (uint32_t pos = tid; pos < n; pos += nt) {
+      const uint64_t ro = A.row_off[b + pos];
+      const uint32_t rl = A.row_len[b + pos];
+      uint32_t m = RS_NONE;
+      for (uint32_t i = rl; i-- > 0;)
+        if (!A.forb[A.rows.key[ro + i]]) { m = A.rows.key[ro + i]; break; }
+      A.tmp[b + pos] = m;
+      if (m != RS_NONE && atomicAdd(&A.occ[m], 1) != -1) s_dirty = 1;
+    }
+    __syncthreads();
+    for (uint32_t pos = tid; pos < n; pos += nt)
+      if (A.tmp[b + pos] != RS_NONE) A.occ[A.tmp[b + pos]] = -1;
+    __syncthreads();
+    if (tid == 0 && !s_dirty) {
+      uint32_t r = 0;
+      for (uint32_t pos = n; pos-- > 0;)
+        if (A.tmp[b + pos] != RS_NONE) A.p3_shadow[b + r++] = A.tmp[b + pos];
+      A.skip[ci] = 2;
+    }
+    __syncthreads();
+  }
+}
+__global__ void k_p3_check(ElimArgs A, const uint32_t *ids, uint64_t n_ids, unsigned int *n_bad) {
+  for (uint64_t ci = gtid(); ci < n_ids; ci += gstride()) {
+    if (A.skip[ci] != 2) continue;
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+    const uint32_t n = (uint32_t)(e - b), m = A.n_sub[c];
+    uint32_t cnt = 0;
+    for (uint32_t pos = 0; pos < n; ++pos) cnt += A.tmp[b + pos] != RS_NONE;
+    bool bad = cnt != m;
+    uint32_t at = 0;
+    for (uint32_t i = 0; !bad && i < m; ++i)
+      if (A.h_sig[b + i] != A.p3_shadow[b + i]) { bad = true; at = i; }
+    if (!bad) continue;
+    if (atomicAdd(n_bad, 1u) >= 4) continue;
+    printf("[p3-verify] cluster %llu n %u subs %u shadow %u first diff slot %u: seq %u shadow %u\n",
+           (unsigned long long)c, n, m, cnt, at, at < m ? A.h_sig[b + at] : 0u, A.p3_shadow[b + at]);
+    for (uint32_t pos = n; pos-- > 0 && pos + 12 > n;) {
+      const uint64_t ro = A.row_off[b + pos];
+      const uint32_t rl = A.row_len[b + pos];
+      printf("[p3-verify]   row pos %u len %u:", pos, rl);
+      for (uint32_t i = 0; i < rl && i < 10; ++i) printf(" %u%s", A.rows.key[ro + i], A.forb[A.rows.key[ro + i]] ? "F" : "");
+      printf("\n");
+    }
   }
 }
 

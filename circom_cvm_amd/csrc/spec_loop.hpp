@@ -57,11 +57,19 @@ __device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) {
 __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// Ordered LDS accesses between the waves of the workgroup.  The LDS performs one wave's accesses in
+// issue order, so only the compiler must not reorder them -- a seq_cst atomic would also make the
+// wave wait for its outstanding global stores (s_waitcnt vmcnt(0)), which the commit path avoids.
 __device__ __forceinline__ uint32_t lds_ld_sc(const uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  return v;
 }
 __device__ __forceinline__ void lds_st_sc(uint32_t *p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 // spin budget of any wait in the speculative loop (~1 s): past it the loop aborts with err bit 64
 // instead of hanging the device
@@ -209,7 +217,7 @@ __device__ __forceinline__ void sp_wait_visible(SpecSmem<NW> &S, uint32_t lane, 
     if (it > kSpecSpin || lds_ld(&S.s_abort)) { lds_st(&S.s_abort, 1); break; }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the holder's loads after the check (same CU: its L1)
 }
 // a holder's header and right-hand side staged in registers: entry i (0 = the header) in lane
 // i % 64 of register i / 64
@@ -349,7 +357,7 @@ __device__ __forceinline__ void sp_reduce(const ElimArgs &A, SpecSmem<NW> &S, ui
       if (cand != RS_NONE && (cst & kStDel)) {
         const uint32_t nho = cst & ~kStDel;
         if (sp_visible<NW>(S, lane, nho)) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
           sp_stage<E>(A, lane, nho, sk, sv);
           pf_ho = nho;
         }
@@ -669,14 +677,14 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
       const uint32_t okey = lane < olen ? A.rows.key[r_off + lane] : 0u;
       const uint32_t osl = lane < olen ? sp_find(S.tk, okey) : kTabEmpty;
       // ---- speculate
-      uint32_t c0 = rdlane(__hip_atomic_load(&S.s_turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+      uint32_t c0 = rdlane(lds_ld_sc(&S.s_turn), 0);
       sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R);
       // ---- wait for the turn, validating the commits that land meanwhile; a conflict found
       // before the turn is reduced again right away (against the newer state)
       bool conflict = false, first = true, late = false;
       for (uint32_t it = 0;; ++it) {
         if (it > kSpecSpin || lds_ld(&S.s_abort)) { lds_st(&S.s_abort, 1); break; }
-        const uint32_t sc = rdlane(__hip_atomic_load(&S.s_turn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+        const uint32_t sc = rdlane(lds_ld_sc(&S.s_turn), 0);
         if (!R.serial && !conflict && c0 < sc) conflict = sp_conflict<NW, 1>(S, wv, lane, R, c0, sc);
         c0 = sc;
         if (sc == j) { late = first; break; }

@@ -43,13 +43,13 @@
 
 // Optional instrumentation of the ordered loop (tools/elim_trace.cpp defines these; no-ops here).
 #ifndef RC_TRACE_CLUSTER
-#define RC_TRACE_CLUSTER(n_rows, n_uniq)
-#define RC_TRACE_CLUSTER3(n_rows)
-#define RC_TRACE_ROW(len)
-#define RC_TRACE_MERGE(key, wlen, hidx, hlen)
-#define RC_TRACE_INSERT(key, hidx, len)
-#define RC_TRACE_LEFT(len)
-#define RC_TRACE_END()
+#define RC_TRACE_CLUSTER(n_rows, n_uniq) do { } while (0)
+#define RC_TRACE_CLUSTER3(n_rows) do { } while (0)
+#define RC_TRACE_ROW(len) do { } while (0)
+#define RC_TRACE_MERGE(key, wlen, hidx, hlen) do { } while (0)
+#define RC_TRACE_INSERT(key, hidx, len) do { } while (0)
+#define RC_TRACE_LEFT(len) do { } while (0)
+#define RC_TRACE_END() do { } while (0)
 #endif
 
 namespace refcpu {
