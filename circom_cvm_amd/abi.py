@@ -6,6 +6,8 @@ GPU."""
 from __future__ import annotations
 
 import ctypes as C
+
+import numpy as np
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
@@ -43,7 +45,37 @@ class RsOutput(C.Structure):
     _fields_ = [("n_constraints", C.c_uint64), ("a", RsLc), ("b", RsLc), ("c", RsLc),
                 ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int32)),
                 ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64),
-                ("n_log", C.c_uint64), ("log_from", C.POINTER(C.c_uint32)), ("log_to", RsLc)]
+                ("n_log", C.c_uint64), ("log_from", C.POINTER(C.c_uint32)), ("log_to", RsLc),
+                ("a_end", C.POINTER(C.c_uint64)), ("b_end", C.POINTER(C.c_uint64)), ("c_end", C.POINTER(C.c_uint64))]
+
+    def block(self, q: int):
+        """(rs_lc, its row ends or None) of part q = 0/1/2 (a/b/c)."""
+        lc = (self.a, self.b, self.c)[q]
+        end = (self.a_end, self.b_end, self.c_end)[q]
+        return lc, (end if end else None)
+
+
+def block_csr(lc: "RsLc", end=None):
+    """Copies of one result block as compact CSR numpy arrays (ptr u64[n+1], col u32, val u64[4 nnz]):
+    a block with row ends (ABI 7, rs_engine_simplify's streamed layout) is compacted row by row."""
+    n = int(lc.n_rows)
+    if n == 0:
+        return np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint64)
+    beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,)).copy()
+    ext = int(lc.nnz)
+    col = np.ctypeslib.as_array(lc.col, shape=(max(ext, 1),))
+    val = np.ctypeslib.as_array(lc.val, shape=(max(ext, 1) * 4,))
+    if end is None:
+        nnz = int(beg[n])
+        return beg, col[:nnz].copy(), val[:4 * nnz].copy()
+    e = np.ctypeslib.as_array(end, shape=(n,)).astype(np.int64)
+    b = beg[:n].astype(np.int64)
+    lens = e - b
+    ptr = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=ptr[1:])
+    idx = np.repeat(b - ptr[:-1].astype(np.int64), lens) + np.arange(int(ptr[n]), dtype=np.int64)
+    v4 = val[: 4 * ext].reshape(-1, 4)
+    return ptr, col[idx].copy(), v4[idx].reshape(-1).copy()
 
 
 class RsStats(C.Structure):

@@ -64,7 +64,7 @@ int main(int argc, char **argv) {
   // constraint_writers/src/log_writer.rs:24-47
   uint64_t nl = 0, l = 0;
   for (uint64_t r = 0; r < o->n_constraints; ++r) {
-    bool lin = o->a.ptr[r] == o->a.ptr[r + 1] && o->b.ptr[r] == o->b.ptr[r + 1];
+    bool lin = o->a.ptr[r] == rs_row_end(&o->a, o->a_end, r) && o->b.ptr[r] == rs_row_end(&o->b, o->b_end, r);
     (lin ? l : nl)++;
   }
   printf("non-linear constraints: %llu\n", (unsigned long long)nl);

@@ -92,6 +92,29 @@ struct Arena {
     }
     return (T *)b.p;
   }
+  // grows `name` to n elements keeping its first `keep`: the producer stream `ps` is waited for,
+  // the kept part copied on `st`
+  template <class T>
+  void grow_keep(const std::string &name, size_t n, size_t keep, hipStream_t ps, hipStream_t st) {
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    B &b = bufs[name];
+    if (b.cap >= bytes) return;
+    const size_t cap = std::max(bytes, b.cap + b.cap / 4);
+    void *p = nullptr;
+    HC(hipMalloc(&p, cap));
+    if (b.p) {
+      HC(hipStreamSynchronize(ps));
+      if (keep) HC(hipMemcpyAsync(p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+      HC(hipStreamSynchronize(st));
+      HC(hipFree(b.p));
+    }
+    b.p = p;
+    b.cap = cap;
+  }
+  size_t cap_bytes(const std::string &name) {
+    auto it = bufs.find(name);
+    return it == bufs.end() ? 0 : it->second.cap;
+  }
   ~Arena() {
     for (auto &kv : bufs)
       if (kv.second.p) (void)hipFree(kv.second.p);
@@ -170,7 +193,7 @@ struct rs_engine {
   std::vector<HostCon> out_host_tail;  // lconst rows appended after the device rows
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr, ev6 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
   // sharded elimination: this engine is rank `comm->rank` of `comm->world`
   std::unique_ptr<rs::Comm> comm;
   // substitution log of the last run (rs_flags.emit_substitution_log), canonical values
@@ -191,16 +214,43 @@ struct rs_engine {
   int *h_vflag = nullptr;  // pinned: per-group verdicts [2g] row pointers, [2g + 1] rows; [8] linear keys unsorted
   bool staged = false;
   const rs_input *hin = nullptr;
-  unsigned long long *h_lvl = nullptr;  // pinned: frontier counts of the head's composition levels
-  hipEvent_t ev_lvl[4] = {};
+  unsigned long long *h_lvl = nullptr;  // pinned: frontier counts of the head's [0..3] / the tail's [4..7] composition levels
+  hipEvent_t ev_lvl[4] = {}, ev_lvlt[4] = {};  // frontier-count events of the head's / the tail's level loops
   double h2d_wait_ms = 0;
   // pinned result buffers of rs_engine_simplify (grow only) and the view handed out
   struct Pin {
     void *p = nullptr;
     size_t cap = 0;
   };
-  Pin pin[13];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers
+  Pin pin[16];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers;
+                // a/b/c row ends (streamed result)
   rs_output view{};
+  // streamed result (output.hpp; rs_engine_simplify): the storage rows final after round 1 go to
+  // pin[3..8] on the copy stream during the later rounds (ev_snap: their D2H is done)
+  bool stream_out = false;  // this run streams (set by rs_engine_simplify around engine_run)
+  bool snap_on = false;     // the early region was taken in this run
+  uint64_t snap_e[3] = {0, 0, 0};  // early-region entries per part
+  uint64_t out_ext[3] = {0, 0, 0};  // streamed layout: early + late entries per part
+  hipEvent_t ev_snap = nullptr, ev_snap0 = nullptr;  // early gather done / its inputs ready
+  // The early region's D2H runs on its own host thread, in chunks, one in flight at a time: the
+  // copy engine serves transfers in order, so one large transfer would hold every small D2H the run
+  // still issues (scan totals, flags, the head's frontier counts) behind it for ~15 ms.
+  struct SnapJob {
+    void *dst;
+    const void *src;
+    size_t bytes;
+  };
+  std::vector<SnapJob> snap_jobs;
+  std::thread snap_thread;
+  hipStream_t stx = nullptr;  // the early region's D2H stream
+  hipEvent_t ev_chunk[2] = {};
+  int snap_rc = 0;
+  // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
+  // when the streamed run skipped it
+  bool csr_ready = false;
+  DRows fin_parts[3] = {}, fin_lvq[3] = {};
+  const uint32_t *fin_keep_ids = nullptr, *fin_lv_ids = nullptr;
+  uint64_t fin_keep = 0, fin_lvn = 0;
 };
 
 namespace rs {
@@ -350,8 +400,10 @@ static void load_wait_all(rs_engine *E) {
   for (int g = 0; g < 4; ++g) load_wait(E, g);
 }
 // After a failed call: the copy stream may still be reading the caller's buffers.
+static void snap_join(rs_engine *E);
 static void load_abort(rs_engine *E) {
   if (E->stc) (void)hipStreamSynchronize(E->stc);
+  snap_join(E);
   for (bool &pd : E->pending) pd = false;
 }
 
@@ -398,6 +450,7 @@ static U3 excl_scan_u3(rs_engine *E, const U3 *in, U3 *out, uint64_t n, const ch
   return U3Plus()(li, lo);
 }
 #include "flatten.hpp"
+#include "output.hpp"
 __global__ void k_pack3(const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n, U3 *out) {
   for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = U3{a[i], b[i], c[i]};
 }
@@ -833,6 +886,47 @@ struct DevClusters {
   bool join_pending = false;
 };
 // the number of largest clusters eliminated on the second stream (RS_HEAD overrides)
+// Split composition (k_big_finish with ElimArgs.split, then one k_compose_level launch per Kahn
+// level of every cluster at once over the whole GPU, k_big_emit at the end).  Level L reads count
+// L%3, appends to (L+1)%3 and zeroes (L+2)%3 -- the one level L-1 read and level L+1 appends to --
+// and likewise alternates the deferred list's count: no memsets.  Every 4 levels the frontier count
+// goes to pinned slot h[b % 4]; with `check` the host reads the slot of two batches back (it never
+// waits for the level it just enqueued; launches past an empty frontier return at once).
+struct LevelLoop {
+  ElimArgs ah;
+  const uint32_t *ids = nullptr;
+  hipStream_t s = nullptr;
+  uint64_t *cur = nullptr, *nxt = nullptr;
+  uint64_t n_slots = 0;
+  unsigned long long *h = nullptr;
+  hipEvent_t *ev = nullptr;
+  uint32_t level = 0, levels = 0;
+  bool done = false;
+  void run(uint32_t upto, bool check) {
+    for (; !done && level <= n_slots + 1 && level < upto; ++level) {
+      ElimArgs al = ah;
+      al.cf_nbig = ah.cf_nbig + (level & 1);
+      unsigned long long *nc = ah.cf_n + level % 3, *zc = ah.cf_n + (level + 2) % 3;
+      unsigned long long *nn = ah.cf_n + (level + 1) % 3;
+      hipLaunchKernelGGL(k_compose_level<8>, dim3(256), dim3(512), 0, s, al, ids, (const uint64_t *)cur, (const unsigned long long *)nc,
+                         nxt, nn, level, zc, ah.cf_nbig + ((level + 1) & 1));
+      hipLaunchKernelGGL(k_compose_big, dim3(256), dim3(64), 0, s, al, ids, nxt, nn);
+      HC(hipGetLastError());
+      std::swap(cur, nxt);
+      levels = level + 1;
+      if (level % 4 == 3) {
+        const uint32_t b = level / 4;
+        HC(hipMemcpyAsync(h + b % 4, nn, 8, hipMemcpyDeviceToHost, s));
+        HC(hipEventRecord(ev[b % 4], s));
+        if (check && b >= 2) {
+          HC(hipEventSynchronize(ev[(b - 2) % 4]));
+          if (!h[(b - 2) % 4]) done = true;
+        }
+      }
+    }
+  }
+};
+
 static uint64_t head_limit() {
   static const uint64_t v = [] {
     const char *hd = getenv("RS_HEAD");
@@ -1156,6 +1250,11 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipMemsetAsync(ah.cf_n, 0, 24, E->st));
       HC(hipMemsetAsync(ah.cf_nbig, 0, 16, E->st));
     }
+    // the tail's composition: inside k_big_finish, one workgroup per cluster (RS_TAIL_FINISH=level:
+    // level by level over the GPU like the head's -- slower on the metric circuit, 15 vs 6.6 ms)
+    static const bool tail_split = getenv("RS_TAIL_FINISH") && !strcmp(getenv("RS_TAIL_FINISH"), "level");
+    constexpr uint32_t kHeadLevels = 36, kTailLevels = 32;
+    LevelLoop hl, tl;
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_head) {
@@ -1196,15 +1295,23 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         // the Kahn levels and the emission follow once the rest is enqueued (the level loop waits)
       }
       if (n_head && getenv("RS_HEAD_ALONE")) HC(hipStreamWaitEvent(E->st, E->evx[3], 0));  // diagnostic
+      // the main stream starts once the head's preparation is done: its short workgroups come after
+      // the head's large-LDS ones have found CUs.  The small clusters first (k_eliminate, one lane
+      // each), then the tail: the frames pass that follows waits for both.
+      if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[10], 0));
+      HC(hipEventRecord(E->ev4, E->st));
+      if (n_small) {
+        uint64_t blocks = (n_small + 63) / 64;
+        hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a,
+                           (const uint32_t *)d_small, (uint64_t)n_small);
+        HC(hipGetLastError());
+      }
+      HC(hipEventRecord(E->evx[5], E->st));
       if (n_tail) {
         // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
         // per-lane pool chunks are bounded by the grid size
         const unsigned gb = (unsigned)std::min<uint64_t>(n_tail, 2048), gm = (unsigned)std::min<uint64_t>(n_tail, 8192);
         const uint32_t *ids = d_big + n_head;
-        // the tail starts once the head's preparation is done: the tail's short prep workgroups come
-        // first, so the head's large-LDS workgroups find free CUs before the tail's ordered loop
-        // (8192 long-lived workgroups) holds every CU
-        if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[10], 0));
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
         // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast)
@@ -1241,60 +1348,68 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           HC(hipMemsetAsync(cls, 0, eo.n_clusters, E->st));
           launch(E->st, k_mark_u8, n_tail, ids, n_tail, cls);
           launch(E->st, k_batch_inv_flat, (n_slots + 63) / 64, at, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
+          if (tail_split) launch(E->st, k_normalize_flat, n_slots, at, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
         }
-        hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
-        HC(hipGetLastError());
+        if (tail_split) {
+          // the tail's composition level by level over the whole GPU (LevelLoop), like the head's,
+          // instead of each cluster's levels inside one k_big_finish workgroup
+          ElimArgs ats = at;
+          ats.split = 1;
+          ats.cf_items = E->A.get<uint64_t>("cft.items0", n_slots);
+          ats.cf_n = E->A.get<unsigned long long>("cft.cnt", 3);
+          ats.cf_deg = E->A.get<uint64_t>("cft.deg", n_tail);
+          ats.cf_dl = E->A.get<uint64_t>("cft.dl", n_tail);
+          ats.cf_done = E->A.get<uint32_t>("cft.done", n_tail);
+          ats.cf_big = E->A.get<uint64_t>("cft.big", n_slots);
+          ats.cf_nbig = E->A.get<unsigned long long>("cft.nbig", 2);
+          HC(hipMemsetAsync(ats.cf_n, 0, 24, E->st));
+          HC(hipMemsetAsync(ats.cf_nbig, 0, 16, E->st));
+          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, ats, ids, n_tail);
+          HC(hipGetLastError());
+          tl.ah = ats;
+          tl.ids = ids;
+          tl.s = E->st;
+          tl.cur = ats.cf_items;
+          tl.nxt = E->A.get<uint64_t>("cft.items1", n_slots);
+          tl.n_slots = n_slots;
+          tl.h = E->h_lvl + 4;
+          tl.ev = E->ev_lvlt;
+          tl.run(kTailLevels, false);
+        } else {
+          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
+          HC(hipGetLastError());
+        }
       }
-      HC(hipEventRecord(E->ev4, E->st));
-      if (n_small) {
-        uint64_t blocks = (n_small + 63) / 64;
-        hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a,
-                           (const uint32_t *)d_small, (uint64_t)n_small);
-        HC(hipGetLastError());
+      // the head's first levels go in before the host waits for the tail's
+      if (n_head) {
+        hl.ah = ah;
+        hl.ids = d_big;
+        hl.s = E->st2;
+        hl.cur = ah.cf_items;
+        hl.nxt = cf_next;
+        hl.n_slots = n_slots;
+        hl.h = E->h_lvl;
+        hl.ev = E->ev_lvl;
+        if (overlap && W == 1) hl.run(kHeadLevels, false);
       }
-      HC(hipEventRecord(E->evx[5], E->st));
+      if (tail_split && n_tail) {
+        tl.run(UINT32_MAX, true);
+        hipLaunchKernelGGL(k_big_emit<4>, dim3((unsigned)std::min<uint64_t>(n_tail, 2048)), dim3(256), 0, E->st, tl.ah, d_big + n_head, n_tail);
+        HC(hipGetLastError());
+        if (g_prof_env) fprintf(stderr, "[rs-prof] tail composition: %u level launches\n", tl.levels);
+      }
+      HC(hipEventRecord(E->ev7, E->st));
       if (D.join_pending) {  // the main stream reads the head clusters' orders from here on
         HC(hipStreamWaitEvent(E->st, E->evx[7], 0));
         D.join_pending = false;
       }
       if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
       if (n_head) {
-        // the head's composition, one Kahn level of all its clusters per launch over the whole GPU
-        // (each cluster's DAG is shallow but wide: ~20 levels for thousands of substitutions)
-        // Level L reads count L%3, appends to (L+1)%3 and zeroes (L+2)%3 -- the one level L-1 read and
-        // level L+1 appends to -- and likewise alternates the deferred list's count: no memsets.
-        uint64_t *cur = ah.cf_items, *nxt = cf_next;
-        unsigned long long *nn = ah.cf_n + 1;
-        uint32_t levels = 0;
-        for (uint32_t level = 0; level <= n_slots + 1; ++level) {
-          ElimArgs al = ah;
-          al.cf_nbig = ah.cf_nbig + (level & 1);
-          unsigned long long *nc = ah.cf_n + level % 3, *zc = ah.cf_n + (level + 2) % 3;
-          nn = ah.cf_n + (level + 1) % 3;
-          hipLaunchKernelGGL(k_compose_level<8>, dim3(256), dim3(512), 0, E->st2, al, (const uint32_t *)d_big,
-                             (const uint64_t *)cur, (const unsigned long long *)nc, nxt, nn, level, zc,
-                             ah.cf_nbig + ((level + 1) & 1));
-          hipLaunchKernelGGL(k_compose_big, dim3(256), dim3(64), 0, E->st2, al, (const uint32_t *)d_big, nxt, nn);
-          HC(hipGetLastError());
-          std::swap(cur, nxt);
-          levels = level + 1;
-          if (level % 4 == 3) {
-            // stop once a frontier is empty: every 4 levels the frontier count goes to a pinned
-            // slot, and the host checks the slot of two batches back -- it never waits for the
-            // level it just enqueued (launches past an empty frontier return at once)
-            const uint32_t b = level / 4;
-            HC(hipMemcpyAsync(E->h_lvl + b % 4, nn, 8, hipMemcpyDeviceToHost, E->st2));
-            HC(hipEventRecord(E->ev_lvl[b % 4], E->st2));
-            if (b >= 2) {
-              HC(hipEventSynchronize(E->ev_lvl[(b - 2) % 4]));
-              if (!E->h_lvl[(b - 2) % 4]) break;
-            }
-          }
-        }
+        hl.run(UINT32_MAX, true);
         hipLaunchKernelGGL(k_big_emit<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[4], E->st2));
-        if (g_prof_env) fprintf(stderr, "[rs-prof] head composition: %u level launches\n", levels);
+        if (g_prof_env) fprintf(stderr, "[rs-prof] head composition: %u level launches\n", hl.levels);
         HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
       }
       HC(hipEventRecord(E->ev3, E->st));
@@ -1326,8 +1441,6 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       float ms = 0;
       unsigned long long by = 0;
       HC(hipEventElapsedTime(&ms, E->ev2, E->ev3));
-      float mb = 0;
-      HC(hipEventElapsedTime(&mb, E->ev2, E->ev4));
       float msm = 0;
       HC(hipEventElapsedTime(&msm, E->ev4, E->evx[5]));
       E->stats.elim_big_ms += ms - msm;  // wall of the workgroup kernels (both streams)
@@ -1344,9 +1457,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       E->stats.tail_main_bytes += b5[3];
       if (n_tail) {
         float m0 = 0, m1 = 0, m2 = 0;
-        HC(hipEventElapsedTime(&m0, E->ev2, E->ev5));
+        HC(hipEventElapsedTime(&m0, E->evx[5], E->ev5));
         HC(hipEventElapsedTime(&m1, E->ev5, E->ev6));
-        HC(hipEventElapsedTime(&m2, E->ev6, E->ev4));
+        HC(hipEventElapsedTime(&m2, E->ev6, E->ev7));
         E->stats.big_prep_ms += m0;
         E->stats.big_main_ms += m1;
         E->stats.big_finish_ms += m2;
@@ -1357,9 +1470,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       if (g_prof_env) {
         float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
         if (n_tail) {
-          HC(hipEventElapsedTime(&t0, E->ev2, E->ev5));
+          HC(hipEventElapsedTime(&t0, E->evx[5], E->ev5));
           HC(hipEventElapsedTime(&t1, E->ev5, E->ev6));
-          HC(hipEventElapsedTime(&t2, E->ev6, E->ev4));
+          HC(hipEventElapsedTime(&t2, E->ev6, E->ev7));
         }
         HC(hipEventElapsedTime(&t3, E->ev4, E->evx[5]));
         fprintf(stderr, "[rs-prof] tail(%llu): prep %.2f main %.2f inv+finish %.2f small %.2f", (unsigned long long)n_tail, t0, t1, t2, t3);
@@ -1404,6 +1517,29 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           const unsigned long long *P = &pf[kProfWords * q];
           fprintf(stderr, " [%llu %llu %llu %llu %llu | %.0f %.0f | %llu %.0f | %.0f]", P[2], P[8], P[9], P[10], P[11],
                   P[12] / 100.0, P[13] / 100.0, P[14], P[15] / 100.0, P[5] / 100.0);
+        }
+        fprintf(stderr, "\n");
+      }
+      if (n_tail) {  // the tail's k_big_finish: per-cluster compose time, Kahn levels
+        double tn = 0, tc = 0;
+        std::map<int, uint64_t> lh;
+        std::vector<uint64_t> tq;
+        for (uint64_t q = n_head; q < n_big; ++q) {
+          const unsigned long long *P = &pf[kProfWords * q];
+          tn += P[6] / 100.0;
+          tc += P[7] / 100.0;
+          int b = 0;
+          while ((1ull << b) < P[20] + 1) ++b;
+          lh[b]++;
+          tq.push_back(q);
+        }
+        std::sort(tq.begin(), tq.end(), [&](uint64_t x, uint64_t y) { return pf[kProfWords * x + 7] > pf[kProfWords * y + 7]; });
+        fprintf(stderr, "[rs-prof] tail finish: summed normalize %.0f us compose %.0f us; levels (log2):", tn, tc);
+        for (auto &kv : lh) fprintf(stderr, " %d:%llu", kv.first, (unsigned long long)kv.second);
+        fprintf(stderr, "; slowest (rows subs levels us):");
+        for (size_t i = 0; i < std::min<size_t>(tq.size(), 6); ++i) {
+          const unsigned long long *P = &pf[kProfWords * tq[i]];
+          fprintf(stderr, " [%llu %llu %llu %.0f]", P[0], P[1], P[20], P[7] / 100.0);
         }
         fprintf(stderr, "\n");
       }
@@ -1602,6 +1738,67 @@ static void debug_check_round(rs_engine *E, const RoundArgs &ra, uint64_t n, uin
 }
 
 // ---------------------------------------------------------------- the run
+// the early region's D2H (see rs_engine::SnapJob): chunks of kSnapChunk bytes, each waited for
+static void snap_join(rs_engine *E) {
+  if (E->snap_thread.joinable()) E->snap_thread.join();
+  E->snap_jobs.clear();
+}
+static void snap_start(rs_engine *E) {
+  if (E->snap_thread.joinable()) E->snap_thread.join();
+  E->snap_rc = 0;
+  std::vector<rs_engine::SnapJob> jobs = E->snap_jobs;
+  E->snap_thread = std::thread([E, jobs]() {
+    static const size_t chunk = getenv("RS_SNAP_CHUNK_MB") ? strtoull(getenv("RS_SNAP_CHUNK_MB"), nullptr, 10) << 20 : 16ull << 20;
+    if (hipSetDevice(E->device) != hipSuccess || hipEventSynchronize(E->ev_snap) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
+    // two chunks in flight: no gap between them, and a transfer another stream enqueues waits for
+    // at most two
+    int k = 0;
+    for (const auto &j : jobs)
+      for (size_t o = 0; o < j.bytes; o += chunk, ++k) {
+        const size_t n = std::min(chunk, j.bytes - o);
+        if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
+        if (hipMemcpyAsync((uint8_t *)j.dst + o, (const uint8_t *)j.src + o, n, hipMemcpyDeviceToHost, E->stx) != hipSuccess ||
+            hipEventRecord(E->ev_chunk[k & 1], E->stx) != hipSuccess) {
+          E->snap_rc = RS_E_HIP;
+          return;
+        }
+      }
+    if (hipStreamSynchronize(E->stx) != hipSuccess) E->snap_rc = RS_E_HIP;
+  });
+}
+
+static void *pin_get(rs_engine *E, int slot, size_t bytes) {
+  rs_engine::Pin &b = E->pin[slot];
+  if (b.cap < bytes) {
+    const size_t cap = std::max(bytes, b.cap + b.cap / 4);
+    if (b.p) HC(hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    HC(hipHostMalloc(&b.p, cap, hipHostMallocDefault));
+    b.cap = cap;
+  }
+  return b.p;
+}
+
+// The compact CSR of the result on the device (out.{a,b,c}.{ptr,col,val}): built by every run that
+// does not stream, and on demand (rs_engine_fetch, the .r1cs writer) after one that does.
+static void ensure_csr(rs_engine *E) {
+  if (E->csr_ready) return;
+  Arena &A = E->A;
+  hipStream_t st = E->st;
+  const char *nm[3] = {"out.a", "out.b", "out.c"};
+  const uint64_t n_keep = E->fin_keep, n_lv = E->fin_lvn, n_out = n_keep + n_lv;
+  for (int q = 0; q < 3; ++q) {
+    const uint64_t tot = E->out_nnz[q];
+    const uint64_t *ptr = A.get<uint64_t>(std::string(nm[q]) + ".ptr", n_out + 1);
+    uint32_t *col = A.get<uint32_t>(std::string(nm[q]) + ".col", tot);
+    uint64_t *val = A.get<uint64_t>(std::string(nm[q]) + ".val", 4 * tot);
+    if (n_keep) launch(st, k_gather_rows, n_keep, E->F, E->fin_parts[q], E->fin_keep_ids, n_keep, ptr, col, val);
+    if (n_lv) launch(st, k_gather_rows, n_lv, E->F, E->fin_lvq[q], E->fin_lv_ids, n_lv, ptr + n_keep, col, val);
+  }
+  E->csr_ready = true;
+}
+
 static void engine_run(rs_engine *E, const rs_flags *fl) {
   const uint64_t S = E->S;
   hipStream_t st = E->st;
@@ -1631,6 +1828,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   HC(hipMemsetAsync(sub_of, 0xff, 4 * S, st));
 
   std::vector<HostCon> lconst;
+  snap_join(E);
+  E->snap_on = false;
+  E->csr_ready = false;
   E->log_on = fl->emit_substitution_log != 0;
   E->log_from.clear();
   E->log_key.clear();
@@ -1949,6 +2149,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       HC(hipMemcpyAsync(nv, E->heap_v, 32 * heap_top, hipMemcpyDeviceToDevice, st));
       HC(hipStreamSynchronize(st));
     }
+    if (E->snap_on) HC(hipStreamSynchronize(E->stc));  // the early gather reads the old heap
     if (E->heap_k) { HC(hipFree(E->heap_k)); HC(hipFree(E->heap_v)); }
     E->heap_k = heap_k = nk;
     E->heap_v = heap_v = nv;
@@ -1985,6 +2186,53 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   }
   // one pass of the frames over the non-linear rows ids[0, n) (phase: see NLArgs); the fill's
   // kernel time is read from (e0, e1) once the caller synchronises
+  // streamed result (output.hpp): the non-linear rows round 1's substitution has finished and left
+  // non-linear (storage rows) are gathered to the early region and copied to the host on the copy
+  // stream while the run goes on.  late: rows a second frames pass still has to do (nullptr: none).
+  uint8_t *so_early = nullptr;
+  U3 *so_eoff = nullptr;
+  auto snap_take = [&](const uint64_t *late) {
+    if (!E->stream_out || !n_nl || getenv("RS_NO_STREAM")) return;
+    so_early = A.get<uint8_t>("so.early", n_nl);
+    so_eoff = A.get<U3>("so.eoff", n_nl);
+    U3 *elen = A.get<U3>("so.elen", n_nl);
+    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, so_early, elen);
+    const U3 et = excl_scan_u3(E, elen, so_eoff, n_nl, "so");
+    const uint64_t ev[3] = {et.a, et.b, et.c};
+    // the gather reads copies of the row views: the second pass and later rounds re-point rows
+    const DRows *src[3] = {&sa, &sb, &sc};
+    const char *nm[3] = {"so.a", "so.b", "so.c"};
+    DRows cp[3];
+    for (int q = 0; q < 3; ++q) {
+      cp[q] = *src[q];
+      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
+      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
+      HC(hipMemcpyAsync(cp[q].off, src[q]->off, 8 * n_nl, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(cp[q].len, src[q]->len, 4 * n_nl, hipMemcpyDeviceToDevice, st));
+    }
+    HC(hipEventRecord(E->ev_snap0, st));
+    HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
+    for (int q = 0; q < 3; ++q) {
+      E->snap_e[q] = ev[q];
+      // the device early region = the head of the layout's arrays; the late rows follow it
+      const uint64_t cap = ev[q] + std::max<uint64_t>(ev[q] / 4, 1 << 16);
+      const std::string xn = std::string("out.") + "abc"[q];
+      uint32_t *col = A.get<uint32_t>(xn + ".xcol", cap);
+      uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
+      if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val);
+      void *hc = pin_get(E, 3 + q, 4 * cap), *hv = pin_get(E, 6 + q, 32 * cap);
+      if (ev[q]) {
+        E->snap_jobs.push_back({hc, col, 4 * ev[q]});
+        E->snap_jobs.push_back({hv, val, 32 * ev[q]});
+      }
+    }
+    HC(hipEventRecord(E->ev_snap, E->stc));
+    E->snap_on = true;
+    snap_start(E);
+    if (g_prof_env)
+      fprintf(stderr, "[rs-prof] stream: early region %llu / %llu / %llu entries (%.1f MB)%s\n", (unsigned long long)ev[0],
+              (unsigned long long)ev[1], (unsigned long long)ev[2], 36e-6 * (ev[0] + ev[1] + ev[2]), late ? " after the first pass" : "");
+  };
   auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1) {
     stage_nl();
     NLArgs a{};
@@ -2084,6 +2332,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     HC(hipGetLastError());
     fr.h_off = ea.h_off; fr.h_len = ea.h_len; fr.pk = ea.pk; fr.pv = ea.pv;
     nl_phase(1, nullptr, n_nl, E->evx[8], E->evx[9]);
+    snap_take(nl_late);
     nl_split = true;
   };
 
@@ -2137,6 +2386,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (nl_split) nl_ms(E->evx[8], E->evx[9]);
     if (!nl_split) {
       nl_phase(0, nullptr, n_nl, E->ev0, E->ev1);
+      snap_take(nullptr);
       nl_ms(E->ev0, E->ev1);
     } else if (n_late) {
       nl_phase(2, nl_lids, n_late, E->ev0, E->ev1);
@@ -2193,6 +2443,12 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
 
   // ======================= rounds >= 2 (:613-646)
   bool apply_round = apply_linear && no_rounds > 0 && n_wl > 0;
+  // streamed result: rows a later round touches are taken from the late region
+  uint8_t *so_dirty = nullptr;
+  if (so_early) {
+    so_dirty = A.get<uint8_t>("so.dirty", n_st ? n_st : 1);
+    if (n_st) HC(hipMemsetAsync(so_dirty, 0, n_st, st));
+  }
   if (getenv("RS_DEBUG")) {
     HC(hipStreamSynchronize(st));
     fprintf(stderr, "[rs-debug] heap %p cap %llu top %llu n_st %llu n_wl %llu\n", (void *)heap_k,
@@ -2515,6 +2771,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         MK.mark("fill");
         if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qt);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
+        if (so_dirty) launch(st, k_or_u8, n_st, (const uint8_t *)ra.touched, n_st, so_dirty);
         // turned rows
         uint64_t *tf = A.get<uint64_t>("r.tf", n_st), *tp = A.get<uint64_t>("r.tp", n_st);
         launch(st, k_turn_flags, n_st, (const int32_t *)ra.turn, n_st, tf);
@@ -2729,11 +2986,44 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       HC(hipMemsetAsync(lens + n_out, 0, 8, st));
       uint64_t tot = excl_scan_u64(E, lens, ptr, n_out + 1, nm[q]);
       E->out_nnz[q] = tot;
-      uint32_t *col = A.get<uint32_t>(std::string(nm[q]) + ".col", tot);
-      uint64_t *val = A.get<uint64_t>(std::string(nm[q]) + ".val", 4 * tot);
-      if (n_keep) launch(st, k_gather_rows, n_keep, E->F, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint64_t *)ptr, col, val);
-      if (n_lv) launch(st, k_gather_rows, n_lv, E->F, lvq, (const uint32_t *)lv_ids, n_lv, (const uint64_t *)(ptr + n_keep), col, val);
+      E->fin_parts[q] = *parts[q];
+      E->fin_lvq[q] = lvq;
+      if (!E->snap_on) continue;
+      // streamed layout: the rows not reused from the early region, after it
+      uint64_t *late = A.get<uint64_t>(std::string(nm[q]) + ".late", n_out + 1);
+      uint64_t *lptr = A.get<uint64_t>(std::string(nm[q]) + ".lptr", n_out + 1);
+      if (n_keep) launch(st, k_out_late_lens, n_keep, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids,
+                         (const uint8_t *)so_early, (const uint8_t *)so_dirty, late);
+      if (n_lv) launch(st, k_row_lens, n_lv, lvq, (const uint32_t *)lv_ids, n_lv, late + n_keep);
+      HC(hipMemsetAsync(late + n_out, 0, 8, st));
+      const uint64_t L = excl_scan_u64(E, late, lptr, n_out + 1, "late");
+      const uint64_t base = E->snap_e[q], ext = base + L;
+      E->out_ext[q] = ext;
+      uint64_t *beg = A.get<uint64_t>(std::string(nm[q]) + ".beg", n_out + 1);
+      uint64_t *end = A.get<uint64_t>(std::string(nm[q]) + ".end", n_out + 1);
+      if (n_keep) launch(st, k_out_extent, n_keep, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids,
+                         (const uint8_t *)so_early, (const uint8_t *)so_dirty, (const U3 *)so_eoff, q, base, (const uint64_t *)lptr, beg, end);
+      if (n_lv) launch(st, k_out_extent, n_lv, lvq, (const uint32_t *)lv_ids, n_lv, (const uint32_t *)nullptr, (const uint8_t *)nullptr,
+                       (const uint8_t *)nullptr, (const U3 *)nullptr, q, base, (const uint64_t *)(lptr + n_keep), beg + n_keep, end + n_keep);
+      launch(st, k_set_u64, 1, beg + n_out, ext);
+      // the device copy of the whole layout grows past the early region when it must (the
+      // early region is copied along once its gather is done)
+      const std::string xc = std::string(nm[q]) + ".xcol", xv = std::string(nm[q]) + ".xval";
+      if (A.cap_bytes(xc) < 4 * ext || A.cap_bytes(xv) < 32 * ext) snap_join(E);  // its D2H reads them
+      A.grow_keep<uint32_t>(xc, ext, base, E->stc, st);
+      A.grow_keep<uint64_t>(xv, 4 * ext, 4 * base, E->stc, st);
+      uint32_t *col = A.get<uint32_t>(xc, ext);
+      uint64_t *val = A.get<uint64_t>(xv, 4 * ext);
+      if (n_keep) launch(st, k_gather_late, n_keep, E->F, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids,
+                         (const uint8_t *)so_early, (const uint8_t *)so_dirty, (const uint64_t *)lptr, col + base, val + 4 * base);
+      if (n_lv) launch(st, k_gather_late, n_lv, E->F, lvq, (const uint32_t *)lv_ids, n_lv, (const uint32_t *)nullptr,
+                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + n_keep), col + base, val + 4 * base);
     }
+    E->fin_keep = n_keep;
+    E->fin_lvn = n_lv;
+    E->fin_keep_ids = keep_ids;
+    E->fin_lv_ids = lv_ids;
+    if (!E->snap_on) ensure_csr(E);
     E->out_host_tail = std::move(lconst);
   }
   load_wait_all(E);  // a group the path never needed (e.g. no non-linear rows) is still checked
@@ -2821,12 +3111,14 @@ int rs_engine_create(int device, rs_engine **eng) {
         HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
     }
     HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&E->stx, hipStreamNonBlocking));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));
     for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipHostMalloc((void **)&E->h_vflag, 10 * sizeof(int), hipHostMallocDefault));
     memset(E->h_vflag, 0, 10 * sizeof(int));
-    HC(hipHostMalloc((void **)&E->h_lvl, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+    HC(hipHostMalloc((void **)&E->h_lvl, 8 * sizeof(unsigned long long), hipHostMallocDefault));
     for (auto &ev : E->ev_lvl) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (auto &ev : E->ev_lvlt) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipEventCreate(&E->ev0));
     HC(hipEventCreate(&E->ev1));
     HC(hipEventCreate(&E->ev2));
@@ -2834,6 +3126,10 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipEventCreate(&E->ev4));
     HC(hipEventCreate(&E->ev5));
     HC(hipEventCreate(&E->ev6));
+    HC(hipEventCreate(&E->ev7));
+    HC(hipEventCreateWithFlags(&E->ev_snap, hipEventDisableTiming));
+    HC(hipEventCreateWithFlags(&E->ev_snap0, hipEventDisableTiming));
+    for (auto &ev : E->ev_chunk) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {
@@ -2851,6 +3147,7 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->st) (void)hipStreamSynchronize(E->st);
   if (E->st2) (void)hipStreamSynchronize(E->st2);
   if (E->stc) (void)hipStreamSynchronize(E->stc);
+  snap_join(E);
   E->comm.reset();
   for (auto &pb : E->pin)
     if (pb.p) (void)hipHostFree(pb.p);
@@ -2858,9 +3155,12 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->h_lvl) (void)hipHostFree(E->h_lvl);
   for (auto &ev : E->ev_lvl)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto &ev : E->ev_lvlt)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : E->ev_grp)
     if (ev) (void)hipEventDestroy(ev);
   if (E->stc) (void)hipStreamDestroy(E->stc);
+  if (E->stx) (void)hipStreamDestroy(E->stx);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
   if (E->ev2) (void)hipEventDestroy(E->ev2);
@@ -2868,6 +3168,11 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->ev4) (void)hipEventDestroy(E->ev4);
   if (E->ev5) (void)hipEventDestroy(E->ev5);
   if (E->ev6) (void)hipEventDestroy(E->ev6);
+  if (E->ev7) (void)hipEventDestroy(E->ev7);
+  if (E->ev_snap) (void)hipEventDestroy(E->ev_snap);
+  if (E->ev_snap0) (void)hipEventDestroy(E->ev_snap0);
+  for (auto &ev : E->ev_chunk)
+    if (ev) (void)hipEventDestroy(ev);
   if (E->heap_k) (void)hipFree(E->heap_k);
   if (E->heap_v) (void)hipFree(E->heap_v);
   if (E->st) (void)hipStreamDestroy(E->st);
@@ -2922,7 +3227,25 @@ namespace rs {
 // pinned buffers for rs_engine_simplify).  Every D2H is enqueued first and waited for once; the
 // host-side lconst rows are then appended after the device rows.  The substitution log is copied
 // (own = true) or pointed at (the engine's vectors, rs_engine_simplify's view).
-static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(int, size_t)> &buf, bool own_log) {
+// grows pinned slot `slot` keeping its first `keep` bytes (the early region, once its D2H is done)
+static void *pin_grow_keep(rs_engine *E, int slot, size_t bytes, size_t keep) {
+  rs_engine::Pin &b = E->pin[slot];
+  if (b.cap >= bytes) return b.p;
+  snap_join(E);
+  const size_t cap = std::max(bytes, b.cap + b.cap / 4);
+  void *p = nullptr;
+  HC(hipHostMalloc(&p, cap, hipHostMallocDefault));
+  if (keep) memcpy(p, b.p, keep);
+  if (b.p) HC(hipHostFree(b.p));
+  b.p = p;
+  b.cap = cap;
+  return p;
+}
+
+// D2H of the last result.  streamed (rs_engine_simplify after a run that took the early region):
+// the early region is already on its way into pin[3..8]; the late rows land after it and every
+// row gets [beg, end) (rs_output.{a,b,c}_end).  Otherwise the compact CSR.
+static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(int, size_t)> &buf, bool own_log, bool streamed) {
   const uint64_t nd = E->out_n_dev;
   // non-empty host rows (lconst after fix may be empty: extract_with removes them)
   std::vector<const HostCon *> hrows;
@@ -2932,36 +3255,73 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
   o->n_constraints = nd + nh;
   const char *nm[3] = {"out.a", "out.b", "out.c"};
   rs_lc *dst[3] = {&o->a, &o->b, &o->c};
+  uint64_t **ends[3] = {&o->a_end, &o->b_end, &o->c_end};
+  uint64_t base[3];  // where the host rows start in col / val
+  if (!streamed) ensure_csr(E);
   for (int q = 0; q < 3; ++q) {
     uint64_t hn = 0;
     for (auto *c : hrows) hn += c->k[q].size();
-    const uint64_t tot = E->out_nnz[q] + hn;
     rs_lc &L = *dst[q];
+    const std::string n(nm[q]);
+    if (!streamed) {
+      const uint64_t tot = E->out_nnz[q] + hn;
+      L.n_rows = nd + nh;
+      L.nnz = tot;
+      L.ptr = (uint64_t *)buf(q, 8 * (nd + nh + 1));
+      L.col = (uint32_t *)buf(3 + q, 4 * (tot ? tot : 1));
+      L.val = (uint64_t *)buf(6 + q, 32 * (tot ? tot : 1));
+      *ends[q] = nullptr;
+      if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(n + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
+      else L.ptr[0] = 0;
+      if (E->out_nnz[q]) {
+        HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(n + ".col", 1), 4 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+        HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(n + ".val", 1), 32 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+      }
+      base[q] = E->out_nnz[q];
+      continue;
+    }
+    const uint64_t early = E->snap_e[q], ext = E->out_ext[q], tot = ext + hn;
     L.n_rows = nd + nh;
     L.nnz = tot;
-    L.ptr = (uint64_t *)buf(q, 8 * (nd + nh + 1));
-    L.col = (uint32_t *)buf(3 + q, 4 * (tot ? tot : 1));
-    L.val = (uint64_t *)buf(6 + q, 32 * (tot ? tot : 1));
-    if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
-    else L.ptr[0] = 0;
-    if (E->out_nnz[q]) {
-      HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(std::string(nm[q]) + ".col", 1), 4 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
-      HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(std::string(nm[q]) + ".val", 1), 32 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+    L.ptr = (uint64_t *)pin_get(E, q, 8 * (nd + nh + 1));
+    *ends[q] = (uint64_t *)pin_get(E, 13 + q, 8 * (nd + nh + 1));
+    L.col = (uint32_t *)pin_grow_keep(E, 3 + q, 4 * (tot ? tot : 1), 4 * early);
+    L.val = (uint64_t *)pin_grow_keep(E, 6 + q, 32 * (tot ? tot : 1), 32 * early);
+    if (nd) {
+      HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(n + ".beg", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
+      HC(hipMemcpyAsync(*ends[q], E->A.get<uint64_t>(n + ".end", 1), 8 * nd, hipMemcpyDeviceToHost, E->st));
+    } else {
+      L.ptr[0] = ext;
     }
+    if (ext > early) {
+      HC(hipMemcpyAsync(L.col + early, E->A.get<uint32_t>(n + ".xcol", 1) + early, 4 * (ext - early), hipMemcpyDeviceToHost, E->st));
+      HC(hipMemcpyAsync(L.val + 4 * early, E->A.get<uint64_t>(n + ".xval", 1) + 4 * early, 32 * (ext - early),
+                        hipMemcpyDeviceToHost, E->st));
+    }
+    base[q] = ext;
   }
   o->n_labels = E->S;
   o->label_to_wire = (int32_t *)buf(9, 4 * E->S);
   HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int32_t>("fin.l2w", 1), 4 * E->S, hipMemcpyDeviceToHost, E->st));
   HC(hipStreamSynchronize(E->st));
+  if (streamed) {
+    snap_join(E);
+    if (E->snap_rc) throw RsError(RS_E_HIP, "D2H of the streamed rows failed");
+  }
   for (int q = 0; q < 3; ++q) {
     rs_lc &L = *dst[q];
-    uint64_t e = E->out_nnz[q];
+    uint64_t e = base[q];
+    uint64_t *end = *ends[q];
     for (uint64_t i = 0; i < nh; ++i) {
       const HostCon &c = *hrows[i];
       const size_t m = c.k[q].size();
       if (m) {
         memcpy(L.col + e, c.k[q].data(), 4 * m);
         memcpy(L.val + 4 * e, c.v[q].data(), 32 * m);
+      }
+      if (end) {
+        L.ptr[nd + i] = e;
+        end[nd + i] = e + m;
       }
       e += m;
       L.ptr[nd + i + 1] = e;
@@ -2997,18 +3357,6 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
   }
 }
 
-static void *pin_get(rs_engine *E, int slot, size_t bytes) {
-  rs_engine::Pin &b = E->pin[slot];
-  if (b.cap < bytes) {
-    const size_t cap = std::max(bytes, b.cap + b.cap / 4);
-    if (b.p) HC(hipHostFree(b.p));
-    b.p = nullptr;
-    b.cap = 0;
-    HC(hipHostMalloc(&b.p, cap, hipHostMallocDefault));
-    b.cap = cap;
-  }
-  return b.p;
-}
 }  // namespace rs
 
 int rs_engine_fetch(rs_engine *E, rs_output **out) {
@@ -3017,7 +3365,8 @@ int rs_engine_fetch(rs_engine *E, rs_output **out) {
     HC(hipSetDevice(E->device));
     rs_output *o = (rs_output *)calloc(1, sizeof(rs_output));
     try {
-      fetch_result(E, o, [](int, size_t bytes) { void *p = malloc(bytes ? bytes : 1); if (!p) throw std::bad_alloc(); return p; }, true);
+      fetch_result(E, o, [](int, size_t bytes) { void *p = malloc(bytes ? bytes : 1); if (!p) throw std::bad_alloc(); return p; }, true,
+                   false);
     } catch (...) {
       rs_output_free(o);
       throw;
@@ -3038,11 +3387,18 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
     const double t0 = now_ms();
     HC(hipSetDevice(E->device));
     load_enqueue(E, in, true);
-    engine_run(E, fl);
+    E->stream_out = true;
+    try {
+      engine_run(E, fl);
+    } catch (...) {
+      E->stream_out = false;
+      throw;
+    }
+    E->stream_out = false;
     E->hin = nullptr;
     const double t1 = now_ms();
     E->view = rs_output{};
-    fetch_result(E, &E->view, [E](int slot, size_t bytes) { return pin_get(E, slot, bytes); }, false);
+    fetch_result(E, &E->view, [E](int slot, size_t bytes) { return pin_get(E, slot, bytes); }, false, E->snap_on);
     const double t2 = now_ms();
     E->stats.d2h_ms = t2 - t1;
     E->stats.host_total_ms = t2 - t0;
@@ -3093,6 +3449,7 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
       E->stats.write_ms = now_ms() - t0;
       return rc;
     }
+    ensure_csr(E);
     const char *nm[3] = {"out.a", "out.b", "out.c"};
     const uint64_t *pq[3];
     for (int q = 0; q < 3; ++q) pq[q] = A.get<uint64_t>(std::string(nm[q]) + ".ptr", 1);
@@ -3243,6 +3600,9 @@ void rs_output_free(rs_output *o) {
   free(o->label_to_wire);
   free(o->log_from);
   free_lc(o->log_to);
+  free(o->a_end);
+  free(o->b_end);
+  free(o->c_end);
   free(o);
 }
 

@@ -2560,6 +2560,23 @@ __global__ void k_batch_inv_flat(ElimArgs A, const uint32_t *cid, const uint8_t 
   }
 }
 
+// normalize_substitutions (:414-437) over the slot space of the flagged clusters (cls == 1), one
+// lane per substitution: the tail stream's clusters when their composition runs level by level
+// over the whole GPU (k_compose_level) instead of inside k_big_finish
+__global__ void k_normalize_flat(ElimArgs A, const uint32_t *cid, const uint8_t *cls, uint64_t n_slots) {
+  const FieldP &F = A.F;
+  unsigned long long by = 0;
+  for (uint64_t sl = gtid(); sl < n_slots; sl += gstride()) {
+    if (!d_inv_slot(A, cid, cls, sl)) continue;
+    const Fe inv_i = A.ftmp[sl];
+    Fe *vv = A.pv + A.h_off[sl];
+    const uint32_t l = A.h_len[sl];
+    for (uint32_t t = 0; t < l; ++t) vv[t] = fmul(F, vv[t], inv_i);
+    by += 64ull * (l + 1);
+  }
+  wave_atomic_add(A.bytes_fin, by);
+}
+
 // Lane-serial composition of slot `sl` (raw_substitution key by key, ascending): the fallback for
 // lists the wave path does not hold.
 __device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t sl, unsigned long long &by) {

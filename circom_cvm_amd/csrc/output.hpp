@@ -1,0 +1,106 @@
+// output.hpp -- row extents of the result and the streamed D2H of rs_engine_simplify (ABI 7).
+//
+// The result is the storage rows in storage order, then the linear rows the rounds left, then the
+// host-side lconst rows (constraint_simplification.rs:648-729).  A storage row is final once round
+// 1's substitution has run on it (non_linear_utils.rs:6-31) unless a later round's substitution
+// touches it (:613-646; in the metric circuit 8 % of the rows).  So as soon as the first frames pass
+// is done, its storage rows ("early") are gathered to an early region and copied to the host on the
+// copy stream while the head's rows, the later rounds and the final assembly run; at the end only
+// the rows that are not early, or that a round touched after all ("dirty"), are gathered after the
+// early region, and every output row is given as [beg, end) into [early | late].  Included by
+// engine.hip inside namespace rs, after U3.
+#pragma once
+
+__device__ __forceinline__ uint64_t u3_sel(const U3 &x, int q) { return q == 0 ? x.a : (q == 1 ? x.b : x.c); }
+
+// early[i]: non-linear row i is done (not left to a second pass) and stayed non-linear -- a
+// storage row (non_linear_utils.rs:6-31: A or B non-empty); elen[i]: its part lengths (0
+// when not early)
+__global__ void k_snap_flags(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, uint8_t *early, U3 *elen) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const bool done = !late || !late[i];
+    const uint32_t la = done ? a.len[i] : 0, lb = done ? b.len[i] : 0, lc = done ? c.len[i] : 0;
+    const bool ok = (la | lb) != 0;  // k_flag_linear: linear iff A and B are both empty
+    early[i] = ok ? 1 : 0;
+    elen[i] = ok ? U3{la, lb, lc} : U3{0, 0, 0};
+  }
+}
+
+// the early rows of one part, canonical, at their early-region offsets (R: a copy of the row views
+// taken at the snapshot, so later rounds may move the rows meanwhile)
+__global__ void k_snap_gather(FieldP F, DRows R, const uint8_t *early, const U3 *eoff, int q, uint64_t n, uint32_t *col,
+                              uint64_t *val) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    if (!early[r]) continue;
+    const uint64_t o = u3_sel(eoff[r], q), s = R.off[r];
+    const uint32_t len = R.len[r];
+    for (uint32_t t = 0; t < len; ++t) {
+      col[o + t] = R.key[s + t];
+      const Fe c = ffrom_mont(F, R.val[s + t]);
+      val[4 * (o + t) + 0] = c.l[0];
+      val[4 * (o + t) + 1] = c.l[1];
+      val[4 * (o + t) + 2] = c.l[2];
+      val[4 * (o + t) + 3] = c.l[3];
+    }
+  }
+}
+
+__global__ void k_or_u8(const uint8_t *x, uint64_t n, uint8_t *acc) {
+  for (uint64_t i = gtid(); i < n; i += gstride())
+    if (x[i]) acc[i] = 1;
+}
+
+// storage row r (non-linear row nl_of[r]) keeps its early copy: early, and no later round touched it
+__device__ __forceinline__ bool d_reused(const uint8_t *early, const uint8_t *dirty, const uint32_t *nl_of, uint32_t r) {
+  return early && early[nl_of[r]] && !dirty[r];
+}
+
+// output rows ids[0..n) of one part: the length each needs in the late region (0: reused)
+__global__ void k_out_late_lens(DRows R, const uint32_t *ids, uint64_t n, const uint32_t *nl_of, const uint8_t *early,
+                                const uint8_t *dirty, uint64_t *late) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t r = ids[i];
+    late[i] = d_reused(early, dirty, nl_of, r) ? 0 : R.len[r];
+  }
+}
+
+// their extents: a reused row keeps its early offset, the others go to base + lptr[i]
+__global__ void k_out_extent(DRows R, const uint32_t *ids, uint64_t n, const uint32_t *nl_of, const uint8_t *early,
+                             const uint8_t *dirty, const U3 *eoff, int q, uint64_t base, const uint64_t *lptr, uint64_t *beg,
+                             uint64_t *end) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t r = ids[i];
+    const uint64_t b = d_reused(early, dirty, nl_of, r) ? u3_sel(eoff[nl_of[r]], q) : base + lptr[i];
+    beg[i] = b;
+    end[i] = b + R.len[r];
+  }
+}
+
+// the late rows, canonical, at lptr[i] of the late region
+__global__ void k_gather_late(FieldP F, DRows R, const uint32_t *ids, uint64_t n, const uint32_t *nl_of, const uint8_t *early,
+                              const uint8_t *dirty, const uint64_t *lptr, uint32_t *col, uint64_t *val) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t r = ids[i];
+    if (d_reused(early, dirty, nl_of, r)) continue;
+    const uint64_t o = lptr[i], s = R.off[r];
+    const uint32_t len = R.len[r];
+    for (uint32_t t = 0; t < len; ++t) {
+      col[o + t] = R.key[s + t];
+      const Fe c = ffrom_mont(F, R.val[s + t]);
+      val[4 * (o + t) + 0] = c.l[0];
+      val[4 * (o + t) + 1] = c.l[1];
+      val[4 * (o + t) + 2] = c.l[2];
+      val[4 * (o + t) + 3] = c.l[3];
+    }
+  }
+}
+
+// device -> (pinned, mapped) host memory, 16 bytes per lane per step, fully coalesced
+__global__ void k_to_host(const uint4 *src, uint4 *dst, uint64_t n16) {
+  for (uint64_t i = gtid(); i < n16; i += gstride()) dst[i] = src[i];
+}
+
+__global__ void k_set_u64(uint64_t *p, uint64_t v) {
+  if (gtid() == 0) *p = v;
+}
+

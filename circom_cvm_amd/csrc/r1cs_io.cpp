@@ -205,9 +205,9 @@ static std::string dec_string(const uint64_t *v) {
 
 // hashmap_as_json (json_porting.rs:16-26) + JsonValue::to_string: {"k":"v",...}, keys ascending
 // (as numbers), `ids` mapped through `l2w` when given (apply_correspondence).
-static bool map_json(std::string &o, const rs_lc &L, uint64_t r, const int32_t *l2w, uint64_t n_labels) {
+static bool map_json(std::string &o, const rs_lc &L, const uint64_t *end, uint64_t r, const int32_t *l2w, uint64_t n_labels) {
   std::vector<std::pair<uint64_t, uint64_t>> ord;  // (key, entry)
-  for (uint64_t e = L.ptr[r]; e < L.ptr[r + 1]; ++e) {
+  for (uint64_t e = L.ptr[r]; e < rs_row_end(&L, end, r); ++e) {
     uint64_t k = L.col[e];
     if (l2w) {
       int64_t w = k < n_labels ? l2w[k] : -1;
@@ -377,6 +377,7 @@ static int write_r1cs(const char *path, const rs_input *in, const rs_output *out
   };
   std::vector<std::pair<uint64_t, uint64_t>> ord;  // (order key, entry)
   const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
+  const uint64_t *ends[3] = {out->a_end, out->b_end, out->c_end};
   const bool with_gates = gates && (gates->have[4] || gates->have[5]);
   fwrite(with_gates ? "r1cs\x01\x00\x00\x00\x05\x00\x00\x00" : "r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
   // constraints section (r1cs_porting.rs:20-35) -- written first, size back-patched
@@ -391,7 +392,7 @@ static int write_r1cs(const char *path, const rs_input *in, const rs_output *out
     for (int q = 0; q < 3; ++q) {
       const rs_lc &b = *parts[q];
       ord.clear();
-      for (uint64_t e = b.ptr[r]; e < b.ptr[r + 1]; ++e) {
+      for (uint64_t e = b.ptr[r]; e < rs_row_end(&b, ends[q], r); ++e) {
         uint32_t k = b.col[e];
         uint32_t w;
         if (k == 0) w = 0;
@@ -483,11 +484,12 @@ int rs_write_constraints_json(const char *path, const rs_output *out) {
   fputs("{\n\"constraints\": [", f);
   std::string line;
   const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
+  const uint64_t *ends[3] = {out->a_end, out->b_end, out->c_end};
   for (uint64_t r = 0; r < out->n_constraints; ++r) {
     line.assign(r ? ",\n[" : "\n[");
     for (int q = 0; q < 3; ++q) {
       if (q) line += ',';
-      if (!map_json(line, *parts[q], r, out->label_to_wire, out->n_labels)) {
+      if (!map_json(line, *parts[q], ends[q], r, out->label_to_wire, out->n_labels)) {
         fclose(f);
         set_error("constraint mentions a removed signal (apply_correspondence panics)");
         return RS_E_INTERNAL;
@@ -513,7 +515,7 @@ int rs_write_substitution_json(const char *path, const rs_output *out) {
     line.assign(i ? ",\n\"" : "\n\"");
     line += std::to_string(out->log_from[i]);
     line += "\" : ";
-    map_json(line, out->log_to, i, nullptr, 0);
+    map_json(line, out->log_to, nullptr, i, nullptr, 0);
     fwrite(line.data(), 1, line.size(), f);
   }
   fputs("\n}", f);

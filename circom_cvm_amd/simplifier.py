@@ -16,6 +16,7 @@ from typing import Dict, List
 
 import numpy as np
 
+from . import abi
 from .abi import Engine, Input, Output, RsInput, check, lib, make_flags
 
 
@@ -99,13 +100,8 @@ class ConstraintList:
         l2w = self.label_to_wire()
         out = []
         blocks = []
-        for b in (o.a, o.b, o.c):
-            n = int(b.n_rows)
-            ptr = np.ctypeslib.as_array(b.ptr, shape=(n + 1,)) if n else np.zeros(1, np.uint64)
-            nnz = int(ptr[n]) if n else 0
-            col = np.ctypeslib.as_array(b.col, shape=(max(nnz, 1),))
-            val = np.ctypeslib.as_array(b.val, shape=(max(nnz, 1) * 4,))
-            blocks.append((ptr, col, val))
+        for q in range(3):
+            blocks.append(abi.block_csr(*o.block(q)))
         for r in range(int(o.n_constraints)):
             row = []
             for ptr, col, val in blocks:

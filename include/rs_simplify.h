@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 6
+#define RS_ABI_VERSION 7
 
 enum rs_status {
   RS_OK = 0,
@@ -125,7 +125,17 @@ typedef struct rs_output {
   uint64_t n_log;
   uint32_t *log_from;
   rs_lc log_to;
+  /* ABI 7: row extents of a / b / c.  NULL: the block is CSR (row i = [ptr[i], ptr[i+1])), as
+   * rs_simplify / rs_engine_fetch return it.  Non-NULL (rs_engine_simplify's streamed result):
+   * row i = [ptr[i], end[i]) of col / val.  Rows stay in storage order but need not be contiguous:
+   * the storage rows that were final after the first round went to the host while the later rounds
+   * ran, the rest follow them, so col / val may hold entries no row refers to.  nnz is then the
+   * extent of col / val (= ptr[n_rows]), not the sum of the row lengths. */
+  uint64_t *a_end, *b_end, *c_end;
 } rs_output;
+
+/* End of row r of a result block: end[r] when the block has row ends (ABI 7), else ptr[r + 1]. */
+static inline uint64_t rs_row_end(const rs_lc *L, const uint64_t *end, uint64_t r) { return end ? end[r] : L->ptr[r + 1]; }
 
 /* Phase timings of the last rs_engine_run (milliseconds, HIP events + host clock). */
 typedef struct rs_stats {

@@ -149,9 +149,11 @@ pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, Signal
         panic!("rs_simplify failed ({}): {}", rc, msg);
     }
     let o = unsafe { &*out };
-    let map_of = |lc: &ffi::rs_lc, r: usize| -> HashMap<usize, BigInt> {
+    // row r = [ptr[r], end[r]) when the block carries row ends (ABI 7), else [ptr[r], ptr[r + 1])
+    let map_of = |lc: &ffi::rs_lc, end: *mut u64, r: usize| -> HashMap<usize, BigInt> {
         let mut m = HashMap::new();
-        let (lo, hi) = unsafe { (*lc.ptr.add(r) as usize, *lc.ptr.add(r + 1) as usize) };
+        let lo = unsafe { *lc.ptr.add(r) as usize };
+        let hi = unsafe { if end.is_null() { *lc.ptr.add(r + 1) as usize } else { *end.add(r) as usize } };
         for e in lo..hi {
             let k = unsafe { *lc.col.add(e) } as usize;
             let limbs: Vec<u64> = (0..4).map(|i| unsafe { *lc.val.add(4 * e + i) }).collect();
@@ -162,7 +164,7 @@ pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, Signal
     let mut storage = ConstraintStorage::new();
     for r in 0..o.n_constraints as usize {
         // Constraint::new is private (algebra.rs:1012): the shim adds `pub fn new_unchecked(a, b, c)`
-        storage.add_constraint(C::new_unchecked(map_of(&o.a, r), map_of(&o.b, r), map_of(&o.c, r)));
+        storage.add_constraint(C::new_unchecked(map_of(&o.a, o.a_end, r), map_of(&o.b, o.b_end, r), map_of(&o.c, o.c_end, r)));
     }
     let mut signal_map = SignalMap::with_capacity(o.n_wires as usize);
     for s in 0..o.n_labels as usize {

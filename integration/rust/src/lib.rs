@@ -1,10 +1,10 @@
-//! Raw bindings of `include/rs_simplify.h` (ABI 6), one item per C declaration, same order and
+//! Raw bindings of `include/rs_simplify.h` (ABI 7), one item per C declaration, same order and
 //! layout.  The safe wrapper a caller uses is `constraint_list_glue.rs` (the body that replaces
 //! `constraint_list::constraint_simplification::simplification`, constraint_simplification.rs:442).
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const RS_ABI_VERSION: c_int = 6;
+pub const RS_ABI_VERSION: c_int = 7;
 pub const RS_COMM_ID_BYTES: usize = 128;
 
 pub const RS_OK: c_int = 0;
@@ -65,6 +65,9 @@ pub struct rs_output {
     pub n_log: u64,
     pub log_from: *mut u32,
     pub log_to: rs_lc,
+    pub a_end: *mut u64,
+    pub b_end: *mut u64,
+    pub c_end: *mut u64,
 }
 
 /// the component DAG rs_flatten_dag expands (dag/src/lib.rs Node / Edge).

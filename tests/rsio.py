@@ -16,7 +16,7 @@ import pyref as R  # noqa: E402
 
 sys.path.insert(0, ROOT)
 from circom_cvm_amd.abi import (PRIME_IDS, U64_MAX, RsFlags, RsInput, RsLc, RsOutput,  # noqa: E402
-                                RsStats, make_flags)
+                                RsStats, block_csr, make_flags)
 
 
 def flags(level="O2", rounds=None, old=False, device=0, log=False) -> RsFlags:
@@ -74,14 +74,11 @@ class InputHolder:
         self.inp = inp
 
 
-def _read_block(b: RsLc) -> List[dict]:
+def _read_block(b: RsLc, end=None) -> List[dict]:
     n = b.n_rows
     if n == 0:
         return []
-    ptr = np.ctypeslib.as_array(b.ptr, shape=(n + 1,))
-    nnz = int(ptr[n])
-    col = np.ctypeslib.as_array(b.col, shape=(max(nnz, 1),))
-    val = np.ctypeslib.as_array(b.val, shape=(max(nnz, 1) * 4,))
+    ptr, col, val = _lc_arrays(b, end)
     out = []
     for r in range(n):
         m = {}
@@ -96,7 +93,7 @@ def _read_block(b: RsLc) -> List[dict]:
 
 def output_to_py(o: RsOutput):
     """-> (list of pyref.Con, signal_map dict label->wire, n_wires, no_private_inputs_witness)."""
-    a, b, c = _read_block(o.a), _read_block(o.b), _read_block(o.c)
+    a, b, c = (_read_block(*o.block(q)) for q in range(3))
     cons = [R.Con(a[i], b[i], c[i]) for i in range(o.n_constraints)]
     l2w = np.ctypeslib.as_array(o.label_to_wire, shape=(max(o.n_labels, 1),))[: o.n_labels]
     sm = {i: int(w) for i, w in enumerate(l2w) if w >= 0}
@@ -296,23 +293,16 @@ def gen_system(seed: int, p: int, n_sig: int = 60, n_rows: int = 80, n_out: int 
 
 
 # --------------------------------------------------------------------------- array comparison
-def _lc_arrays(b: RsLc):
-    n = int(b.n_rows)
-    if n == 0:
-        return np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint64)
-    ptr = np.ctypeslib.as_array(b.ptr, shape=(n + 1,)).copy()
-    nnz = int(ptr[n])
-    col = np.ctypeslib.as_array(b.col, shape=(max(nnz, 1),))[:nnz].copy()
-    val = np.ctypeslib.as_array(b.val, shape=(max(nnz, 1) * 4,))[:4 * nnz].copy()
-    return ptr, col, val
+def _lc_arrays(b: RsLc, end=None):
+    return block_csr(b, end)
 
 
 def output_arrays(o: RsOutput):
     """All arrays of an rs_output, copied (numpy): for size-independent comparisons at full size."""
     d = {"n_constraints": int(o.n_constraints), "n_wires": int(o.n_wires),
          "npiw": int(o.no_private_inputs_witness), "n_labels": int(o.n_labels)}
-    for nm in ("a", "b", "c"):
-        d[nm] = _lc_arrays(getattr(o, nm))
+    for q, nm in enumerate(("a", "b", "c")):
+        d[nm] = _lc_arrays(*o.block(q))
     d["l2w"] = np.ctypeslib.as_array(o.label_to_wire, shape=(max(int(o.n_labels), 1),))[: int(o.n_labels)].copy()
     return d
 

@@ -115,3 +115,29 @@ def test_hosthost_unsorted_long_rows():
         v[s:e] = v[s:e][perm]
     got = rsio.output_arrays(engine().simplify(h.inp, rsio.flags("O2")))
     assert rsio.diff_output_arrays(got, ref) is None
+
+
+@pytest.mark.parametrize("kind,rows,prime", [(0, 400_000, "bn128"), (2, 200_000, "bls12381"), (5, 300_000, "bn128")])
+def test_hosthost_streamed_layout(kind, rows, prime):
+    """rs_engine_simplify streams the storage rows final after round 1 while later rounds run (ABI 7
+    row ends): every row lies inside col / val, the compacted rows equal the oracle's, the rows a
+    round >= 3 reaches after all (chain: 8 rounds) are taken from the late region, and
+    rs_engine_fetch of the same result is the compact CSR."""
+    inp = M.Input.synth(kind, rows, 5, prime)
+    pin = M.PinnedInput(inp.c)
+    fl = rsio.flags("O2")
+    o = engine().simplify(pin.c, fl)
+    got = rsio.output_arrays(o)
+    n = int(o.n_constraints)
+    for q in range(3):
+        lc, end = o.block(q)
+        assert end is not None, "a run with storage rows streams"
+        beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,))
+        e = np.ctypeslib.as_array(end, shape=(n,))
+        assert (beg[:n] <= e).all() and (e <= int(lc.nnz)).all() and int(beg[n]) == int(lc.nnz)
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
+    assert rsio.diff_output_arrays(got, ref) is None
+    out = engine().fetch()
+    assert not out.c.a_end and not out.c.b_end and not out.c.c_end
+    assert rsio.diff_output_arrays(rsio.output_arrays(out.c), ref) is None
+    pin.free()

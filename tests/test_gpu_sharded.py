@@ -96,6 +96,21 @@ def test_sharded_synth_arrays(kind, rows, world):
     assert len({st.n_substitutions for _, st in outs}) == 1  # every rank holds the whole map
 
 
+@pytest.mark.parametrize("kind,rows,prime,world", [(2, 1_500_000, "bn128", 4), (0, 2_000_000, "bls12381", 8)])
+def test_sharded_baseline_configs(kind, rows, prime, world):
+    """The sharded forms BASELINE.json names: configs[3] (the ECDSA stand-in, deep chains, 1.5 M rows)
+    dealt over 4 ranks and configs[4]'s --prime bls12381 over 8 ranks (2 M rows of the mixed
+    circuit), every rank array for array equal to the single-GPU oracle."""
+    inp = M.Input.synth(kind, rows, 3, prime)
+    fl = rsio.flags("O2")
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
+    outs = sharded_run(inp.c, fl, world, arrays=True)
+    for r, (got, st) in enumerate(outs):
+        assert rsio.diff_output_arrays(got, ref) is None, f"rank {r}/{world}"
+        assert st.world == world and st.exchange_bytes > 0
+    assert len({st.n_substitutions for _, st in outs}) == 1
+
+
 def test_simplify_multi_one_device_listed_twice():
     """rs_simplify_multi (the one-shot entry point) with device 0 listed twice: in-process transport."""
     sys_ = rsio.gen_system(77, R.PRIMES["bn128"], n_sig=300, n_rows=250, big_cluster=700)

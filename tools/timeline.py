@@ -1,22 +1,46 @@
-"""Prints the kernel timeline of the last rs_engine_run in a rocprofv3 --kernel-trace csv (one step of
-bench.py): start offset, duration and queue of every kernel above a threshold.
-usage: python3 tools/timeline.py <kernel_trace.csv> [min_ms]"""
+"""Kernel + copy timeline of rs_engine calls from a rocprofv3 --kernel-trace [--memory-copy-trace]
+csv pair: the trace is cut into calls at idle gaps, and one call is printed as start offset,
+duration, stream and name of every kernel / copy above a threshold, plus per-stream busy time.
+usage: python3 tools/timeline.py <prefix_or_kernel_trace.csv> [--call N] [--min-ms T] [--gap-ms G]"""
+import argparse
 import csv
-import sys
+import os
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-thr = float(sys.argv[2]) if len(sys.argv) > 2 else 0.15
-rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-names = [r["Kernel_Name"].split("(")[0].replace("void ", "")[:44] for r in rows]
-starts = [i for i, n in enumerate(names) if n == "rs::k_mark_list"]
-firsts = [starts[0]] + [b for a, b in zip(starts, starts[1:]) if b - a > 20]
-a = firsts[-1]
-T0 = int(rows[a]["Start_Timestamp"])
-end = 0
-for r, n in zip(rows[a:], names[a:]):
-    s = (int(r["Start_Timestamp"]) - T0) / 1e6
-    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-    end = max(end, (int(r["End_Timestamp"]) - T0) / 1e6)
-    if d >= thr:
-        print(f"{s:8.2f} {d:7.2f} q{r['Queue_Id']} {n} grid={r['Grid_Size_X']}")
-print(f"end {end:.2f} ms")
+ap = argparse.ArgumentParser()
+ap.add_argument("trace")
+ap.add_argument("--call", type=int, default=-1, help="which call (default: the last)")
+ap.add_argument("--min-ms", type=float, default=0.15)
+ap.add_argument("--gap-ms", type=float, default=4.0)
+args = ap.parse_args()
+
+kt = args.trace if args.trace.endswith(".csv") else args.trace + "_kernel_trace.csv"
+ct = kt.replace("_kernel_trace.csv", "_memory_copy_trace.csv")
+ev = []  # (start, end, stream, name)
+for r in csv.DictReader(open(kt)):
+    ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "s" + r["Stream_Id"],
+               r["Kernel_Name"].split("(")[0].replace("void ", "")[:48] + f" g={r['Grid_Size_X']}"))
+if os.path.exists(ct):
+    for r in csv.DictReader(open(ct)):
+        d = r["Direction"].replace("MEMORY_COPY_", "")
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "s" + r["Stream_Id"], "copy " + d))
+ev.sort()
+calls, cur, last_end = [], [], None
+for e in ev:
+    if last_end is not None and e[0] - last_end > args.gap_ms * 1e6 and cur:
+        calls.append(cur)
+        cur = []
+    cur.append(e)
+    last_end = e[1] if last_end is None else max(last_end, e[1])
+if cur:
+    calls.append(cur)
+print(f"{len(calls)} calls: " + " ".join(f"{(c[-1][1] - c[0][0]) / 1e6:.1f}ms/{len(c)}" for c in calls))
+call = calls[args.call]
+T0 = call[0][0]
+busy = {}
+for s, e, q, n in call:
+    busy.setdefault(q, 0)
+    busy[q] += e - s
+    if (e - s) / 1e6 >= args.min_ms:
+        print(f"{(s - T0) / 1e6:8.2f} {(e - s) / 1e6:7.2f} {q:>4} {n}")
+end = max(e for _, e, _, _ in call)
+print(f"end {(end - T0) / 1e6:.2f} ms; busy per stream: " + ", ".join(f"{q} {v / 1e6:.1f}" for q, v in sorted(busy.items())))
