@@ -89,7 +89,7 @@ def shard_seed(seed: int, rank: int) -> int:
 
 
 KERNELS = (  # (name, stats fields: ms, bytes, launches)
-    ("k_big_main_lds (head)", "head_main_ms", "head_main_bytes", "head_launches"),
+    ("k_big_spec<8> (head)", "head_main_ms", "head_main_bytes", "head_launches"),
     ("k_big_main<256> (tail)", "tail_main_ms", "tail_main_bytes", "tail_launches"),
     ("k_frames_wave<0> (non-linear)", "apply_kernel_ms", "apply_bytes", "apply_kernel_launches"),
     ("k_frames_wave<1> (rounds)", "round_fill_ms", "round_fill_bytes", "round_fill_launches"),
@@ -105,7 +105,11 @@ def pmc_traffic():
         return {}, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d.get("bytes_per_launch", {}), os.path.relpath(files[-1], ROOT)
+    tab = {k: {"per_launch": v, "per_step": d.get("bytes_per_step", {}).get(k),
+               "launches_per_step": d.get("launches_per_step", {}).get(k)}
+           for k, v in d.get("bytes_per_launch", {}).items()}
+    src = os.path.relpath(files[-1], ROOT) + (f" @ {d['commit']}" if d.get("commit") else "")
+    return tab, src
 
 
 class _Con:  # the .a / .b / .c shape circom_cvm_amd.Dag reads
@@ -331,10 +335,18 @@ def main():
             per_s = (ms / 1000.0) / max(n, 1)
             per_b = by / max(n, 1)
             ach = per_b / per_s / 1e9 if per_s > 0 else 0.0
-            return {"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
-                    "avg_launch_ms": round(per_s * 1000.0, 4), "alg_bytes_per_launch": int(per_b),
-                    "launches_per_step": n / K, "ms_per_step": round(ms / K, 3),
-                    "traffic": traffic_tab.get(k)}
+            tr = traffic_tab.get(k) or {}
+            r = {"achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6),
+                 "avg_launch_ms": round(per_s * 1000.0, 4), "alg_bytes_per_launch": int(per_b),
+                 "launches_per_step": n / K, "ms_per_step": round(ms / K, 3),
+                 "traffic": tr.get("per_launch")}
+            if tr.get("per_step") is not None:
+                # per step, so a launch-count difference cannot skew the ratio; the profile's own
+                # launch count is reported beside this run's
+                r["traffic_per_step"] = tr["per_step"]
+                r["traffic_launches_per_step"] = tr.get("launches_per_step")
+                r["traffic_over_alg"] = round(tr["per_step"] / max(by / K, 1.0), 3)
+            return r
         dom = kline(k_name)
         path_ach = tot["alg_bytes"] / K / (ms_step / 1000.0) / 1e9
         line = {
@@ -350,6 +362,9 @@ def main():
                        "constraints": n_rows, "parallelism": f"clusters{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "kernel": k_name, "achieved": dom["achieved"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic"],
+                         "traffic_per_step": dom.get("traffic_per_step"),
+                         "traffic_launches_per_step": dom.get("traffic_launches_per_step"),
+                         "traffic_over_alg": dom.get("traffic_over_alg"),
                          "traffic_source": traffic_src, "avg_launch_ms": dom["avg_launch_ms"],
                          "alg_bytes_per_launch": dom["alg_bytes_per_launch"],
                          "launches_per_step": dom["launches_per_step"],

@@ -2717,6 +2717,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           w.err = d_fw_err;
           w.bytes = ra.bytes;
           HC(hipMemsetAsync(w.n_big, 0, 8, st));
+#ifdef RS_FWCLK
+          w.clk = A.get<unsigned long long>("fw.clkr", 32);
+          HC(hipMemsetAsync(w.clk, 0, 8 * 32, st));
+#endif
           RoundArgs rb = ra, rt = ra;
           rb.rlist = w.big; rb.n_rlist = w.n_big;
           rt.rlist = w.turn_list; rt.n_rlist = w.n_turn;
@@ -2726,6 +2730,17 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
             unsigned nbig = 0;
             HC(hipMemcpyAsync(&nbig, w.n_big, 4, hipMemcpyDeviceToHost, st));
             HC(hipStreamSynchronize(st));
+#ifdef RS_FWCLK
+            if (g_prof_env) {
+              unsigned long long c[32];
+              HC(hipMemcpy(c, w.clk, sizeof c, hipMemcpyDeviceToHost));
+              fprintf(stderr, "[rs-prof] round frames clocks (Mcycles summed over waves): groups %.1f entries %.1f terms %.1f "
+                      "rank %.1f emit %.1f rows %.1f plan %.1f | batches %llu, wave total %.1f over %llu waves | emit: loads %.1f "
+                      "values %.1f sync %.1f stores %.1f | %u rows over a batch of %llu\n", c[0] / 1e6, c[1] / 1e6, c[2] / 1e6,
+                      c[3] / 1e6, c[5] / 1e6, c[6] / 1e6, c[7] / 1e6, c[8], c[9] / 1e6, c[10], c[16] / 1e6, c[17] / 1e6,
+                      c[18] / 1e6, c[19] / 1e6, nbig, (unsigned long long)ra.n_ids);
+            }
+#endif
             if (nbig) {
               const uint64_t nseg = 3ull * nbig;
               uint64_t *xc = A.get<uint64_t>("x.cnt", nseg), *xo = A.get<uint64_t>("x.off", nseg + 1);

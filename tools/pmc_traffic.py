@@ -4,9 +4,11 @@ the bytes of wide streaming reads, so it is doubled; WRITE_SIZE is taken as is. 
 both counters in KiB.
 
 usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> -o profiles/roundN_pmc_traffic.json
-           [--wrreq <dir of a TCC_EA0_WRREQ / TCC_EA0_WRREQ_64B pass>]
-The JSON's `bytes_per_launch` keys are bench.py's KERNELS names; bench.py reads the newest
-profiles/round*_pmc_traffic.json into roofline.traffic."""
+           [--wrreq <dir of a TCC_EA0_WRREQ / TCC_EA0_WRREQ_64B pass>] [--steps K] [--commit SHA]
+The JSON's `bytes_per_launch` / `bytes_per_step` / `launches_per_step` keys are bench.py's KERNELS
+names (the passes run `bench.py --steps K --warmup 0`, so dispatches / K = launches per step of the
+profiled code); bench.py reads the newest profiles/round*_pmc_traffic.json into roofline.traffic and
+reports the profile's launch count beside its own, so a version skew between the two shows."""
 import argparse
 import csv
 import glob
@@ -16,7 +18,7 @@ import sys
 
 # bench.py KERNELS name -> substring of the rocprofv3 kernel name
 GROUPS = {
-    "k_big_main_lds (head)": "k_big_main_lds",
+    "k_big_spec<8> (head)": "k_big_spec<",
     "k_big_main<256> (tail)": "k_big_main<256u>",
     "k_frames_wave<0> (non-linear)": "k_frames_wave<0>",
     "k_frames_wave<1> (rounds)": "k_frames_wave<1>",
@@ -46,6 +48,8 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("-o", "--out", required=True)
     ap.add_argument("--wrreq", default=None)
+    ap.add_argument("--steps", type=int, default=1, help="bench steps of each pass (warmup 0)")
+    ap.add_argument("--commit", default=None, help="git commit the profiled tree was at")
     args = ap.parse_args()
     fe = per_dispatch(args.fetch_dir, "FETCH_SIZE")
     wr = per_dispatch(args.write_dir, "WRITE_SIZE")
@@ -53,7 +57,8 @@ def main():
     req64 = per_dispatch(args.wrreq, "TCC_EA0_WRREQ_64B_sum") if args.wrreq else {}
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of "
                      "`bench.py --steps 1 --warmup 0 --no-cpu`; FETCH_SIZE x2 (gfx950), KiB -> bytes",
-           "bytes_per_launch": {}, "detail": {}}
+           "commit": args.commit, "steps": args.steps,
+           "bytes_per_launch": {}, "bytes_per_step": {}, "launches_per_step": {}, "detail": {}}
     for name, pat in GROUPS.items():
         f, nf = group_avg(fe, pat)
         w, nw = group_avg(wr, pat)
@@ -62,6 +67,8 @@ def main():
         fetch = 2.0 * f * 1024.0
         write = w * 1024.0
         res["bytes_per_launch"][name] = int(fetch + write)
+        res["bytes_per_step"][name] = int((fetch + write) * nf / args.steps)
+        res["launches_per_step"][name] = nf / args.steps
         det = {"fetch_bytes_x2": int(fetch), "write_bytes": int(write), "dispatches": [nf, nw]}
         r, _ = group_avg(req, pat)
         r64, _ = group_avg(req64, pat)
