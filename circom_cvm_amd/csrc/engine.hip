@@ -1290,7 +1290,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         hipLaunchKernelGGL(k_normalize, dim3(16, g), dim3(256), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
-        hipLaunchKernelGGL(k_big_finish<8>, dim3(g), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_big_finish<8>, dim3(g), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head, 0u);
         HC(hipGetLastError());
         // the Kahn levels and the emission follow once the rest is enqueued (the level loop waits)
       }
@@ -1364,7 +1364,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           ats.cf_nbig = E->A.get<unsigned long long>("cft.nbig", 2);
           HC(hipMemsetAsync(ats.cf_n, 0, 24, E->st));
           HC(hipMemsetAsync(ats.cf_nbig, 0, 16, E->st));
-          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, ats, ids, n_tail);
+          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, ats, ids, n_tail, 0u);
           HC(hipGetLastError());
           tl.ah = ats;
           tl.ids = ids;
@@ -1376,7 +1376,11 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           tl.ev = E->ev_lvlt;
           tl.run(kTailLevels, false);
         } else {
-          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
+          // clusters of kFinWaveBelow rows and more by the workgroup, the rest one wave each (most
+          // compose chains: the level latency, not the lanes, is their cost); RS_FIN_WAVE_BELOW
+          // overrides the threshold (0: every cluster by a workgroup)
+          static const uint32_t wb = getenv("RS_FIN_WAVE_BELOW") ? (uint32_t)atoi(getenv("RS_FIN_WAVE_BELOW")) : kFinWaveBelow;
+          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail, wb);
           HC(hipGetLastError());
         }
       }

@@ -14,9 +14,10 @@
 //   rank     lane-per-term: a term's position in its group's sorted order = its index in its own run
 //            plus, per other run of the group (each run is sorted: a right-hand side or one entry), a
 //            binary search; ties between runs broken by run order, so the ranks are a permutation
-//   emit     lane-per-position over the sorted order: the first term of each key sums the values of
-//            its run of equal keys (coefficient x right-hand-side coefficient, Montgomery products);
-//            output slots from a scan of the key heads, so consecutive lanes write consecutive
+//            (groups of many runs: pairwise merge rounds, fw_rank_rounds)
+//   emit     lane-per-position over the sorted order: every term's value (coefficient x right-hand-
+//            side coefficient, Montgomery products), runs of equal keys summed by a segmented scan;
+//            output slots from a scan of the run ends, so consecutive lanes write consecutive
 //            (key, value) slots of a group: coalesced stores, each output written once
 // Sorting the union of the terms and summing equal keys equals the reference's sequence of frames
 // (each frame a sort + combine + drop zeros): the per-key sums are the same field elements.
@@ -36,6 +37,7 @@ constexpr uint32_t kFwG = 192;            // groups: 64 rows x 3 linear combinat
 constexpr uint32_t kFwPT = kFwT / 64;     // terms per lane
 constexpr uint32_t kFwPE = kFwE / 64;     // entries per lane
 constexpr uint32_t kFwWaves = 4;          // waves per workgroup (each with its own LDS slice)
+constexpr uint32_t kFwRunsRank = 8;       // groups of more runs than this rank by merge rounds
 #ifndef FW_KB
 #define FW_KB 2                            // emit: sorted positions per lane whose loads go together
 #endif
@@ -166,13 +168,6 @@ __device__ __forceinline__ Fe fw_combine(const FieldP &F, uint32_t kd, const Fe 
   const Fe p = fmul(F, c, m);
   return kd == 4 ? fneg(F, p) : p;
 }
-__device__ inline Fe fw_term_value(const FrameWaveArgs &A, const FwLds &L, uint32_t t) {
-  const uint32_t src = L.tsrc[t], e = src >> 10;
-  Fe c, m;
-  fw_operands(A, L, e, src & 1023, c, m);
-  return fw_combine(A.fr.F, L.e_kind[e] & 15, c, m);
-}
-
 // ---- the stages after the entries (shared by the main pass and the fix pass)
 
 // keys of the terms (lane = every 64th term: consecutive lanes on consecutive right-hand-side entries,
@@ -236,6 +231,63 @@ __device__ inline void fw_rank(FwLds &L, uint32_t lane, uint32_t n_t) {
   }
 }
 
+// The same ranks by pairwise merge rounds, for groups of many runs (fw_rank costs a binary search per
+// other run and term): in round r every segment of 2^r consecutive runs of a group is sorted, and each
+// pair of neighbouring segments merges -- a term's place in the merged segment is its offset in its own
+// plus, in the partner segment, the count of keys below it (the left segment first on equal keys).
+// Segments keep the position ranges of their runs, so only the keys move (registers -> LDS each round);
+// ceil(log2 runs) rounds of one search each.
+__device__ inline void fw_rank_rounds(FwLds &L, uint32_t lane, uint32_t n_t, uint32_t rounds) {
+  uint32_t key[kFwPT], q[kFwPT];
+#pragma unroll
+  for (uint32_t k = 0; k < kFwPT; ++k) {
+    const uint32_t t = lane + 64 * k;
+    key[k] = t < n_t ? L.tkey[t] : 0u;
+    q[k] = t;
+  }
+  for (uint32_t r = 0; r < rounds; ++r) {
+    uint32_t nq[kFwPT];
+#pragma unroll
+    for (uint32_t k = 0; k < kFwPT; ++k) {
+      const uint32_t t = lane + 64 * k;
+      nq[k] = q[k];
+      if (t >= n_t) continue;
+      const uint32_t e = L.tsrc[t] >> 10, g = L.e_grp[e], e0 = L.g_e0[g], R = L.g_e0[g + 1] - e0, i = e - e0;
+      const uint32_t S = i >> r, P = S ^ 1u;
+      if ((P << r) >= R) continue;  // no partner segment this round
+      uint32_t a = L.e_t0[e0 + (P << r)], b = L.e_t0[e0 + min((P + 1) << r, R)];
+      const uint32_t os = L.e_t0[e0 + (S << r)], ms = L.e_t0[e0 + ((S & ~1u) << r)], lo = a;
+      if (S < P) {  // left: partner keys below
+        while (a < b) {
+          const uint32_t mid = (a + b) >> 1;
+          if (L.tkey[mid] < key[k]) a = mid + 1; else b = mid;
+        }
+      } else {      // right: partner keys up to and including
+        while (a < b) {
+          const uint32_t mid = (a + b) >> 1;
+          if (L.tkey[mid] <= key[k]) a = mid + 1; else b = mid;
+        }
+      }
+      nq[k] = ms + (q[k] - os) + (a - lo);
+    }
+    wave_sync();
+#pragma unroll
+    for (uint32_t k = 0; k < kFwPT; ++k) {
+      if (lane + 64 * k < n_t) L.tkey[nq[k]] = key[k];
+      q[k] = nq[k];
+    }
+    wave_sync();
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kFwPT; ++k) {
+    const uint32_t t = lane + 64 * k;
+    if (t < n_t) {
+      L.tkey[t] = key[k];  // back to term order (emit reads keys by term)
+      L.perm[q[k]] = (uint16_t)t;
+    }
+  }
+}
+
 // non-zero key heads before sorted position q (from the emit ballots)
 __device__ __forceinline__ uint32_t fw_nz_before(const FwLds &L, uint32_t q) {
   return L.nzp[q >> 6] + (uint32_t)__popcll(L.nzm[q >> 6] & fw_below(q & 63));
@@ -244,12 +296,14 @@ __device__ __forceinline__ uint32_t fw_glen(const FwLds &L, uint32_t g) {
   return fw_nz_before(L, L.g_t0[g + 1]) - fw_nz_before(L, L.g_t0[g]);
 }
 
-// Emit (lane = every 64th sorted position: consecutive lanes write consecutive slots).  A key head (the
-// first position of its key in the group) sums its run of equal keys; zero sums are dropped -- the
-// pool keeps the zero-valued entries of the reference's maps ({0: 0} from
-// initialize_hashmap_for_expression, algebra.rs:1279-1294, and cancellations), so they are common.
-// Output slots: ballots of the non-zero heads per 64 positions (nzm) and their running count (nzp).
-// Blocks of kB positions per lane have all their loads in flight before any product or store.
+// Emit (lane = every 64th sorted position: consecutive lanes write consecutive slots).  Every position
+// computes its term's value (all of a block's loads in flight together); a run of equal keys is summed
+// by a segmented scan over the block's 64 lanes (a carry moves a run on into the next block), so a key
+// that many right-hand sides share costs log 64 steps, not a serial walk of its run.  The last position
+// of a run emits the sum unless it is zero -- the pool keeps the zero-valued entries of the reference's
+// maps ({0: 0} from initialize_hashmap_for_expression, algebra.rs:1279-1294, and cancellations), so
+// zero sums are common.  Output slots: ballots of the emitting positions per 64 positions (nzm) and
+// their running count (nzp).
 __device__ inline void fw_emit(const FrameWaveArgs &A, FwLds &L, uint32_t lane, uint32_t n_t
 #ifdef RS_FWCLK
                                , unsigned long long *clk_acc, unsigned long long &clk_last
@@ -258,16 +312,16 @@ __device__ inline void fw_emit(const FrameWaveArgs &A, FwLds &L, uint32_t lane, 
   const FieldP &F = A.fr.F;
   constexpr uint32_t kB = FW_KB;
   static_assert(kFwPT % kB == 0, "emit blocks");
-  uint32_t before = 0;  // non-zero heads in the blocks done
+  uint32_t before = 0;  // emitted positions in the blocks done
+  Fe carry = fe_zero();  // the running sum of a run that goes on past the block before
 #pragma unroll
   for (uint32_t kb = 0; kb < kFwPT; kb += kB) {
     Fe c[kB], m[kB];
-    uint32_t key[kB], kd[kB], gg[kB], run[kB], pp[kB];
+    uint32_t key[kB], kd[kB], gg[kB], fl[kB];  // fl: bit 0 valid, 1 run start, 2 run end
 #pragma unroll
     for (uint32_t k = 0; k < kB; ++k) {
       const uint32_t p = lane + 64 * (kb + k);
-      pp[k] = p;
-      run[k] = 0;
+      fl[k] = 0;
       kd[k] = 0;
       key[k] = 0;
       gg[k] = 0;
@@ -275,31 +329,43 @@ __device__ inline void fw_emit(const FrameWaveArgs &A, FwLds &L, uint32_t lane, 
         const uint32_t t = L.perm[p], src = L.tsrc[t], e = src >> 10, g = L.e_grp[e];
         key[k] = L.tkey[t];
         gg[k] = g;
-        if (p == L.g_t0[g] || L.tkey[L.perm[p - 1]] != key[k]) {
-          const uint32_t end = L.g_t0[g + 1];
-          uint32_t q = p + 1;
-          while (q < end && L.tkey[L.perm[q]] == key[k]) ++q;
-          run[k] = q - p;
-          kd[k] = L.e_kind[e] & 15;
-          fw_operands(A, L, e, src & 1023, c[k], m[k]);
-        }
+        const bool st = p == L.g_t0[g] || L.tkey[L.perm[p - 1]] != key[k];
+        const bool en = p + 1 == L.g_t0[g + 1] || L.tkey[L.perm[p + 1]] != key[k];
+        fl[k] = 1u | (st ? 2u : 0u) | (en ? 4u : 0u);
+        kd[k] = L.e_kind[e] & 15;
+        fw_operands(A, L, e, src & 1023, c[k], m[k]);
       }
     }
     FW_WAIT();
     FW_CLK(16);
     uint64_t nz[kB];
-    // one value per block slot; written out per slot (not a loop) so the arrays stay in registers
-    auto value = [&](Fe &v, const Fe &mv, uint32_t kdv, uint32_t runv, uint32_t pv_) -> bool {
-      if (!runv) return false;
-      v = fw_combine(F, kdv, v, mv);
-      for (uint32_t q = 1; q < runv; ++q) v = fadd(F, v, fw_term_value(A, L, L.perm[pv_ + q]));
-      return !fe_is_zero(v);
+    // one block's sums; written out per slot (not a loop) so the arrays stay in registers
+    auto sums = [&](Fe &v, const Fe &mv, uint32_t kdv, uint32_t f) -> uint64_t {
+      v = (f & 1) ? fw_combine(F, kdv, v, mv) : fe_zero();
+      if (lane == 0 && (f & 3) == 1) v = fadd(F, v, carry);
+      if (__ballot(lane > 0 && (f & 3) == 1)) {  // a run crosses lanes: segmented inclusive scan
+        bool hd = (f & 3) != 1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          Fe y;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) y.l[w] = __shfl_up(v.l[w], d);
+          const bool yh = __shfl_up(hd ? 1 : 0, d) != 0;
+          if ((int)lane >= d) {
+            if (!hd) v = fadd(F, v, y);
+            hd = hd || yh;
+          }
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) carry.l[w] = __shfl(v.l[w], 63);
+      return __ballot((f & 5) == 5 && !fe_is_zero(v));
     };
-    static_assert(kB <= 5, "value() is applied to at most five slots");
-#define FW_VALUE(i) \
-  if constexpr (kB > i) nz[i] = __ballot(value(c[i], m[i], kd[i], run[i], pp[i]));
-    FW_VALUE(0) FW_VALUE(1) FW_VALUE(2) FW_VALUE(3) FW_VALUE(4)
-#undef FW_VALUE
+    static_assert(kB <= 5, "sums() is applied to at most five slots");
+#define FW_SUMS(i) \
+  if constexpr (kB > i) nz[i] = sums(c[i], m[i], kd[i], fl[i]);
+    FW_SUMS(0) FW_SUMS(1) FW_SUMS(2) FW_SUMS(3) FW_SUMS(4)
+#undef FW_SUMS
 #pragma unroll
     for (uint32_t k = 0; k < kB; ++k) {
       if (lane == 0) {
@@ -526,7 +592,16 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
   fw_terms(A, L, lane, n_e, n_t);
   wave_sync();
   FW_CLK(2);
-  fw_rank(L, lane, n_t);
+  uint32_t rmax = max(n0, max(n1, n2));  // the most runs in one group of the batch
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d));
+  if (rmax > kFwRunsRank) {
+    uint32_t rounds = 0;
+    while ((1u << rounds) < rmax) ++rounds;
+    fw_rank_rounds(L, lane, n_t, rounds);
+  } else {
+    fw_rank(L, lane, n_t);
+  }
   wave_sync();
   FW_CLK(3);
   FW_EMIT(n_t);

@@ -2455,28 +2455,6 @@ __global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t 
   }
 }
 
-// block-wide exclusive scan (256 lanes) of a[0..n) in global memory; s_part: 4 words of LDS
-__device__ inline uint32_t blk_excl_scan(uint32_t *a, uint32_t n, uint32_t *s_part) {
-  const uint32_t tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6;
-  uint32_t per = (n + nt - 1) / nt, lo = min(n, tid * per), hi = min(n, lo + per);
-  uint32_t sum = 0;
-  for (uint32_t i = lo; i < hi; ++i) sum += a[i];
-  uint32_t x = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d);
-    if ((int)lane >= d) x += y;
-  }
-  if (lane == 63) s_part[w] = x;
-  __syncthreads();
-  uint32_t base = 0, total = 0;
-  for (uint32_t q = 0; q < nt / 64; ++q) { if (q < w) base += s_part[q]; total += s_part[q]; }
-  uint32_t acc = base + x - sum;
-  for (uint32_t i = lo; i < hi; ++i) { uint32_t t = a[i]; a[i] = acc; acc += t; }
-  __syncthreads();
-  return total;
-}
-
 // multi_inv (modular_arithmetic.rs:71-91) of the pivot coefficients of every workgroup cluster,
 // before normalisation: one block per cluster, each lane inverts chunks of 64 slots with one
 // inversion per chunk (Montgomery's trick), so no cluster waits on an inversion chain of its own.
@@ -2611,6 +2589,178 @@ __device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t s
 
 
 constexpr uint32_t kComposeCap = 256;  // entries one wave composes in LDS
+constexpr uint32_t kFinWaveBelow = 512;  // tail clusters under this many rows finish on one wave (k_big_finish)
+
+// Composition of slot `sl` by one wave as a k-way merge of sorted runs (every dependency already
+// final; the same result as d_compose_wave): run 0 = the slot's own (non-deleted) entries, run 1 + j =
+// R(t_j) of its j-th deleted key, scaled by c_j at read time.  Each run is sorted by key, so an
+// element's place in the sorted union is its index in its run plus, per other run, a binary search
+// of its key (ties: the earlier run first); the first run holding a key is its head and sums the
+// equal keys of the later runs.  Only the keys live in LDS (values are read where they lie), so the
+// cost per element is D searches, not a sort: a chain link (D = 1, a long R(t)) composes in
+// O(E / 64) instead of bitonic passes or a lane-serial merge.
+// Scratch: K[KCAP] keys, OI[OCAP] own entry -> RHS index, RS[DCAP + 2] run starts, DOF[DCAP] /
+// DMU[DCAP] dependency offsets / coefficients, HB[KCAP / 64] head bits, HP[KCAP / 64 + 1] prefixes.
+// Returns 0 on success, 1 when the lists do not fit (caller falls back), 2 on pool exhaustion.
+struct MergeScratch {
+  uint32_t *K;
+  uint16_t *OI;
+  uint32_t *RS;
+  uint64_t *DOF;
+  Fe *DMU;
+  uint64_t *HB;
+  uint32_t *HP;
+};
+template <uint32_t KCAP, uint32_t OCAP, uint32_t DCAP>
+__device__ inline int d_compose_merge(const ElimArgs &A, Alloc &al, uint64_t sl, const MergeScratch &M,
+                                      unsigned long long &by) {
+  static_assert(KCAP % 64 == 0 && KCAP / 64 <= 4096, "merge scratch");
+  const FieldP &F = A.F;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? ((1ull << lane) - 1ull) : 0ull;
+  const uint64_t off = A.h_off[sl];
+  const uint32_t len = A.h_len[sl];
+  if (len > OCAP + DCAP) return 1;
+  // pass 1: own entries (their RHS index) and dependencies (offset, length prefix, coefficient)
+  uint32_t n_own = 0, D = 0, tot = 0;
+  for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    int32_t hs = -1;
+    uint32_t dl = 0;
+    if (i < len) {
+      hs = A.holder_idx[A.pk[off + i]];
+      if (hs >= 0) dl = A.h_len[hs];
+    }
+    const uint64_t dm = __ballot(hs >= 0), om = __ballot(i < len && hs < 0);
+    uint32_t x = dl;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if ((int)lane >= d) x += y;
+    }
+    const uint32_t ctot = __shfl(x, 63), nd = (uint32_t)__popcll(dm), no = (uint32_t)__popcll(om);
+    if (n_own + no > OCAP || D + nd > DCAP || n_own + no + tot + ctot > KCAP) return 1;
+    if (hs >= 0) {
+      const uint32_t r = D + (uint32_t)__popcll(dm & lt);
+      M.RS[1 + r] = tot + x - dl;  // made absolute below
+      M.DOF[r] = A.h_off[hs];
+      M.DMU[r] = A.pv[off + i];
+    } else if (i < len) {
+      M.OI[n_own + (uint32_t)__popcll(om & lt)] = (uint16_t)i;
+    }
+    n_own += no;
+    D += nd;
+    tot += ctot;
+  }
+  const uint32_t E = n_own + tot, W = (E + 63) / 64;
+  if (D > 16 && E <= kComposeCap) return 1;  // many runs, few entries: d_compose_wave's sort is cheaper
+  wave_sync();
+  for (uint32_t j = lane; j < D; j += 64) M.RS[1 + j] += n_own;
+  if (lane == 0) {
+    M.RS[0] = 0;
+    M.RS[D + 1] = E;
+  }
+  for (uint32_t w = lane; w < W; w += 64) M.HB[w] = 0;
+  wave_sync();
+  // the keys of every run, concatenated (consecutive lanes on consecutive entries of a run)
+  for (uint32_t x = lane; x < E; x += 64) {
+    if (x < n_own) {
+      M.K[x] = A.pk[off + M.OI[x]];
+    } else {
+      uint32_t lo = 1, hi = D + 1;  // the run: last j with RS[j] <= x
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (M.RS[mid] <= x) lo = mid; else hi = mid;
+      }
+      M.K[x] = A.pk[M.DOF[lo - 1] + (x - M.RS[lo])];
+    }
+  }
+  wave_sync();
+  // an element's run, its sorted rank, and whether it heads its key (pass 2: head bits; pass 3: output)
+  auto locate = [&](uint32_t x, uint32_t &a, uint32_t &rank, bool &head) {
+    uint32_t lo = 0, hi = D + 1;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (M.RS[mid] <= x) lo = mid; else hi = mid;
+    }
+    a = lo;
+    const uint32_t k = M.K[x];
+    rank = x - M.RS[a];
+    head = true;
+    for (uint32_t b = 0; b <= D; ++b) {
+      if (b == a) continue;
+      uint32_t s = M.RS[b], e = M.RS[b + 1];
+      const uint32_t s0 = s;
+      if (b < a) {  // elements <= k
+        while (s < e) {
+          const uint32_t m = (s + e) >> 1;
+          if (M.K[m] <= k) s = m + 1; else e = m;
+        }
+        if (s > s0 && M.K[s - 1] == k) head = false;
+      } else {  // elements < k
+        while (s < e) {
+          const uint32_t m = (s + e) >> 1;
+          if (M.K[m] < k) s = m + 1; else e = m;
+        }
+      }
+      rank += s - s0;
+    }
+  };
+  for (uint32_t x = lane; x < E; x += 64) {
+    uint32_t a, rank;
+    bool head;
+    locate(x, a, rank, head);
+    if (head) atomicOr((unsigned long long *)&M.HB[rank >> 6], 1ull << (rank & 63));
+  }
+  wave_sync();
+  uint32_t run_tot = 0;
+  for (uint32_t w0 = 0; w0 < W; w0 += 64) {  // word prefixes of the head bits
+    const uint32_t w = w0 + lane;
+    const uint32_t c = w < W ? (uint32_t)__popcll(M.HB[w]) : 0u;
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if ((int)lane >= d) x += y;
+    }
+    if (w < W) M.HP[w] = run_tot + x - c;
+    run_tot += __shfl(x, 63);
+  }
+  uint64_t o = 0;
+  if (lane == 0) o = pool_alloc(A, al, run_tot ? run_tot : 1);
+  o = __shfl(o, 0);
+  if (o == RS_NONE) return 2;
+  wave_sync();
+  auto value = [&](uint32_t run, uint32_t x) -> Fe {
+    if (run == 0) return A.pv[off + M.OI[x]];
+    return fmul(F, M.DMU[run - 1], A.pv[M.DOF[run - 1] + (x - M.RS[run])]);
+  };
+  for (uint32_t x = lane; x < E; x += 64) {
+    uint32_t a, rank;
+    bool head;
+    locate(x, a, rank, head);
+    if (!head) continue;
+    const uint32_t k = M.K[x];
+    Fe v = value(a, x);
+    for (uint32_t b = a + 1; b <= D; ++b) {  // the equal keys of the later runs
+      uint32_t s = M.RS[b], e = M.RS[b + 1];
+      while (s < e) {
+        const uint32_t m = (s + e) >> 1;
+        if (M.K[m] < k) s = m + 1; else e = m;
+      }
+      if (s < M.RS[b + 1] && M.K[s] == k) v = fadd(F, v, value(b, s));
+    }
+    const uint32_t slot = M.HP[rank >> 6] + (uint32_t)__popcll(M.HB[rank >> 6] & ((1ull << (rank & 63)) - 1ull));
+    A.pk[o + slot] = k;
+    A.pv[o + slot] = v;
+  }
+  if (lane == 0) {
+    A.h_off[sl] = o;
+    A.h_len[sl] = run_tot;
+    by += 36ull * (len + tot + run_tot);
+  }
+  return 0;
+}
 
 // Composition of slot `sl` by one wave (every dependency already final): the result is the sum of
 // the slot's non-deleted entries and c_t * R(t) for each deleted key t (coefficient c_t), with
@@ -2712,6 +2862,29 @@ __device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, 
     by += 36ull * (len + tot + run);
   }
   return 0;
+}
+
+// the per-wave composition buffers of k_big_finish / k_compose_level, seen as d_compose_merge scratch
+__device__ __forceinline__ MergeScratch merge_scratch_small(uint64_t *S, Fe *V, uint32_t *dex, uint64_t *dof, Fe *dmu) {
+  MergeScratch M;
+  M.K = (uint32_t *)V;                     // 256 Fe = 2,048 keys
+  M.OI = (uint16_t *)S;                    // 512 own entries (1 KB)
+  M.HB = S + 128;                          // 32 words
+  M.HP = (uint32_t *)(S + 160);            // 33 prefixes
+  M.RS = dex;                              // 64 run starts
+  M.DOF = dof;
+  M.DMU = dmu;
+  return M;
+}
+constexpr uint32_t kMergeK = 2048, kMergeO = 512, kMergeD = 62;
+// one composition by one wave: the k-way merge, else the bitonic sort; 1 = neither fits (the caller
+// falls back), 2 = pool exhausted
+__device__ inline int d_compose_wave_any(const ElimArgs &A, Alloc &al, uint64_t sl, uint64_t *S, Fe *V, uint32_t *dex,
+                                         uint64_t *dof, Fe *dmu, unsigned long long &by) {
+  const int rc = d_compose_merge<kMergeK, kMergeO, kMergeD>(A, al, sl, merge_scratch_small(S, V, dex, dof, dmu), by);
+  if (rc != 1) return rc;
+  wave_sync();
+  return d_compose_wave(A, al, sl, S, V, dex, dof, dmu, by);
 }
 
 // d_compose_wave for right-hand sides of up to LCAP entries composing to up to ECAP entries: the
@@ -2818,170 +2991,238 @@ __device__ inline int d_compose_wave_big(const ElimArgs &A, Alloc &al, uint64_t 
   return 0;
 }
 
-template <int NW>  // waves per workgroup
-__global__ __launch_bounds__(64 * NW) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+// k_big_finish's per-cluster work, by a team of NT threads (a workgroup, or one wave: NT = 64):
+// team-scoped barriers and scans, the team's scalars in `T`, one composition buffer set per wave.
+struct FinTeam {
+  uint32_t ok, nf, part[16];
+  uint64_t scr;
+  unsigned long long hsum, hmax;
+};
+template <uint32_t NT>
+__device__ __forceinline__ void team_sync() {
+  if constexpr (NT == 64) wave_sync();
+  else __syncthreads();
+}
+// exclusive scan of a[0..n) in place by the team; returns the total
+template <uint32_t NT>
+__device__ inline uint32_t team_excl_scan(uint32_t *a, uint32_t n, FinTeam &T, uint32_t tid) {
+  const uint32_t lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (n + NT - 1) / NT, lo = min(n, tid * per), hi = min(n, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += a[i];
+  uint32_t x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if ((int)lane >= d) x += y;
+  }
+  if (lane == 63) T.part[w] = x;
+  team_sync<NT>();
+  uint32_t base = 0, total = 0;
+  for (uint32_t q = 0; q < NT / 64; ++q) { if (q < w) base += T.part[q]; total += T.part[q]; }
+  uint32_t acc = base + x - sum;
+  for (uint32_t i = lo; i < hi; ++i) { const uint32_t t = a[i]; a[i] = acc; acc += t; }
+  team_sync<NT>();
+  return total;
+}
+struct FinBufs {  // the composition buffers of wave 0 of the workgroup; wave w's are w strides on
+  uint64_t *S;    // kComposeCap per wave
+  Fe *V;          // kComposeCap
+  uint32_t *dex;  // 64
+  uint64_t *dof;  // 64
+  Fe *dmu;        // 64
+};
+template <uint32_t NT>
+__device__ inline void d_finish_cluster(const ElimArgs &A, Alloc &al, uint64_t ci, uint64_t c, uint32_t tid, FinTeam &T,
+                                        const FinBufs &bufs, uint32_t wave0, unsigned long long &by_el,
+                                        unsigned long long &by_fin) {
   const FieldP &F = A.F;
-  __shared__ uint32_t s_ok, s_nf, s_part[NW];
+  constexpr uint32_t nt = NT;
+  const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
+  const uint32_t n = (uint32_t)(e - b);
+  const uint32_t m = A.n_sub[c];
+  unsigned long long t_2 = wall_clock64();
+  unsigned long long by = 0;  // algorithmic bytes of this lane
+  if (tid == 0) T.ok = 1;
+  // ---- normalize_substitutions (:414-437): the inverses come from k_batch_inv (split clusters:
+  // k_normalize did it over the whole GPU)
+  for (uint32_t i = tid; i < (A.split ? 0u : m); i += nt) {
+    const Fe inv_i = A.ftmp[b + i];
+    Fe *vv = A.pv + A.h_off[b + i];
+    for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
+    by += 64ull * (A.h_len[b + i] + 1);
+  }
+  team_sync<NT>();
+  unsigned long long t_3 = wall_clock64();
+  // ---- composition over the dependency DAG in Kahn order: a substitution is composed once every
+  // deleted key of its right-hand side is final (the result does not depend on the order).
+  // scratch (u32): deg[m], dcnt[m+1], dfill[m], frontier[2][m], dependents[sum deg]
+  if (tid == 0) {
+    T.scr = pool_alloc_global(A, 6ull * m + 8);
+    if (T.scr == RS_NONE) T.ok = 0;
+    if (A.split) A.cf_done[ci] = 0;
+  }
+  team_sync<NT>();
+  uint32_t levels = 0;
+  if (A.split && !(T.ok && m)) {  // nothing to compose: k_big_emit still finishes the cluster
+    if (tid == 0 && !T.ok) atomicOr(A.err, 8);
+    by_fin += by;
+    team_sync<NT>();
+    return;
+  }
+  if (T.ok && m) {
+    uint32_t *deg = A.pk + T.scr, *dcnt = deg + m, *dfill = dcnt + m + 1, *fr0 = dfill + m, *fr1 = fr0 + m;
+    for (uint32_t i = tid; i < m; i += nt) { deg[i] = 0; dcnt[i] = 0; dfill[i] = 0; }
+    if (tid == 0) { dcnt[m] = 0; T.nf = 0; }
+    team_sync<NT>();
+    for (uint32_t i = tid; i < m; i += nt) {
+      const uint32_t *kk = A.pk + A.h_off[b + i];
+      uint32_t len = A.h_len[b + i], d = 0;
+      for (uint32_t t = 0; t < len; ++t) {
+        int32_t hs = A.holder_idx[kk[t]];
+        if (hs >= 0) { ++d; atomicAdd(&dcnt[hs - b], 1u); }
+      }
+      deg[i] = d;
+      if (!d) fr0[atomicAdd(&T.nf, 1u)] = i;
+    }
+    team_sync<NT>();
+    const uint32_t n_edges = team_excl_scan<NT>(dcnt, m + 1, T, tid);
+    if (tid == 0) {
+      T.scr = pool_alloc_global(A, (uint64_t)n_edges + 1);
+      if (T.scr == RS_NONE) T.ok = 0;
+    }
+    team_sync<NT>();
+    if (T.ok) {
+      uint32_t *dl = A.pk + T.scr;
+      for (uint32_t i = tid; i < m; i += nt) {
+        if (!deg[i]) continue;
+        const uint32_t *kk = A.pk + A.h_off[b + i];
+        uint32_t len = A.h_len[b + i];
+        for (uint32_t t = 0; t < len; ++t) {
+          int32_t hs = A.holder_idx[kk[t]];
+          if (hs >= 0) { uint32_t q = (uint32_t)(hs - b); dl[dcnt[q] + atomicAdd(&dfill[q], 1u)] = i; }
+        }
+      }
+      team_sync<NT>();
+      if (A.split) {  // hand the DAG and the first frontier to k_compose_level
+        const uint32_t nf0 = T.nf;
+        if (tid == 0) {
+          A.cf_deg[ci] = (uint64_t)(deg - A.pk);
+          A.cf_dl[ci] = T.scr;
+          A.cf_done[ci] = nf0;
+          T.scr = atomicAdd(A.cf_n, (unsigned long long)nf0);
+        }
+        team_sync<NT>();
+        for (uint32_t f = tid; f < nf0; f += nt) A.cf_items[T.scr + f] = ((uint64_t)ci << 32) | fr0[f];
+        by_fin += by;
+        team_sync<NT>();
+        return;  // team-uniform: k_big_emit finishes the cluster
+      }
+      uint32_t nf = T.nf, done = nf;
+      uint32_t *cur = fr0, *nxt = fr1;
+      while (nf && T.ok) {
+        team_sync<NT>();
+        if (tid == 0) T.nf = 0;
+        team_sync<NT>();
+        for (uint32_t f = tid; f < nf; f += nt) {
+          uint32_t q = cur[f];
+          for (uint32_t t = dcnt[q]; t < dcnt[q + 1]; ++t) {
+            uint32_t d = dl[t];
+            if (atomicSub(&deg[d], 1u) == 1u) nxt[atomicAdd(&T.nf, 1u)] = d;
+          }
+        }
+        team_sync<NT>();
+        nf = T.nf;
+        {  // one wave per substitution of the frontier
+          const uint32_t wv_ = tid >> 6, nw = nt >> 6;
+          const uint32_t bw = wave0 + wv_;  // this wave's buffers
+          uint64_t *bS = bufs.S + bw * kComposeCap, *bdof = bufs.dof + bw * 64;
+          Fe *bV = bufs.V + bw * kComposeCap, *bdmu = bufs.dmu + bw * 64;
+          uint32_t *bdex = bufs.dex + bw * 64;
+          for (uint32_t f = wv_; f < nf; f += nw) {
+            const uint64_t sl = b + nxt[f];
+            const int rc = d_compose_wave_any(A, al, sl, bS, bV, bdex, bdof, bdmu, by);
+            if (rc == 2) { if ((tid & 63) == 0) T.ok = 0; continue; }
+            if (rc == 1 && (tid & 63) == 0 && !d_compose_serial(A, al, sl, by)) T.ok = 0;
+            wave_sync();
+          }
+        }
+        done += nf;
+        ++levels;
+        uint32_t *t = cur; cur = nxt; nxt = t;
+        team_sync<NT>();  // T.ok is read by every lane in the loop condition
+      }
+      team_sync<NT>();
+      if (T.ok && done != m) { if (tid == 0) { T.ok = 0; atomicOr(A.err, 32); } }
+    }
+  }
+  team_sync<NT>();
+  // ---- emit, reset the dense scratch
+  for (uint32_t i = tid; i < m; i += nt) {
+    uint32_t s = A.h_sig[b + i];
+    A.holder_idx[s] = -1;
+    A.del[s] = 0;
+    A.sub_of[s] = (int32_t)(b + i);
+    A.deleted[s] = 1;
+  }
+  const uint32_t *touch = A.pk + A.big_touch_off[ci];
+  for (uint32_t t = tid; t < A.big_touch_n[ci]; t += nt) A.occ[touch[t]] = -1;
+  uint64_t rows_e = 0, subs_e = 0;
+  uint32_t hmax = 0;
+  for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
+  for (uint32_t i = tid; i < m; i += nt) { subs_e += A.h_len[b + i]; hmax = max(hmax, A.h_len[b + i]); }
+  by_el += 36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0);
+  by_fin += by;
+  if (A.prof) {
+    if (tid == 0) { T.hsum = 0; T.hmax = 0; }
+    team_sync<NT>();
+    atomicAdd(&T.hsum, (unsigned long long)subs_e);
+    atomicMax(&T.hmax, (unsigned long long)hmax);
+    team_sync<NT>();
+  }
+  if (tid == 0) {
+    if (!T.ok) atomicOr(A.err, 8);
+    if (A.prof) {
+      unsigned long long *P = A.prof + kProfWords * ci;
+      P[1] = m; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3; P[20] = levels;
+    }
+  }
+  team_sync<NT>();
+}
+
+// normalize + compose + emit of every listed cluster.  Clusters of at least `wave_below` rows (a prefix
+// of the size-ordered list) take a whole workgroup each; the rest one wave each -- most of them compose
+// chains (one substitution per Kahn level), where the level latency, not the lanes, is the cost, so
+// NW clusters of a workgroup advance at once.  wave_below = 0: every cluster by the workgroup.
+template <int NW>  // waves per workgroup
+__global__ __launch_bounds__(64 * NW, 3) void k_big_finish(ElimArgs A, const uint32_t *ids, uint64_t n_ids,
+                                                        uint32_t wave_below = 0) {
+  static_assert(NW <= 16, "FinTeam.part");
+  __shared__ FinTeam s_team[NW];
   __shared__ uint64_t cw_S[NW][kComposeCap];  // per-wave composition buffers
   __shared__ Fe cw_V[NW][kComposeCap];
   __shared__ uint32_t cw_dex[NW][64];
   __shared__ uint64_t cw_dof[NW][64];
   __shared__ Fe cw_dmu[NW][64];
-  __shared__ uint64_t s_scr;
-  __shared__ unsigned long long s_hsum, s_hmax;
-  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  const uint32_t tid = threadIdx.x, wv = tid >> 6;
+  const FinBufs bufs{cw_S[0], cw_V[0], cw_dex[0], cw_dof[0], cw_dmu[0]};
   Alloc al;
   al.chunk = 128;
   unsigned long long by_el = 0, by_fin = 0;  // this lane's algorithmic bytes (one atomic per wave at the end)
-  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
-    const uint64_t c = ids[ci];
-    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
-    const uint32_t n = (uint32_t)(e - b);
-    const uint32_t m = A.n_sub[c];
-    unsigned long long t_2 = wall_clock64();
-    unsigned long long by = 0;  // algorithmic bytes of this lane
-    if (tid == 0) s_ok = 1;
-    // ---- normalize_substitutions (:414-437): the inverses come from k_batch_inv (split clusters:
-    // k_normalize did it over the whole GPU)
-    for (uint32_t i = tid; i < (A.split ? 0u : m); i += nt) {
-      const Fe inv_i = A.ftmp[b + i];
-      Fe *vv = A.pv + A.h_off[b + i];
-      for (uint32_t t = 0; t < A.h_len[b + i]; ++t) vv[t] = fmul(F, vv[t], inv_i);
-      by += 64ull * (A.h_len[b + i] + 1);
+  // the list is ordered largest first: the workgroup part is the prefix of clusters >= wave_below rows
+  uint64_t split = n_ids;
+  if (wave_below) {
+    uint64_t lo = 0, hi = n_ids;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1, c = ids[mid];
+      if (A.cl_off[c + 1] - A.cl_off[c] >= wave_below) lo = mid + 1; else hi = mid;
     }
-    __syncthreads();
-    unsigned long long t_3 = wall_clock64();
-    // ---- composition over the dependency DAG in Kahn order: a substitution is composed once every
-    // deleted key of its right-hand side is final (the result does not depend on the order).
-    // scratch (u32): deg[m], dcnt[m+1], dfill[m], frontier[2][m], dependents[sum deg]
-    if (tid == 0) {
-      s_scr = pool_alloc_global(A, 6ull * m + 8);
-      if (s_scr == RS_NONE) s_ok = 0;
-      if (A.split) A.cf_done[ci] = 0;
-    }
-    __syncthreads();
-    uint32_t levels = 0;
-    if (A.split && !(s_ok && m)) {  // nothing to compose: k_big_emit still finishes the cluster
-      if (tid == 0 && !s_ok) atomicOr(A.err, 8);
-      by_fin += by;
-      __syncthreads();
-      continue;
-    }
-    if (s_ok && m) {
-      uint32_t *deg = A.pk + s_scr, *dcnt = deg + m, *dfill = dcnt + m + 1, *fr0 = dfill + m, *fr1 = fr0 + m;
-      for (uint32_t i = tid; i < m; i += nt) { deg[i] = 0; dcnt[i] = 0; dfill[i] = 0; }
-      if (tid == 0) { dcnt[m] = 0; s_nf = 0; }
-      __syncthreads();
-      for (uint32_t i = tid; i < m; i += nt) {
-        const uint32_t *kk = A.pk + A.h_off[b + i];
-        uint32_t len = A.h_len[b + i], d = 0;
-        for (uint32_t t = 0; t < len; ++t) {
-          int32_t hs = A.holder_idx[kk[t]];
-          if (hs >= 0) { ++d; atomicAdd(&dcnt[hs - b], 1u); }
-        }
-        deg[i] = d;
-        if (!d) fr0[atomicAdd(&s_nf, 1u)] = i;
-      }
-      __syncthreads();
-      const uint32_t n_edges = blk_excl_scan(dcnt, m + 1, s_part);
-      if (tid == 0) {
-        s_scr = pool_alloc_global(A, (uint64_t)n_edges + 1);
-        if (s_scr == RS_NONE) s_ok = 0;
-      }
-      __syncthreads();
-      if (s_ok) {
-        uint32_t *dl = A.pk + s_scr;
-        for (uint32_t i = tid; i < m; i += nt) {
-          if (!deg[i]) continue;
-          const uint32_t *kk = A.pk + A.h_off[b + i];
-          uint32_t len = A.h_len[b + i];
-          for (uint32_t t = 0; t < len; ++t) {
-            int32_t hs = A.holder_idx[kk[t]];
-            if (hs >= 0) { uint32_t q = (uint32_t)(hs - b); dl[dcnt[q] + atomicAdd(&dfill[q], 1u)] = i; }
-          }
-        }
-        __syncthreads();
-        if (A.split) {  // hand the DAG and the first frontier to k_compose_level
-          const uint32_t nf0 = s_nf;
-          if (tid == 0) {
-            A.cf_deg[ci] = (uint64_t)(deg - A.pk);
-            A.cf_dl[ci] = s_scr;
-            A.cf_done[ci] = nf0;
-            s_scr = atomicAdd(A.cf_n, (unsigned long long)nf0);
-          }
-          __syncthreads();
-          for (uint32_t f = tid; f < nf0; f += nt) A.cf_items[s_scr + f] = ((uint64_t)ci << 32) | fr0[f];
-          by_fin += by;
-          __syncthreads();
-          continue;  // block-uniform: k_big_emit finishes the cluster
-        }
-        uint32_t nf = s_nf, done = nf;
-        uint32_t *cur = fr0, *nxt = fr1;
-        while (nf && s_ok) {
-          __syncthreads();
-          if (tid == 0) s_nf = 0;
-          __syncthreads();
-          for (uint32_t f = tid; f < nf; f += nt) {
-            uint32_t q = cur[f];
-            for (uint32_t t = dcnt[q]; t < dcnt[q + 1]; ++t) {
-              uint32_t d = dl[t];
-              if (atomicSub(&deg[d], 1u) == 1u) nxt[atomicAdd(&s_nf, 1u)] = d;
-            }
-          }
-          __syncthreads();
-          nf = s_nf;
-          {  // one wave per substitution of the frontier
-            const uint32_t wv_ = tid >> 6, nw = nt >> 6;
-            for (uint32_t f = wv_; f < nf; f += nw) {
-              const uint64_t sl = b + nxt[f];
-              const int rc = d_compose_wave(A, al, sl, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
-              if (rc == 2) { if ((tid & 63) == 0) s_ok = 0; continue; }
-              if (rc == 1 && (tid & 63) == 0 && !d_compose_serial(A, al, sl, by)) s_ok = 0;
-              wave_sync();
-            }
-          }
-          done += nf;
-          ++levels;
-          uint32_t *t = cur; cur = nxt; nxt = t;
-          __syncthreads();  // s_ok is read by every lane in the loop condition
-        }
-        __syncthreads();
-        if (s_ok && done != m) { if (tid == 0) { s_ok = 0; atomicOr(A.err, 32); } }
-      }
-    }
-    __syncthreads();
-    // ---- emit, reset the dense scratch
-    for (uint32_t i = tid; i < m; i += nt) {
-      uint32_t s = A.h_sig[b + i];
-      A.holder_idx[s] = -1;
-      A.del[s] = 0;
-      A.sub_of[s] = (int32_t)(b + i);
-      A.deleted[s] = 1;
-    }
-    const uint32_t *touch = A.pk + A.big_touch_off[ci];
-    for (uint32_t t = tid; t < A.big_touch_n[ci]; t += nt) A.occ[touch[t]] = -1;
-    uint64_t rows_e = 0, subs_e = 0;
-    uint32_t hmax = 0;
-    for (uint32_t pos = tid; pos < n; pos += nt) rows_e += A.rows.len[A.perm[b + pos]];
-    for (uint32_t i = tid; i < m; i += nt) { subs_e += A.h_len[b + i]; hmax = max(hmax, A.h_len[b + i]); }
-    by_el += 36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0);
-    by_fin += by;
-    if (A.prof) {
-      if (tid == 0) { s_hsum = 0; s_hmax = 0; }
-      __syncthreads();
-      atomicAdd(&s_hsum, (unsigned long long)subs_e);
-      atomicMax(&s_hmax, (unsigned long long)hmax);
-      __syncthreads();
-    }
-    if (tid == 0) {
-      if (!s_ok) atomicOr(A.err, 8);
-      if (A.prof) {
-        unsigned long long *P = A.prof + kProfWords * ci;
-        P[1] = m; P[6] = t_3 - t_2; P[7] = wall_clock64() - t_3; P[20] = levels;
-      }
-    }
-    __syncthreads();
+    split = lo;
   }
+  for (uint64_t ci = blockIdx.x; ci < split; ci += gridDim.x)
+    d_finish_cluster<64 * NW>(A, al, ci, ids[ci], tid, s_team[0], bufs, 0, by_el, by_fin);
+  for (uint64_t ci = split + (uint64_t)blockIdx.x * NW + wv; ci < n_ids; ci += (uint64_t)gridDim.x * NW)
+    d_finish_cluster<64>(A, al, ci, ids[ci], tid & 63, s_team[wv], bufs, wv, by_el, by_fin);
   wave_atomic_add(A.bytes, by_el);
   wave_atomic_add(A.bytes_fin, by_fin);
 }
@@ -3016,7 +3257,7 @@ __global__ __launch_bounds__(64 * NW) void k_compose_level(ElimArgs A, const uin
     const uint64_t b = A.cl_off[c];
     const uint32_t m = A.n_sub[c];
     if (level > 0) {
-      const int rc = d_compose_wave(A, al, b + q, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
+      const int rc = d_compose_wave_any(A, al, b + q, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
       if (rc == 2 && lane == 0) atomicOr(A.err, 8);
       if (rc == 1) {  // too long for this wave's LDS: k_compose_big composes it and releases its dependents
         if (lane == 0) A.cf_big[atomicAdd(A.cf_nbig, 1ull)] = item;
@@ -3059,7 +3300,19 @@ __global__ __launch_bounds__(64) void k_compose_big(ElimArgs A, const uint32_t *
     const uint32_t c = ids[ci];
     const uint64_t b = A.cl_off[c];
     const uint32_t m = A.n_sub[c];
-    const int rc = d_compose_wave_big<ECAP, LCAP>(A, al, b + q, S, V, dex, dof, dmu, by);
+    MergeScratch ms;
+    ms.K = (uint32_t *)V;                  // 16,384 keys
+    ms.OI = (uint16_t *)S;                 // 4,096 own entries
+    ms.HB = S + 1024;                      // 256 words
+    ms.HP = (uint32_t *)(S + 1280);        // 257 prefixes
+    ms.RS = dex;
+    ms.DOF = dof;
+    ms.DMU = dmu;
+    int rc = d_compose_merge<16 * ECAP / 2, 4096, LCAP - 2>(A, al, b + q, ms, by);
+    if (rc == 1) {
+      wave_sync();
+      rc = d_compose_wave_big<ECAP, LCAP>(A, al, b + q, S, V, dex, dof, dmu, by);
+    }
     if (rc == 2 && lane == 0) atomicOr(A.err, 8);
     if (rc == 1 && lane == 0 && !d_compose_serial(A, al, b + q, by)) atomicOr(A.err, 8);
     wave_sync();
