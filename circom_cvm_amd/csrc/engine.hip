@@ -927,6 +927,17 @@ struct LevelLoop {
   }
 };
 
+// Kahn levels of the head's composition launched over the whole GPU before k_compose_rest takes the
+// rest per cluster (RS_HEAD_GPU_LEVELS; "all": every level over the GPU, the host loop until empty)
+static uint32_t head_gpu_levels() {
+  static const uint32_t v = [] {
+    const char *e = getenv("RS_HEAD_GPU_LEVELS");
+    if (e && !strcmp(e, "all")) return UINT32_MAX;
+    const uint32_t k = e ? (uint32_t)atoi(e) : 8u;
+    return k < 1 ? 1u : k;  // level 0's items need no composition: k_compose_rest starts after it
+  }();
+  return v;
+}
 static uint64_t head_limit() {
   static const uint64_t v = [] {
     const char *hd = getenv("RS_HEAD");
@@ -1206,6 +1217,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.pool_top = P.top;
     a.pool_cap = P.cap;
     a.err = d_err;
+    // compositions sort unless the sort cannot take them (RS_COMPOSE=merge: also merge the short ones
+    // with at most four dependencies -- 45 % slower on the metric circuit's tail, equal on templated)
+    static const bool compose_merge = getenv("RS_COMPOSE") && !strcmp(getenv("RS_COMPOSE"), "merge");
+    a.compose_sort = compose_merge ? 0 : 1;
     // in-kernel algorithmic-byte counters: [0] k_eliminate / composition emits, [1] / [2] the head's
     // k_big_main / normalisation + composition, [3] / [4] the tail's
     a.bytes = E->A.get<unsigned long long>("el.bytes", 5);
@@ -1286,7 +1301,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         else hipLaunchKernelGGL(k_big_spec<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
-        hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        // one inversion per head cluster (RS_HEAD_INV=chains: k_batch_inv, one per 16 pivots)
+        static const bool inv_chains = getenv("RS_HEAD_INV") && !strcmp(getenv("RS_HEAD_INV"), "chains");
+        if (inv_chains) hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        else hipLaunchKernelGGL(k_batch_inv_tree, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         hipLaunchKernelGGL(k_normalize, dim3(16, g), dim3(256), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -1394,7 +1412,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hl.n_slots = n_slots;
         hl.h = E->h_lvl;
         hl.ev = E->ev_lvl;
-        if (overlap && W == 1) hl.run(kHeadLevels, false);
+        if (overlap && W == 1) hl.run(std::min(head_gpu_levels(), kHeadLevels), false);
       }
       if (tail_split && n_tail) {
         tl.run(UINT32_MAX, true);
@@ -1409,7 +1427,14 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       }
       if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
       if (n_head) {
-        hl.run(UINT32_MAX, true);
+        // the first (wide) Kahn levels over the whole GPU, the rest in one workgroup per cluster
+        const uint32_t kg = head_gpu_levels();
+        hl.run(kg, kg == UINT32_MAX);
+        if (!hl.done && kg < UINT32_MAX) {
+          hipLaunchKernelGGL(k_compose_rest<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big,
+                             (const uint64_t *)hl.cur, (const unsigned long long *)(ah.cf_n + hl.level % 3), n_head);
+          HC(hipGetLastError());
+        }
         hipLaunchKernelGGL(k_big_emit<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[4], E->st2));

@@ -546,6 +546,7 @@ struct ElimArgs {
   // dependency DAG, k_compose_level composes one Kahn level of every cluster at a time over the
   // whole GPU, k_big_emit finishes
   int split;
+  int compose_sort;         // 1: compositions merge only where the sort cannot (0: RS_COMPOSE=merge)
   uint64_t *cf_items;         // the first frontier (cluster position << 32 | local slot)
   unsigned long long *cf_n;   // its length
   uint64_t *cf_deg, *cf_dl;   // per cluster: pool offsets of deg[m] (+ dcnt[m+1]) and of the dependents
@@ -2485,6 +2486,55 @@ __global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *i
     }
   }
 }
+// The same inverses with one Fermat inversion per cluster (one workgroup each): thread t takes a
+// contiguous chunk of the pivots, the chunks' products are scanned across the workgroup both ways
+// (prefix X_t, suffix S_t) in LDS, and the inverse of the whole product -- the only inversion --
+// gives every chunk the inverse of its running product (inv_T * S_{t+1}), from which the chunk walks
+// back as Montgomery's trick does.  A chain-per-lane k_batch_inv needs one inversion per 16 pivots
+// (hundreds of waves for the head's clusters, queued behind the tail's workgroups for CUs); this is
+// one inversion's latency per cluster.  ftmp[slot] <- h_coef[slot]^-1.
+__global__ __launch_bounds__(256) void k_batch_inv_tree(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
+  const FieldP &F = A.F;
+  __shared__ Fe s_x[256], s_y[256];
+  __shared__ Fe s_inv;
+  const uint32_t t = threadIdx.x;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c];
+    const uint32_t m = A.n_sub[c];
+    if (m == 0) continue;
+    const uint32_t per = (m + 255) / 256, c0 = min(m, t * per), c1 = min(m, c0 + per);
+    Fe acc = F.one;  // the chunk's running product, kept in ftmp
+    for (uint32_t i = c0; i < c1; ++i) {
+      acc = i == c0 ? A.h_coef[b + i] : fmul(F, acc, A.h_coef[b + i]);
+      A.ftmp[b + i] = acc;
+    }
+    // inclusive prefix (s_x) and suffix (s_y) products of the chunk totals
+    s_x[t] = acc;
+    s_y[t] = acc;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+      const Fe px = t >= d ? s_x[t - d] : F.one, py = t + d < 256 ? s_y[t + d] : F.one;
+      __syncthreads();
+      if (t >= d) s_x[t] = fmul(F, s_x[t], px);
+      if (t + d < 256) s_y[t] = fmul(F, s_y[t], py);
+      __syncthreads();
+    }
+    if (t == 0) s_inv = finv(F, s_x[255]);
+    __syncthreads();
+    if (c0 < c1) {
+      const Fe X = t ? s_x[t - 1] : F.one;                          // product before the chunk
+      Fe inv = t < 255 ? fmul(F, s_inv, s_y[t + 1]) : s_inv;            // (X * chunk product)^-1
+      for (uint32_t i = c1 - 1; i > c0; --i) {
+        const Fe h = A.h_coef[b + i];
+        A.ftmp[b + i] = fmul(F, fmul(F, X, A.ftmp[b + i - 1]), inv);  // prefix through i-1, over prefix through i
+        inv = fmul(F, inv, h);
+      }
+      A.ftmp[b + c0] = fmul(F, X, inv);
+    }
+    __syncthreads();
+  }
+}
 // normalize_substitutions (:414-437) of the split clusters: every RHS times its pivot's inverse,
 // one lane per substitution over a 2-D grid like k_batch_inv's
 __global__ __launch_bounds__(256) void k_normalize(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
@@ -2613,7 +2663,7 @@ struct MergeScratch {
 };
 template <uint32_t KCAP, uint32_t OCAP, uint32_t DCAP>
 __device__ inline int d_compose_merge(const ElimArgs &A, Alloc &al, uint64_t sl, const MergeScratch &M,
-                                      unsigned long long &by) {
+                                      unsigned long long &by, uint32_t sort_runs = ~0u, uint32_t sort_cap = 0) {
   static_assert(KCAP % 64 == 0 && KCAP / 64 <= 4096, "merge scratch");
   const FieldP &F = A.F;
   const uint32_t lane = threadIdx.x & 63;
@@ -2653,7 +2703,7 @@ __device__ inline int d_compose_merge(const ElimArgs &A, Alloc &al, uint64_t sl,
     tot += ctot;
   }
   const uint32_t E = n_own + tot, W = (E + 63) / 64;
-  if (D > 16 && E <= kComposeCap) return 1;  // many runs, few entries: d_compose_wave's sort is cheaper
+  if (D > sort_runs && E <= sort_cap) return 1;  // the caller's sort is cheaper for many short runs
   wave_sync();
   for (uint32_t j = lane; j < D; j += 64) M.RS[1 + j] += n_own;
   if (lane == 0) {
@@ -2769,7 +2819,8 @@ __device__ inline int d_compose_merge(const ElimArgs &A, Alloc &al, uint64_t sl,
 // dependency entry, spread over the lanes), bitonic-sorted by key, summed per key and written out.
 // Returns 0 on success, 1 when the lists do not fit (caller falls back), 2 on pool exhaustion.
 __device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, uint64_t *S, Fe *V,
-                                     uint32_t *dex, uint64_t *dof, Fe *dmu, unsigned long long &by) {
+                                     uint32_t *dex, uint64_t *dof, Fe *dmu, unsigned long long &by,
+                                     bool merge_few = false) {
   const FieldP &F = A.F;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t off = A.h_off[sl];
@@ -2799,6 +2850,7 @@ __device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, 
   const uint32_t tot = __shfl(x, 63), ex = x - dl;
   const uint32_t E = n_own + tot;
   if (E > kComposeCap) return 1;
+  if (merge_few && __popcll(dm) <= 4) return 3;  // few runs: d_compose_merge is cheaper
   if (hs >= 0) {
     const uint32_t r = (uint32_t)__popcll(dm & lt);
     dex[r] = ex;
@@ -2879,12 +2931,16 @@ __device__ __forceinline__ MergeScratch merge_scratch_small(uint64_t *S, Fe *V, 
 constexpr uint32_t kMergeK = 2048, kMergeO = 512, kMergeD = 62;
 // one composition by one wave: the k-way merge, else the bitonic sort; 1 = neither fits (the caller
 // falls back), 2 = pool exhausted
+// (a right-hand side of <= 64 entries composing to <= 256 sorts -- with compose_sort = 0 only when it
+// has more than four dependencies; the lists the sort cannot hold merge)
 __device__ inline int d_compose_wave_any(const ElimArgs &A, Alloc &al, uint64_t sl, uint64_t *S, Fe *V, uint32_t *dex,
                                          uint64_t *dof, Fe *dmu, unsigned long long &by) {
-  const int rc = d_compose_merge<kMergeK, kMergeO, kMergeD>(A, al, sl, merge_scratch_small(S, V, dex, dof, dmu), by);
-  if (rc != 1) return rc;
-  wave_sync();
-  return d_compose_wave(A, al, sl, S, V, dex, dof, dmu, by);
+  if (A.h_len[sl] <= 64) {
+    const int rc = d_compose_wave(A, al, sl, S, V, dex, dof, dmu, by, !A.compose_sort);
+    if (rc != 1 && rc != 3) return rc;
+    wave_sync();
+  }
+  return d_compose_merge<kMergeK, kMergeO, kMergeD>(A, al, sl, merge_scratch_small(S, V, dex, dof, dmu), by);
 }
 
 // d_compose_wave for right-hand sides of up to LCAP entries composing to up to ECAP entries: the
@@ -3308,7 +3364,7 @@ __global__ __launch_bounds__(64) void k_compose_big(ElimArgs A, const uint32_t *
     ms.RS = dex;
     ms.DOF = dof;
     ms.DMU = dmu;
-    int rc = d_compose_merge<16 * ECAP / 2, 4096, LCAP - 2>(A, al, b + q, ms, by);
+    int rc = d_compose_merge<16 * ECAP / 2, 4096, LCAP - 2>(A, al, b + q, ms, by, 16, ECAP);
     if (rc == 1) {
       wave_sync();
       rc = d_compose_wave_big<ECAP, LCAP>(A, al, b + q, S, V, dex, dof, dmu, by);
@@ -3324,6 +3380,69 @@ __global__ __launch_bounds__(64) void k_compose_big(ElimArgs A, const uint32_t *
         nxt[atomicAdd(n_nxt, 1ull)] = ((uint64_t)ci << 32) | d;
         atomicAdd(&A.cf_done[ci], 1u);
       }
+    }
+  }
+  wave_atomic_add(A.bytes_fin, by);
+}
+
+// The head's composition after its first (wide) Kahn levels: one workgroup per cluster continues the
+// levels in-kernel from the frontier k_compose_level left (its items for this cluster gathered from
+// `cur`), one wave per substitution, a workgroup barrier between levels -- the narrow deep levels
+// cost a barrier each instead of a launch.  Compositions too long for a wave's buffers fall back to
+// the lane-serial composition.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_compose_rest(ElimArgs A, const uint32_t *ids, const uint64_t *cur,
+                                                         const unsigned long long *n_cur, uint64_t n_ids) {
+  __shared__ uint64_t cw_S[NW][kComposeCap];
+  __shared__ Fe cw_V[NW][kComposeCap];
+  __shared__ uint32_t cw_dex[NW][64];
+  __shared__ uint64_t cw_dof[NW][64];
+  __shared__ Fe cw_dmu[NW][64];
+  __shared__ uint32_t s_nf;
+  const uint32_t tid = threadIdx.x, nt = 64 * NW, wv = tid >> 6, lane = tid & 63;
+  Alloc al;
+  al.chunk = 128;
+  unsigned long long by = 0;
+  const uint64_t n = *n_cur;
+  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    const uint64_t c = ids[ci];
+    const uint64_t b = A.cl_off[c];
+    const uint32_t m = A.n_sub[c];
+    if (m == 0) continue;  // block-uniform
+    uint32_t *deg = A.pk + A.cf_deg[ci], *dcnt = deg + m, *fr0 = dcnt + m + 1 + m, *fr1 = fr0 + m;
+    const uint32_t *dl = A.pk + A.cf_dl[ci];
+    if (tid == 0) s_nf = 0;
+    __syncthreads();
+    for (uint64_t f = tid; f < n; f += nt) {
+      const uint64_t item = cur[f];
+      if ((item >> 32) == ci) fr0[atomicAdd(&s_nf, 1u)] = (uint32_t)item;
+    }
+    __syncthreads();
+    uint32_t nf = s_nf;
+    uint32_t *cu = fr0, *nx = fr1;
+    while (nf) {
+      for (uint32_t f = wv; f < nf; f += NW) {
+        const uint64_t sl = b + cu[f];
+        const int rc = d_compose_wave_any(A, al, sl, cw_S[wv], cw_V[wv], cw_dex[wv], cw_dof[wv], cw_dmu[wv], by);
+        if (rc == 2 && lane == 0) atomicOr(A.err, 8);
+        if (rc == 1 && lane == 0 && !d_compose_serial(A, al, sl, by)) atomicOr(A.err, 8);
+        wave_sync();
+      }
+      __syncthreads();
+      if (tid == 0) s_nf = 0;
+      __syncthreads();
+      for (uint32_t f = tid; f < nf; f += nt) {
+        const uint32_t q = cu[f];
+        for (uint32_t t = dcnt[q]; t < dcnt[q + 1]; ++t) {
+          const uint32_t d = dl[t];
+          if (atomicSub(&deg[d], 1u) == 1u) nx[atomicAdd(&s_nf, 1u)] = d;
+        }
+      }
+      __syncthreads();
+      nf = s_nf;
+      if (tid == 0) atomicAdd(&A.cf_done[ci], nf);
+      uint32_t *t = cu; cu = nx; nx = t;
+      __syncthreads();
     }
   }
   wave_atomic_add(A.bytes_fin, by);
