@@ -31,8 +31,17 @@
 
 namespace rs {
 
-constexpr uint32_t kFwT = 640;            // terms per batch (A, B and C of its rows)
-constexpr uint32_t kFwE = 320;            // entries per batch
+#ifndef FW_T
+#define FW_T 640
+#endif
+#ifndef FW_E
+#define FW_E 320
+#endif
+#ifndef FW_OCC
+#define FW_OCC 2                           // waves per SIMD the launch bounds ask for
+#endif
+constexpr uint32_t kFwT = FW_T;           // terms per batch (A, B and C of its rows)
+constexpr uint32_t kFwE = FW_E;           // entries per batch
 constexpr uint32_t kFwG = 192;            // groups: 64 rows x 3 linear combinations
 constexpr uint32_t kFwPT = kFwT / 64;     // terms per lane
 constexpr uint32_t kFwPE = kFwE / 64;     // entries per lane
@@ -663,7 +672,7 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
 // kRound: 0 = the non-linear rows of round 1, 1 = the storage rows of rounds >= 2 (separate symbols so
 // profiles tell the two apart)
 template <int kRound>
-__global__ __launch_bounds__(256, 2) void k_frames_wave(FrameWaveArgs A) {
+__global__ __launch_bounds__(256, FW_OCC) void k_frames_wave(FrameWaveArgs A) {
   __shared__ FwLds lds[kFwWaves];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   FwLds &L = lds[wv];
