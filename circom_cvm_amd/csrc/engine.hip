@@ -949,6 +949,37 @@ static uint64_t head_limit() {
   }();
   return v;
 }
+// The arena replay of one cluster on the host (k_cl_replay_lane's walk): rows in index order, each
+// pair's previous row found by path halving and its root's list appended to the row's.  A serial
+// union-find of dependent accesses: ~20 ns a pair in a host cache against ~0.3 us in LDS, and the
+// largest clusters' replays gate the head's ordered loop.  qo: the cluster's per-row pair offsets
+// (n + 1, relative), st: its pairs, srow: its rows; out: the rows in list order.
+static void host_replay(uint32_t n, const uint64_t *qo, const uint32_t *st, const uint32_t *srow, uint32_t *out) {
+  std::vector<uint32_t> C2(n), T(n), N(n, RS_NONE);
+  for (uint32_t t = 0; t < n; ++t) {
+    C2[t] = t;
+    T[t] = t;
+    for (uint64_t q = qo[t]; q < qo[t + 1]; ++q) {
+      uint32_t p = st[q] & ~kClRowBit;
+      if (p == kClNoPrev) continue;
+      while (C2[p] != p) {
+        const uint32_t g = C2[C2[p]];
+        C2[p] = g;
+        p = g;
+      }
+      if (p == t) continue;
+      N[T[t]] = p;
+      T[t] = T[p];
+      C2[p] = t;
+    }
+  }
+  uint32_t x = n - 1, q = 0;
+  while (x != RS_NONE && q < n) {
+    out[q++] = srow[x];
+    x = N[x];
+  }
+}
+
 static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, const uint8_t *d_forb, ElimOut &eo) {
   Arena &A = E->A;
   hipStream_t st = E->st;
@@ -1027,8 +1058,80 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
          (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm, (const uint32_t *)n_ordered,
          old_heur);
   unsigned long long *rprof = nullptr;
-  if (hc[4]) {  // (kClMid, kClLds]: the largest LDS footprint, on the second stream (the few
-                // largest clusters' serial replays overlap everything else's)
+  // (kClMid, kClLds] on the host by default (RS_DEVICE_REPLAY: k_cl_replay_wave on the second stream)
+  static const bool dev_replay = getenv("RS_DEVICE_REPLAY") != nullptr;
+  if (hc[4] && !dev_replay) {
+    // launched first, so the device has the mid-size replays to do while the host replays
+    if (hc[2] > hc[4]) {
+      const uint64_t nm = hc[2] - hc[4];
+      hipLaunchKernelGGL((k_cl_replay_wave<kClMid>), dim3((unsigned)std::min<uint64_t>(nm, 16384)), dim3(64), 0, st,
+                         (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3] + hc[4]), nm,
+                         (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
+                         (const uint32_t *)n_ordered, old_heur);
+      HC(hipGetLastError());
+    }
+    const double th0 = now_ms();
+    // every input of the replays is complete (the stream was synchronised above): copy on stx
+    const uint64_t nh = hc[4];
+    std::vector<uint32_t> hid(nh), hord(nh);
+    eo.cl_off.resize(n_cl + 1);
+    HC(hipMemcpyAsync(hid.data(), sorted + hc[3], 4 * nh, hipMemcpyDeviceToHost, E->stx));
+    HC(hipMemcpyAsync(eo.cl_off.data(), D.cl_off, 8 * (n_cl + 1), hipMemcpyDeviceToHost, E->stx));
+    HC(hipStreamSynchronize(E->stx));
+    std::vector<uint64_t> qb(nh), qn(nh);  // each cluster's (first row's pair offset) and row count
+    uint64_t tot_q = 0, tot_n = 0;
+    for (uint64_t i = 0; i < nh; ++i) {
+      HC(hipMemcpyAsync(&hord[i], n_ordered + hid[i], 4, hipMemcpyDeviceToHost, E->stx));
+      qn[i] = eo.cl_off[hid[i] + 1] - eo.cl_off[hid[i]];
+      tot_n += qn[i];
+    }
+    std::vector<uint64_t> qo(tot_n + nh);
+    for (uint64_t i = 0, o = 0; i < nh; o += qn[i] + 1, ++i)
+      HC(hipMemcpyAsync(qo.data() + o, q_off + eo.cl_off[hid[i]], 8 * (qn[i] + 1), hipMemcpyDeviceToHost, E->stx));
+    HC(hipStreamSynchronize(E->stx));
+    for (uint64_t i = 0, o = 0; i < nh; o += qn[i] + 1, ++i) {
+      qb[i] = qo[o];
+      tot_q += qo[o + qn[i]] - qo[o];
+    }
+    std::vector<uint32_t> hst(tot_q), hsrow(tot_n), hperm(tot_n);
+    for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += qo[o + qn[i]] - qo[o], on += qn[i], o += qn[i] + 1, ++i) {
+      const uint64_t nq = qo[o + qn[i]] - qo[o];
+      if (nq) HC(hipMemcpyAsync(hst.data() + oq, stream + qb[i], 4 * nq, hipMemcpyDeviceToHost, E->stx));
+      HC(hipMemcpyAsync(hsrow.data() + on, srow + eo.cl_off[hid[i]], 4 * qn[i], hipMemcpyDeviceToHost, E->stx));
+    }
+    HC(hipStreamSynchronize(E->stx));
+    {  // one host thread per cluster (a few dozen at most)
+      std::vector<std::thread> th;
+      th.reserve(nh);
+      for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += qo[o + qn[i]] - qo[o], on += qn[i], o += qn[i] + 1, ++i) {
+        const uint64_t *qoi = qo.data() + o, q0 = qo[o];
+        const uint32_t n_i = (uint32_t)qn[i];
+        const bool order_free = n_i >= 350 && n_i < 1000000 && !old_heur && hord[i] == 0;  // d_cl_order_free
+        uint32_t *out = hperm.data() + on;
+        const uint32_t *sr = hsrow.data() + on, *sq = hst.data() + oq;
+        th.emplace_back([=] {
+          if (order_free) {
+            std::copy(sr, sr + n_i, out);
+            return;
+          }
+          std::vector<uint64_t> rel(n_i + 1);
+          for (uint32_t t = 0; t <= n_i; ++t) rel[t] = qoi[t] - q0;
+          host_replay(n_i, rel.data(), sq, sr, out);
+        });
+      }
+      for (auto &t : th) t.join();
+    }
+    HC(hipEventRecord(E->evx[6], st));
+    HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
+    for (uint64_t i = 0, on = 0; i < nh; on += qn[i], ++i)
+      HC(hipMemcpyAsync(D.perm + eo.cl_off[hid[i]], hperm.data() + on, 4 * qn[i], hipMemcpyHostToDevice, E->st2));
+    HC(hipStreamSynchronize(E->st2));  // the pageable sources go out of scope
+    if (g_prof_env)
+      fprintf(stderr, "[rs-prof] host replay: %llu clusters, %llu rows, %llu pairs, %.2f ms\n", (unsigned long long)nh,
+              (unsigned long long)tot_n, (unsigned long long)tot_q, now_ms() - th0);
+  }
+  if (hc[4] && dev_replay) {  // (kClMid, kClLds]: the largest LDS footprint, on the second stream (the few
+                              // largest clusters' serial replays overlap everything else's)
     HC(hipEventRecord(E->evx[6], st));
     HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
     if (g_prof_env) rprof = A.get<unsigned long long>("cl.rprof", 4 * hc[4]);
@@ -1046,7 +1149,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
                 rp[4 * i], rp[4 * i + 1], rp[4 * i + 2], rp[4 * i + 3] / 100.0);
     }
   }
-  if (hc[2] > hc[4]) {  // (kClSmall, kClMid]
+  if (hc[2] > hc[4] && (dev_replay || !hc[4])) {  // (kClSmall, kClMid] (launched above with a host replay)
     const uint64_t nm = hc[2] - hc[4];
     hipLaunchKernelGGL((k_cl_replay_wave<kClMid>), dim3((unsigned)std::min<uint64_t>(nm, 16384)), dim3(64), 0, st,
                        (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3] + hc[4]), nm,

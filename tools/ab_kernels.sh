@@ -11,6 +11,7 @@ for arg in "$@"; do
   tag=${arg%%:*}
   envs=${arg#*:}
   ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
+    unset IFS
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$tag -o k -- \
       python3 tools/config_bench.py --reps ${REPS:-4} ${CONFIGS:-mixed10M} > $OUT/$tag.log 2>&1 )
   echo "$tag done"
