@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <map>
@@ -243,6 +244,7 @@ struct rs_engine {
   std::vector<SnapJob> snap_jobs;
   std::thread snap_thread;
   hipStream_t stx = nullptr;  // the early region's D2H stream
+  hipStream_t str = nullptr;  // the host replay's copies (small; never behind the bulk copies)
   hipEvent_t ev_chunk[2] = {};
   int snap_rc = 0;
   // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
@@ -1071,60 +1073,69 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
       HC(hipGetLastError());
     }
     const double th0 = now_ms();
-    // every input of the replays is complete (the stream was synchronised above): copy on stx
+    // every input of the replays is complete (the stream was synchronised above): two copy rounds on
+    // str -- each cluster's (first row, rows, first pair, pairs, ordered rows), then its offsets,
+    // pair stream and rows
     const uint64_t nh = hc[4];
-    std::vector<uint32_t> hid(nh), hord(nh);
-    eo.cl_off.resize(n_cl + 1);
-    HC(hipMemcpyAsync(hid.data(), sorted + hc[3], 4 * nh, hipMemcpyDeviceToHost, E->stx));
-    HC(hipMemcpyAsync(eo.cl_off.data(), D.cl_off, 8 * (n_cl + 1), hipMemcpyDeviceToHost, E->stx));
-    HC(hipStreamSynchronize(E->stx));
-    std::vector<uint64_t> qb(nh), qn(nh);  // each cluster's (first row's pair offset) and row count
+    uint64_t *d_meta = A.get<uint64_t>("cl.rmeta", 5 * nh);
+    launch(E->str, k_replay_meta, nh, (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), nh,
+           (const uint64_t *)q_off, (const uint32_t *)n_ordered, d_meta);
+    std::vector<uint64_t> meta(5 * nh);
+    HC(hipMemcpyAsync(meta.data(), d_meta, 40 * nh, hipMemcpyDeviceToHost, E->str));
+    HC(hipStreamSynchronize(E->str));
+    std::vector<uint64_t> qn(nh), rb(nh);
+    std::vector<uint32_t> hord(nh);
     uint64_t tot_q = 0, tot_n = 0;
     for (uint64_t i = 0; i < nh; ++i) {
-      HC(hipMemcpyAsync(&hord[i], n_ordered + hid[i], 4, hipMemcpyDeviceToHost, E->stx));
-      qn[i] = eo.cl_off[hid[i] + 1] - eo.cl_off[hid[i]];
+      rb[i] = meta[5 * i];
+      qn[i] = meta[5 * i + 1];
+      hord[i] = (uint32_t)meta[5 * i + 4];
       tot_n += qn[i];
+      tot_q += meta[5 * i + 3];
     }
     std::vector<uint64_t> qo(tot_n + nh);
-    for (uint64_t i = 0, o = 0; i < nh; o += qn[i] + 1, ++i)
-      HC(hipMemcpyAsync(qo.data() + o, q_off + eo.cl_off[hid[i]], 8 * (qn[i] + 1), hipMemcpyDeviceToHost, E->stx));
-    HC(hipStreamSynchronize(E->stx));
-    for (uint64_t i = 0, o = 0; i < nh; o += qn[i] + 1, ++i) {
-      qb[i] = qo[o];
-      tot_q += qo[o + qn[i]] - qo[o];
-    }
     std::vector<uint32_t> hst(tot_q), hsrow(tot_n), hperm(tot_n);
-    for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += qo[o + qn[i]] - qo[o], on += qn[i], o += qn[i] + 1, ++i) {
-      const uint64_t nq = qo[o + qn[i]] - qo[o];
-      if (nq) HC(hipMemcpyAsync(hst.data() + oq, stream + qb[i], 4 * nq, hipMemcpyDeviceToHost, E->stx));
-      HC(hipMemcpyAsync(hsrow.data() + on, srow + eo.cl_off[hid[i]], 4 * qn[i], hipMemcpyDeviceToHost, E->stx));
+    for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += meta[5 * i + 3], on += qn[i], o += qn[i] + 1, ++i) {
+      HC(hipMemcpyAsync(qo.data() + o, q_off + rb[i], 8 * (qn[i] + 1), hipMemcpyDeviceToHost, E->str));
+      if (meta[5 * i + 3])
+        HC(hipMemcpyAsync(hst.data() + oq, stream + meta[5 * i + 2], 4 * meta[5 * i + 3], hipMemcpyDeviceToHost, E->str));
+      HC(hipMemcpyAsync(hsrow.data() + on, srow + rb[i], 4 * qn[i], hipMemcpyDeviceToHost, E->str));
     }
-    HC(hipStreamSynchronize(E->stx));
-    {  // one host thread per cluster (a few dozen at most)
-      std::vector<std::thread> th;
-      th.reserve(nh);
-      for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += qo[o + qn[i]] - qo[o], on += qn[i], o += qn[i] + 1, ++i) {
-        const uint64_t *qoi = qo.data() + o, q0 = qo[o];
-        const uint32_t n_i = (uint32_t)qn[i];
-        const bool order_free = n_i >= 350 && n_i < 1000000 && !old_heur && hord[i] == 0;  // d_cl_order_free
-        uint32_t *out = hperm.data() + on;
-        const uint32_t *sr = hsrow.data() + on, *sq = hst.data() + oq;
-        th.emplace_back([=] {
-          if (order_free) {
+    HC(hipStreamSynchronize(E->str));
+    {  // the clusters over a few host threads (largest first: the list is size-ordered)
+      std::vector<uint64_t> o_q(nh), o_n(nh), o_o(nh);
+      for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += meta[5 * i + 3], on += qn[i], o += qn[i] + 1, ++i) {
+        o_q[i] = oq;
+        o_n[i] = on;
+        o_o[i] = o;
+      }
+      std::atomic<uint64_t> next_i{0};
+      auto work = [&] {
+        for (uint64_t i; (i = next_i.fetch_add(1)) < nh;) {
+          const uint64_t *qoi = qo.data() + o_o[i], q0 = qoi[0];
+          const uint32_t n_i = (uint32_t)qn[i];
+          uint32_t *out = hperm.data() + o_n[i];
+          const uint32_t *sr = hsrow.data() + o_n[i], *sq = hst.data() + o_q[i];
+          if (n_i >= 350 && n_i < 1000000 && !old_heur && hord[i] == 0) {  // d_cl_order_free
             std::copy(sr, sr + n_i, out);
-            return;
+            continue;
           }
           std::vector<uint64_t> rel(n_i + 1);
           for (uint32_t t = 0; t <= n_i; ++t) rel[t] = qoi[t] - q0;
           host_replay(n_i, rel.data(), sq, sr, out);
-        });
-      }
+        }
+      };
+      const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+      const uint64_t n_th = std::min<uint64_t>({nh, (uint64_t)hw, 16});
+      std::vector<std::thread> th;
+      for (uint64_t k = 1; k < n_th; ++k) th.emplace_back(work);
+      work();
       for (auto &t : th) t.join();
     }
     HC(hipEventRecord(E->evx[6], st));
     HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
     for (uint64_t i = 0, on = 0; i < nh; on += qn[i], ++i)
-      HC(hipMemcpyAsync(D.perm + eo.cl_off[hid[i]], hperm.data() + on, 4 * qn[i], hipMemcpyHostToDevice, E->st2));
+      HC(hipMemcpyAsync(D.perm + rb[i], hperm.data() + on, 4 * qn[i], hipMemcpyHostToDevice, E->st2));
     HC(hipStreamSynchronize(E->st2));  // the pageable sources go out of scope
     if (g_prof_env)
       fprintf(stderr, "[rs-prof] host replay: %llu clusters, %llu rows, %llu pairs, %.2f ms\n", (unsigned long long)nh,
@@ -3259,6 +3270,7 @@ int rs_engine_create(int device, rs_engine **eng) {
     }
     HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->stx, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&E->str, hipStreamNonBlocking));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));
     for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipHostMalloc((void **)&E->h_vflag, 10 * sizeof(int), hipHostMallocDefault));
@@ -3308,6 +3320,7 @@ void rs_engine_destroy(rs_engine *E) {
     if (ev) (void)hipEventDestroy(ev);
   if (E->stc) (void)hipStreamDestroy(E->stc);
   if (E->stx) (void)hipStreamDestroy(E->stx);
+  if (E->str) (void)hipStreamDestroy(E->str);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
   if (E->ev2) (void)hipEventDestroy(E->ev2);
