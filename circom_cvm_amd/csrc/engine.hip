@@ -1539,10 +1539,12 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipStreamWaitEvent(E->st, E->evx[7], 0));
         D.join_pending = false;
       }
-      if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
-      if (n_head) {
-        // the first (wide) Kahn levels over the whole GPU, the rest in one workgroup per cluster
-        const uint32_t kg = head_gpu_levels();
+      // the head's composition: the first (wide) Kahn levels over the whole GPU, the rest in one
+      // workgroup per cluster.  With a fixed level count nothing waits on the host, so all of it is
+      // enqueued before the first frames pass (whose set-up synchronises with the main stream);
+      // RS_HEAD_GPU_LEVELS=all keeps the host-checked level loop after it.
+      const uint32_t kg = head_gpu_levels();
+      auto finish_head = [&] {
         hl.run(kg, kg == UINT32_MAX);
         if (!hl.done && kg < UINT32_MAX) {
           hipLaunchKernelGGL(k_compose_rest<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big,
@@ -1553,6 +1555,11 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[4], E->st2));
         if (g_prof_env) fprintf(stderr, "[rs-prof] head composition: %u level launches\n", hl.levels);
+      };
+      if (n_head && kg < UINT32_MAX) finish_head();
+      if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
+      if (n_head) {
+        if (kg == UINT32_MAX) finish_head();
         HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
       }
       HC(hipEventRecord(E->ev3, E->st));
