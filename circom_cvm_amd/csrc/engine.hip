@@ -240,7 +240,9 @@ struct rs_engine {
     void *dst;
     const void *src;
     size_t bytes;
+    int part;  // ev_snapq[part] marks its gather done
   };
+  hipEvent_t ev_snapq[3] = {};
   std::vector<SnapJob> snap_jobs;
   std::thread snap_thread;
   hipStream_t stx = nullptr;  // the early region's D2H stream
@@ -1899,11 +1901,15 @@ static void snap_start(rs_engine *E) {
   std::vector<rs_engine::SnapJob> jobs = E->snap_jobs;
   E->snap_thread = std::thread([E, jobs]() {
     static const size_t chunk = getenv("RS_SNAP_CHUNK_MB") ? strtoull(getenv("RS_SNAP_CHUNK_MB"), nullptr, 10) << 20 : 16ull << 20;
-    if (hipSetDevice(E->device) != hipSuccess || hipEventSynchronize(E->ev_snap) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
+    if (hipSetDevice(E->device) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
     // two chunks in flight: no gap between them, and a transfer another stream enqueues waits for
     // at most two
-    int k = 0;
-    for (const auto &j : jobs)
+    int k = 0, part = -1;
+    for (const auto &j : jobs) {
+      if (j.part != part) {
+        part = j.part;
+        if (hipEventSynchronize(E->ev_snapq[part]) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
+      }
       for (size_t o = 0; o < j.bytes; o += chunk, ++k) {
         const size_t n = std::min(chunk, j.bytes - o);
         if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
@@ -1913,6 +1919,7 @@ static void snap_start(rs_engine *E) {
           return;
         }
       }
+    }
     if (hipStreamSynchronize(E->stx) != hipSuccess) E->snap_rc = RS_E_HIP;
   });
 }
@@ -2371,9 +2378,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
       if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val);
       void *hc = pin_get(E, 3 + q, 4 * cap), *hv = pin_get(E, 6 + q, 32 * cap);
-      if (ev[q]) {
-        E->snap_jobs.push_back({hc, col, 4 * ev[q]});
-        E->snap_jobs.push_back({hv, val, 32 * ev[q]});
+      if (ev[q]) {  // a part's copies start once its own gather is done
+        HC(hipEventRecord(E->ev_snapq[q], E->stc));
+        E->snap_jobs.push_back({hc, col, 4 * ev[q], q});
+        E->snap_jobs.push_back({hv, val, 32 * ev[q], q});
       }
     }
     HC(hipEventRecord(E->ev_snap, E->stc));
@@ -3296,6 +3304,7 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipEventCreateWithFlags(&E->ev_snap, hipEventDisableTiming));
     HC(hipEventCreateWithFlags(&E->ev_snap0, hipEventDisableTiming));
     for (auto &ev : E->ev_chunk) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (auto &ev : E->ev_snapq) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {
@@ -3339,6 +3348,8 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->ev_snap) (void)hipEventDestroy(E->ev_snap);
   if (E->ev_snap0) (void)hipEventDestroy(E->ev_snap0);
   for (auto &ev : E->ev_chunk)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto &ev : E->ev_snapq)
     if (ev) (void)hipEventDestroy(ev);
   if (E->heap_k) (void)hipFree(E->heap_k);
   if (E->heap_v) (void)hipFree(E->heap_v);
