@@ -17,11 +17,13 @@ import os
 import sys
 
 # bench.py KERNELS name -> substring of the rocprofv3 kernel name
+# (the tail's in-kernel byte counter also counts k_p3_fast, which runs just before k_big_main on the
+# same clusters' list: its traffic is added to the tail's, per launch of k_big_main)
 GROUPS = {
-    "k_big_spec<8> (head)": "k_big_spec<",
-    "k_big_main<256> (tail)": "k_big_main<256u>",
-    "k_frames_wave<0> (non-linear)": "k_frames_wave<0>",
-    "k_frames_wave<1> (rounds)": "k_frames_wave<1>",
+    "k_big_spec<8> (head)": ("k_big_spec<",),
+    "k_big_main<256> (tail)": ("k_big_main<256u>", "k_p3_fast"),
+    "k_frames_wave<0> (non-linear)": ("k_frames_wave<0>",),
+    "k_frames_wave<1> (rounds)": ("k_frames_wave<1>",),
 }
 
 
@@ -59,11 +61,19 @@ def main():
                      "`bench.py --steps 1 --warmup 0 --no-cpu`; FETCH_SIZE x2 (gfx950), KiB -> bytes",
            "commit": args.commit, "steps": args.steps,
            "bytes_per_launch": {}, "bytes_per_step": {}, "launches_per_step": {}, "detail": {}}
-    for name, pat in GROUPS.items():
+    for name, pats in GROUPS.items():
+        pat = pats[0]
         f, nf = group_avg(fe, pat)
         w, nw = group_avg(wr, pat)
         if f is None or w is None:
             continue
+        for extra in pats[1:]:  # added per launch of the main kernel
+            fx, nfx = group_avg(fe, extra)
+            wx, nwx = group_avg(wr, extra)
+            if fx is not None and nf:
+                f += fx * nfx / nf
+            if wx is not None and nw:
+                w += wx * nwx / nw
         fetch = 2.0 * f * 1024.0
         write = w * 1024.0
         res["bytes_per_launch"][name] = int(fetch + write)
