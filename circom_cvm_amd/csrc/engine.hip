@@ -31,6 +31,7 @@
 #include "spec_loop.hpp"
 #include "cluster.hpp"
 #include "writer.hpp"
+#include "maplists.hpp"
 
 namespace rs {
 
@@ -81,11 +82,13 @@ struct Arena {
   // named, grow-only device buffers (a few hundred names, each looked up a few times per run):
   // one hash probe per lookup
   std::unordered_map<std::string, B> bufs{512};
+  uint64_t gen = 0;  // bumped whenever a buffer moves (raw pointers taken before are then stale)
   template <class T>
   T *get(const std::string &name, size_t n) {
     size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
     B &b = bufs[name];
     if (b.cap < bytes) {
+      ++gen;
       if (b.p) HC(hipFree(b.p));
       size_t cap = std::max(bytes, b.cap + b.cap / 4);
       HC(hipMalloc(&b.p, cap));
@@ -102,6 +105,7 @@ struct Arena {
     if (b.cap >= bytes) return;
     const size_t cap = std::max(bytes, b.cap + b.cap / 4);
     void *p = nullptr;
+    ++gen;
     HC(hipMalloc(&p, cap));
     if (b.p) {
       HC(hipStreamSynchronize(ps));
@@ -122,12 +126,8 @@ struct Arena {
   }
 };
 
-// grid of k_frames_wave: RS_FW_BLOCKS (diagnostic knob), else one 64-row chunk per wave up to 16384 blocks
-static uint64_t fw_blocks_env() {
-  static const uint64_t v = getenv("RS_FW_BLOCKS") ? strtoull(getenv("RS_FW_BLOCKS"), nullptr, 10) : 16384;
-  return v ? v : 16384;
-}
-#define fw_blocks(E) fw_blocks_env()
+// grid of k_frames_wave: one 64-row chunk per wave, at most 16384 workgroups (grid-stride beyond)
+constexpr uint64_t kFwBlocks = 16384;
 
 // grid-stride kernels that end in per-wave atomics: a capped grid keeps the atomics few
 template <class K, class... Args>
@@ -252,9 +252,12 @@ struct rs_engine {
   // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
   // when the streamed run skipped it
   bool csr_ready = false;
+  // Invariant: these point into arena buffers (sv.*, fin.keep, fin.lvids, fin.zlen) and the storage
+  // heap as the run left them; nothing between the run and ensure_csr may move them (fin_gen = the
+  // arena generation then; ensure_csr refuses a stale view instead of gathering from freed memory).
   DRows fin_parts[3] = {}, fin_lvq[3] = {};
   const uint32_t *fin_keep_ids = nullptr, *fin_lv_ids = nullptr;
-  uint64_t fin_keep = 0, fin_lvn = 0;
+  uint64_t fin_keep = 0, fin_lvn = 0, fin_gen = 0;
 };
 
 namespace rs {
@@ -932,27 +935,10 @@ struct LevelLoop {
 };
 
 // Kahn levels of the head's composition launched over the whole GPU before k_compose_rest takes the
-// rest per cluster (RS_HEAD_GPU_LEVELS; "all": every level over the GPU, the host loop until empty)
-static uint32_t head_gpu_levels() {
-  static const uint32_t v = [] {
-    const char *e = getenv("RS_HEAD_GPU_LEVELS");
-    if (e && !strcmp(e, "all")) return UINT32_MAX;
-    const uint32_t k = e ? (uint32_t)atoi(e) : 8u;
-    return k < 1 ? 1u : k;  // level 0's items need no composition: k_compose_rest starts after it
-  }();
-  return v;
-}
-static uint64_t head_limit() {
-  static const uint64_t v = [] {
-    const char *hd = getenv("RS_HEAD");
-    if (!hd || !*hd) return (uint64_t)16;
-    char *end = nullptr;
-    const unsigned long long x = strtoull(hd, &end, 10);
-    if (*end || hd[0] == '-') return (uint64_t)16;  // not a plain count: the default
-    return (uint64_t)std::min<unsigned long long>(x, 4096);
-  }();
-  return v;
-}
+// rest per cluster in one workgroup each (level 0's items need no composition)
+constexpr uint32_t kHeadGpuLevels = 8;
+// the number of largest clusters eliminated on the second stream (16 / 32 / 64 measured equal)
+constexpr uint64_t kHeadLimit = 16;
 // The arena replay of one cluster on the host (k_cl_replay_lane's walk): rows in index order, each
 // pair's previous row found by path halving and its root's list appended to the row's.  A serial
 // union-find of dependent accesses: ~20 ns a pair in a host cache against ~0.3 us in LDS, and the
@@ -1061,10 +1047,8 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   launch(st, k_cl_replay_lane, n_cl, (const uint64_t *)D.cl_off, n_cl, (const uint64_t *)q_off,
          (const uint32_t *)stream, (const uint32_t *)srow, c2c, tail, next, D.perm, (const uint32_t *)n_ordered,
          old_heur);
-  unsigned long long *rprof = nullptr;
-  // (kClMid, kClLds] on the host by default (RS_DEVICE_REPLAY: k_cl_replay_wave on the second stream)
-  static const bool dev_replay = getenv("RS_DEVICE_REPLAY") != nullptr;
-  if (hc[4] && !dev_replay) {
+  // (kClMid, kClLds]: the arena replay on the host (host_replay), beside the mid-size replays on the device
+  if (hc[4]) {
     // launched first, so the device has the mid-size replays to do while the host replays
     if (hc[2] > hc[4]) {
       const uint64_t nm = hc[2] - hc[4];
@@ -1143,26 +1127,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
       fprintf(stderr, "[rs-prof] host replay: %llu clusters, %llu rows, %llu pairs, %.2f ms\n", (unsigned long long)nh,
               (unsigned long long)tot_n, (unsigned long long)tot_q, now_ms() - th0);
   }
-  if (hc[4] && dev_replay) {  // (kClMid, kClLds]: the largest LDS footprint, on the second stream (the few
-                              // largest clusters' serial replays overlap everything else's)
-    HC(hipEventRecord(E->evx[6], st));
-    HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
-    if (g_prof_env) rprof = A.get<unsigned long long>("cl.rprof", 4 * hc[4]);
-    hipLaunchKernelGGL((k_cl_replay_wave<kClLds>), dim3((unsigned)std::min<uint64_t>(hc[4], 4096)), dim3(64), 0, E->st2,
-                       (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), (uint64_t)hc[4],
-                       (const uint64_t *)q_off, (const uint32_t *)stream, (const uint32_t *)srow, next, D.perm,
-                       (const uint32_t *)n_ordered, old_heur, rprof);
-    HC(hipGetLastError());
-    if (rprof) {
-      std::vector<unsigned long long> rp(4 * hc[4]);
-      HC(hipMemcpyAsync(rp.data(), rprof, 8 * rp.size(), hipMemcpyDeviceToHost, E->st2));
-      HC(hipStreamSynchronize(E->st2));
-      for (uint64_t i = 0; i < hc[4]; ++i)
-        fprintf(stderr, "[rs-prof] replay #%llu: cluster %llu rows %llu pairs %llu %.1f us\n", (unsigned long long)i,
-                rp[4 * i], rp[4 * i + 1], rp[4 * i + 2], rp[4 * i + 3] / 100.0);
-    }
-  }
-  if (hc[2] > hc[4] && (dev_replay || !hc[4])) {  // (kClSmall, kClMid] (launched above with a host replay)
+  if (hc[2] && !hc[4]) {  // (kClSmall, kClMid] (launched above when there is a host replay)
     const uint64_t nm = hc[2] - hc[4];
     hipLaunchKernelGGL((k_cl_replay_wave<kClMid>), dim3((unsigned)std::min<uint64_t>(nm, 16384)), dim3(64), 0, st,
                        (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3] + hc[4]), nm,
@@ -1174,7 +1139,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
                 // replayed there is a head cluster (single rank: the head is this rank's largest)
     HC(hipEventRecord(E->evx[7], E->st2));
     const bool sharded = E->comm && E->comm->world > 1;
-    if (!sharded && hc[3] + hc[4] <= head_limit()) D.join_pending = true;
+    if (!sharded && hc[3] + hc[4] <= kHeadLimit) D.join_pending = true;
     else HC(hipStreamWaitEvent(st, E->evx[7], 0));
   }
   // elimination split: clusters of kWaveMin rows or more and the heavy small ones (a prefix of the
@@ -1333,10 +1298,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     a.pool_top = P.top;
     a.pool_cap = P.cap;
     a.err = d_err;
-    // compositions sort unless the sort cannot take them (RS_COMPOSE=merge: also merge the short ones
-    // with at most four dependencies -- 45 % slower on the metric circuit's tail, equal on templated)
-    static const bool compose_merge = getenv("RS_COMPOSE") && !strcmp(getenv("RS_COMPOSE"), "merge");
-    a.compose_sort = compose_merge ? 0 : 1;
+    // compositions sort unless the sort cannot take them (merging the short ones too was 45 % slower
+    // on the metric circuit's tail, equal on templated)
+    a.compose_sort = 1;
     // in-kernel algorithmic-byte counters: [0] k_eliminate / composition emits, [1] / [2] the head's
     // k_big_main / normalisation + composition, [3] / [4] the tail's
     a.bytes = E->A.get<unsigned long long>("el.bytes", 5);
@@ -1353,7 +1317,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     HC(hipMemsetAsync(a.bytes, 0, 40, E->st));
     // The largest clusters' prep -> main -> finish chain runs on a second stream: the elimination
     // time is the critical path of the largest cluster, and everything else overlaps it.
-    const uint64_t n_head = std::min<uint64_t>(n_big, head_limit()), n_tail = n_big - n_head;
+    const uint64_t n_head = std::min<uint64_t>(n_big, kHeadLimit), n_tail = n_big - n_head;
     a.wide = 1;       // the head's largest process_4 clusters go through the k_wide_* grid
     a.skip = nullptr;
     ElimArgs at = a;  // the tail's per-cluster side arrays follow the head's
@@ -1381,11 +1345,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipMemsetAsync(ah.cf_n, 0, 24, E->st));
       HC(hipMemsetAsync(ah.cf_nbig, 0, 16, E->st));
     }
-    // the tail's composition: inside k_big_finish, one workgroup per cluster (RS_TAIL_FINISH=level:
-    // level by level over the GPU like the head's -- slower on the metric circuit, 15 vs 6.6 ms)
-    static const bool tail_split = getenv("RS_TAIL_FINISH") && !strcmp(getenv("RS_TAIL_FINISH"), "level");
-    constexpr uint32_t kHeadLevels = 36, kTailLevels = 32;
-    LevelLoop hl, tl;
+    // the tail's composition: inside k_big_finish, one workgroup per cluster (level by level over the
+    // GPU like the head's was slower on the metric circuit, 15 vs 6.6 ms)
+    constexpr uint32_t kHeadLevels = 36;
+    LevelLoop hl;
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_head) {
@@ -1407,20 +1370,13 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));
         HC(hipEventRecord(E->evx[10], E->st2));
-        // the ordered loop with LDS-resident signal state (RS_NO_LDS_HEAD: k_big_main<512>, diagnostic)
-        // (RS_HEAD_KERNEL=lds: the one-wave k_big_main_lds; =plain: k_big_main<512>; diagnostics)
-        static const char *hk = getenv("RS_HEAD_KERNEL");
-        static const int spec_nw = getenv("RS_SPEC_NW") ? atoi(getenv("RS_SPEC_NW")) : 8;
-        if (hk && !strcmp(hk, "plain")) hipLaunchKernelGGL(k_big_main<512>, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        else if (hk && !strcmp(hk, "lds")) hipLaunchKernelGGL(k_big_main_lds, dim3(g), dim3(64), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        else if (spec_nw == 4) hipLaunchKernelGGL(k_big_spec<4>, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        else hipLaunchKernelGGL(k_big_spec<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        // the ordered loop: eight waves reduce rows speculatively against the LDS signal table and
+        // commit in pop order (spec_loop.hpp)
+        hipLaunchKernelGGL(k_big_spec<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
-        // one inversion per head cluster (RS_HEAD_INV=chains: k_batch_inv, one per 16 pivots)
-        static const bool inv_chains = getenv("RS_HEAD_INV") && !strcmp(getenv("RS_HEAD_INV"), "chains");
-        if (inv_chains) hipLaunchKernelGGL(k_batch_inv, dim3(16, g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
-        else hipLaunchKernelGGL(k_batch_inv_tree, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        // one inversion per head cluster
+        hipLaunchKernelGGL(k_batch_inv_tree, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         hipLaunchKernelGGL(k_normalize, dim3(16, g), dim3(256), 0, E->st2, ah, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -1428,7 +1384,6 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         // the Kahn levels and the emission follow once the rest is enqueued (the level loop waits)
       }
-      if (n_head && getenv("RS_HEAD_ALONE")) HC(hipStreamWaitEvent(E->st, E->evx[3], 0));  // diagnostic
       // the main stream starts once the head's preparation is done: its short workgroups come after
       // the head's large-LDS ones have found CUs.  The small clusters first (k_eliminate, one lane
       // each), then the tail: the frames pass that follows waits for both.
@@ -1448,75 +1403,26 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         const uint32_t *ids = d_big + n_head;
         hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
         HC(hipGetLastError());
-        // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast)
-        static const bool no_p3_fast = getenv("RS_NO_P3_FAST") != nullptr;
-        static const bool p3_verify = getenv("RS_P3_VERIFY") != nullptr;
-        if (p3_verify) {  // diagnostic: the fast path's pivots checked against the ordered loop's
-          at.skip = E->A.get<uint8_t>("el.skip", n_tail);
-          at.p3_shadow = E->A.get<uint32_t>("el.p3_shadow", n_slots);
-          HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
-          hipLaunchKernelGGL(k_p3_shadow, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
-          HC(hipGetLastError());
-        } else if (!no_p3_fast) {
-          at.skip = E->A.get<uint8_t>("el.skip", n_tail);
-          HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
-          hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
-          HC(hipGetLastError());
-        }
+        // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast); the
+        // ordered loop skips the clusters it took
+        at.skip = E->A.get<uint8_t>("el.skip", n_tail);
+        HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
+        hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
+        HC(hipGetLastError());
         HC(hipEventRecord(E->ev5, E->st));
-        {
-          ElimArgs am = at;
-          if (p3_verify) am.skip = nullptr;  // the ordered loop does every cluster, then the check
-          hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, am, ids, n_tail);
-          HC(hipGetLastError());
-          if (p3_verify) {
-            unsigned int *nb = E->A.get<unsigned int>("el.p3_bad", 1);
-            HC(hipMemsetAsync(nb, 0, 4, E->st));
-            launch(E->st, k_p3_check, n_tail, at, ids, n_tail, nb);
-            HC(hipStreamSynchronize(E->st));
-          }
-        }
+        hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
+        HC(hipGetLastError());
         HC(hipEventRecord(E->ev6, E->st));
         {  // tail clusters flagged in cls, then one inversion per 64 slots across clusters
           uint8_t *cls = E->A.get<uint8_t>("el.cls", eo.n_clusters);
           HC(hipMemsetAsync(cls, 0, eo.n_clusters, E->st));
           launch(E->st, k_mark_u8, n_tail, ids, n_tail, cls);
           launch(E->st, k_batch_inv_flat, (n_slots + 63) / 64, at, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
-          if (tail_split) launch(E->st, k_normalize_flat, n_slots, at, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
         }
-        if (tail_split) {
-          // the tail's composition level by level over the whole GPU (LevelLoop), like the head's,
-          // instead of each cluster's levels inside one k_big_finish workgroup
-          ElimArgs ats = at;
-          ats.split = 1;
-          ats.cf_items = E->A.get<uint64_t>("cft.items0", n_slots);
-          ats.cf_n = E->A.get<unsigned long long>("cft.cnt", 3);
-          ats.cf_deg = E->A.get<uint64_t>("cft.deg", n_tail);
-          ats.cf_dl = E->A.get<uint64_t>("cft.dl", n_tail);
-          ats.cf_done = E->A.get<uint32_t>("cft.done", n_tail);
-          ats.cf_big = E->A.get<uint64_t>("cft.big", n_slots);
-          ats.cf_nbig = E->A.get<unsigned long long>("cft.nbig", 2);
-          HC(hipMemsetAsync(ats.cf_n, 0, 24, E->st));
-          HC(hipMemsetAsync(ats.cf_nbig, 0, 16, E->st));
-          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, ats, ids, n_tail, 0u);
-          HC(hipGetLastError());
-          tl.ah = ats;
-          tl.ids = ids;
-          tl.s = E->st;
-          tl.cur = ats.cf_items;
-          tl.nxt = E->A.get<uint64_t>("cft.items1", n_slots);
-          tl.n_slots = n_slots;
-          tl.h = E->h_lvl + 4;
-          tl.ev = E->ev_lvlt;
-          tl.run(kTailLevels, false);
-        } else {
-          // clusters of kFinWaveBelow rows and more by the workgroup, the rest one wave each (most
-          // compose chains: the level latency, not the lanes, is their cost); RS_FIN_WAVE_BELOW
-          // overrides the threshold (0: every cluster by a workgroup)
-          static const uint32_t wb = getenv("RS_FIN_WAVE_BELOW") ? (uint32_t)atoi(getenv("RS_FIN_WAVE_BELOW")) : kFinWaveBelow;
-          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail, wb);
-          HC(hipGetLastError());
-        }
+        // clusters of kFinWaveBelow rows and more by the workgroup, the rest one wave each (most compose
+        // chains: the level latency, not the lanes, is their cost)
+        hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail, kFinWaveBelow);
+        HC(hipGetLastError());
       }
       // the head's first levels go in before the host waits for the tail's
       if (n_head) {
@@ -1528,13 +1434,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hl.n_slots = n_slots;
         hl.h = E->h_lvl;
         hl.ev = E->ev_lvl;
-        if (overlap && W == 1) hl.run(std::min(head_gpu_levels(), kHeadLevels), false);
-      }
-      if (tail_split && n_tail) {
-        tl.run(UINT32_MAX, true);
-        hipLaunchKernelGGL(k_big_emit<4>, dim3((unsigned)std::min<uint64_t>(n_tail, 2048)), dim3(256), 0, E->st, tl.ah, d_big + n_head, n_tail);
-        HC(hipGetLastError());
-        if (g_prof_env) fprintf(stderr, "[rs-prof] tail composition: %u level launches\n", tl.levels);
+        if (overlap && W == 1) hl.run(std::min(kHeadGpuLevels, kHeadLevels), false);
       }
       HC(hipEventRecord(E->ev7, E->st));
       if (D.join_pending) {  // the main stream reads the head clusters' orders from here on
@@ -1543,12 +1443,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       }
       // the head's composition: the first (wide) Kahn levels over the whole GPU, the rest in one
       // workgroup per cluster.  With a fixed level count nothing waits on the host, so all of it is
-      // enqueued before the first frames pass (whose set-up synchronises with the main stream);
-      // RS_HEAD_GPU_LEVELS=all keeps the host-checked level loop after it.
-      const uint32_t kg = head_gpu_levels();
+      // enqueued before the first frames pass (whose set-up synchronises with the main stream).
       auto finish_head = [&] {
-        hl.run(kg, kg == UINT32_MAX);
-        if (!hl.done && kg < UINT32_MAX) {
+        hl.run(kHeadGpuLevels, false);
+        if (!hl.done) {
           hipLaunchKernelGGL(k_compose_rest<8>, dim3((unsigned)n_head), dim3(512), 0, E->st2, ah, (const uint32_t *)d_big,
                              (const uint64_t *)hl.cur, (const unsigned long long *)(ah.cf_n + hl.level % 3), n_head);
           HC(hipGetLastError());
@@ -1558,12 +1456,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipEventRecord(E->evx[4], E->st2));
         if (g_prof_env) fprintf(stderr, "[rs-prof] head composition: %u level launches\n", hl.levels);
       };
-      if (n_head && kg < UINT32_MAX) finish_head();
+      if (n_head) finish_head();
       if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
-      if (n_head) {
-        if (kg == UINT32_MAX) finish_head();
-        HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
-      }
+      if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
       HC(hipEventRecord(E->ev3, E->st));
     }
     int err = 0;
@@ -1653,7 +1548,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     if (a.prof) {
       std::vector<unsigned long long> pf(kProfWords * n_big);
       HC(hipMemcpy(pf.data(), a.prof, 8 * pf.size(), hipMemcpyDeviceToHost));
-      {  // head workgroups' start offsets (k_big_main_lds)
+      {  // head workgroups' start offsets (k_big_spec)
         unsigned long long t0m = ~0ull;
         for (uint64_t q = 0; q < std::min<uint64_t>(n_big, 16); ++q)
           if (pf[kProfWords * q + 22]) t0m = std::min(t0m, pf[kProfWords * q + 22]);
@@ -1900,7 +1795,8 @@ static void snap_start(rs_engine *E) {
   E->snap_rc = 0;
   std::vector<rs_engine::SnapJob> jobs = E->snap_jobs;
   E->snap_thread = std::thread([E, jobs]() {
-    static const size_t chunk = getenv("RS_SNAP_CHUNK_MB") ? strtoull(getenv("RS_SNAP_CHUNK_MB"), nullptr, 10) << 20 : 16ull << 20;
+    // 16 MB chunks (8 / 16 / 64 MB measured 53.0 / 52.2 / 55.0 ms host -> host)
+    constexpr size_t chunk = 16ull << 20;
     if (hipSetDevice(E->device) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
     // two chunks in flight: no gap between them, and a transfer another stream enqueues waits for
     // at most two
@@ -1942,6 +1838,7 @@ static void *pin_get(rs_engine *E, int slot, size_t bytes) {
 static void ensure_csr(rs_engine *E) {
   if (E->csr_ready) return;
   Arena &A = E->A;
+  if (A.gen != E->fin_gen) throw RsError(RS_E_INTERNAL, "result views are stale: a buffer moved after the run");
   hipStream_t st = E->st;
   const char *nm[3] = {"out.a", "out.b", "out.c"};
   const uint64_t n_keep = E->fin_keep, n_lv = E->fin_lvn, n_out = n_keep + n_lv;
@@ -2349,7 +2246,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   uint8_t *so_early = nullptr;
   U3 *so_eoff = nullptr;
   auto snap_take = [&](const uint64_t *late) {
-    if (!E->stream_out || !n_nl || getenv("RS_NO_STREAM")) return;
+    if (!E->stream_out || !n_nl) return;
     so_early = A.get<uint8_t>("so.early", n_nl);
     so_eoff = A.get<U3>("so.eoff", n_nl);
     U3 *elen = A.get<U3>("so.elen", n_nl);
@@ -2440,7 +2337,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     a.xlist = w.big;
     a.n_xlist = w.n_big;
     HC(hipEventRecord(e0, st));
-    launch_capped(st, k_frames_wave<0>, n, fw_blocks(E), w);
+    launch_capped(st, k_frames_wave<0>, n, kFwBlocks, w);
     launch(st, k_nl_fill, n, a);  // a grid for every row: the list may be long, idle lanes leave at once
     HC(hipEventRecord(e1, st));
     if (g_prof_env) {
@@ -2638,7 +2535,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       HC(hipMemcpyAsync(ic0.off, tc_.off, 8 * n_st, hipMemcpyDeviceToDevice, st));
       HC(hipMemcpyAsync(ic0.len, tc_.len, 4 * n_st, hipMemcpyDeviceToDevice, st));
     }
-    std::unordered_map<uint32_t, std::vector<uint32_t>> minit;  // queried signals only
+    // the appended lists of the non-linear signal map, lazily (maplists.hpp)
+    MapLists ML;
+    auto &minit = ML.minit;  // initial lists, queried signals only
     uint8_t *qflag = A.get<uint8_t>("m.qflag", S);
     HC(hipMemsetAsync(qflag, 0, S, st));
     auto query_initial = [&](const std::vector<uint32_t> &sigs) {
@@ -2670,86 +2569,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         break;
       }
       launch(st, k_unmark_list, q.size(), (const uint32_t *)d_q, (uint64_t)q.size(), qflag);
-    };
-    // The appends of apply_substitution_to_map (:369-377) -- every key of a substitution's RHS gets
-    // the row list of its `from` -- kept lazily: per round that another round follows, its
-    // substitutions' `from` and RHS keys (a batch).  A signal's appended list is materialised only
-    // when a later round orders the rows it turned linear by their positions in that list
-    // (resolve_ext); most appended lists are never read, and building them all costs
-    // sum |RHS| x |rows| host appends per round.
-    struct MapBatch {
-      std::vector<uint32_t> from, keys;
-      std::vector<uint64_t> ptr;
-    };
-    std::vector<MapBatch> batches;
-    // the appended lists of the signals X from batches [0, upto), in append order: batch, then
-    // substitution, then RHS position (a substitution's `from` is in no RHS of its own round, so a
-    // batch's appends never depend on each other; a visit list depends on earlier batches only).
-    // list(x, u) = concat over batches b < u, over the substitutions j of b whose RHS holds x (in
-    // order): minit[from_j] ++ list(from_j, b) -- memoised per (signal, batch bound), so chains of
-    // rounds cost one evaluation per pair instead of one per path.
-    std::vector<std::unordered_map<uint32_t, std::vector<uint32_t>>> bidx;  // per batch: key -> j's
-    auto batch_index = [&](size_t bi) -> const std::unordered_map<uint32_t, std::vector<uint32_t>> & {
-      if (bidx.size() < batches.size()) bidx.resize(batches.size());
-      auto &ix = bidx[bi];
-      if (ix.empty() && !batches[bi].keys.empty()) {
-        const MapBatch &B = batches[bi];
-        for (uint64_t j = 0; j < B.from.size(); ++j)
-          for (uint64_t t = B.ptr[j]; t < B.ptr[j + 1]; ++t) ix[B.keys[t]].push_back((uint32_t)j);
-      }
-      return ix;
-    };
-    std::unordered_map<uint64_t, std::vector<uint32_t>> ext_memo;
-    auto memo_key = [&](uint32_t x, size_t u) { return (uint64_t)x * (batches.size() + 1) + u; };
-    std::function<const std::vector<uint32_t> &(uint32_t, size_t)> ext_list = [&](uint32_t x, size_t u) -> const std::vector<uint32_t> & {
-      const uint64_t key = memo_key(x, u);
-      auto it = ext_memo.find(key);
-      if (it != ext_memo.end()) return it->second;
-      std::vector<uint32_t> out;
-      for (size_t bi = 0; bi < u; ++bi) {
-        const auto &ix = batch_index(bi);
-        auto h = ix.find(x);
-        if (h == ix.end()) continue;
-        for (uint32_t j : h->second) {
-          const uint32_t f = batches[bi].from[j];
-          const std::vector<uint32_t> &L0 = minit[f];
-          out.insert(out.end(), L0.begin(), L0.end());
-          const std::vector<uint32_t> &pr = ext_list(f, bi);
-          out.insert(out.end(), pr.begin(), pr.end());
-        }
-      }
-      return ext_memo.emplace(key, std::move(out)).first->second;
-    };
-    auto resolve_ext = [&](const std::vector<uint32_t> &X, size_t upto) {
-      std::unordered_map<uint32_t, std::vector<uint32_t>> res;
-      if (X.empty() || upto == 0) return res;
-      // every `from` the lists reach, fetched from the device in one query
-      std::vector<uint32_t> froms;
-      std::unordered_set<uint64_t> seen;
-      std::vector<std::pair<uint32_t, size_t>> work;
-      for (uint32_t x : X) work.push_back({x, upto});
-      while (!work.empty()) {
-        auto [x, u] = work.back();
-        work.pop_back();
-        if (!seen.insert(memo_key(x, u)).second || ext_memo.count(memo_key(x, u))) continue;
-        for (size_t bi = 0; bi < u; ++bi) {
-          const auto &ix = batch_index(bi);
-          auto h = ix.find(x);
-          if (h == ix.end()) continue;
-          for (uint32_t j : h->second) {
-            froms.push_back(batches[bi].from[j]);
-            work.push_back({batches[bi].from[j], bi});
-          }
-        }
-      }
-      std::sort(froms.begin(), froms.end());
-      froms.erase(std::unique(froms.begin(), froms.end()), froms.end());
-      query_initial(froms);
-      for (uint32_t x : X) {
-        const std::vector<uint32_t> &L = ext_list(x, upto);
-        if (!L.empty()) res[x] = L;
-      }
-      return res;
     };
     E->stats.subst_ms += now_ms() - Tm;
     E->stats.map_ms += now_ms() - Tm;
@@ -2883,7 +2702,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           rb.rlist = w.big; rb.n_rlist = w.n_big;
           rt.rlist = w.turn_list; rt.n_rlist = w.n_turn;
           HC(hipEventRecord(E->ev0, st));
-          launch_capped(st, k_frames_wave<1>, ra.n_ids, fw_blocks(E), w);
+          launch_capped(st, k_frames_wave<1>, ra.n_ids, kFwBlocks, w);
           {  // the rows too long for a wave's LDS batch: A / B / C expanded by one device-wide sort
             unsigned nbig = 0;
             HC(hipMemcpyAsync(&nbig, w.n_big, 4, hipMemcpyDeviceToHost, st));
@@ -2969,7 +2788,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           std::sort(qs.begin(), qs.end());
           qs.erase(std::unique(qs.begin(), qs.end()), qs.end());
           query_initial(qs);
-          ext = resolve_ext(qs, batches.size());
+          ext = ML.resolve(qs, query_initial);
           E->stats.map_ms += now_ms() - Tq;
         }
         // order key: (rank of the turning substitution, first position in map[from])
@@ -3032,7 +2851,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         double Tq = now_ms();
         need_usig();
         // this round's batch of appends: every substitution's `from` and RHS keys (no values)
-        MapBatch B;
+        MapLists::Batch B;
         std::vector<uint64_t> uoff(nU);
         std::vector<uint32_t> ulen(nU);
         HC(hipMemcpyAsync(uoff.data(), d_uoff, 8 * nU, hipMemcpyDeviceToHost, st));
@@ -3040,7 +2859,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         HC(hipStreamSynchronize(st));
         fetch_pool_keys(E, uoff, ulen, P.pk, B.keys, B.ptr);
         B.from = usig;
-        batches.push_back(std::move(B));
+        ML.add_batch(std::move(B));
         E->stats.map_ms += now_ms() - Tq;
       }
       MK.mark("appends2");
@@ -3194,6 +3013,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
     E->fin_keep = n_keep;
     E->fin_lvn = n_lv;
+    E->fin_gen = A.gen;
     E->fin_keep_ids = keep_ids;
     E->fin_lv_ids = lv_ids;
     if (!E->snap_on) ensure_csr(E);
@@ -3249,34 +3069,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     }
     std::unique_ptr<rs_engine> E(new rs_engine());
     E->device = device;
-    {
-      // The main stream leaves kHeadCUs compute units to the second stream: the head's ordered loop
-      // (k_big_main_lds, one workgroup of ~154 KB LDS per cluster) finds whole CUs free there
-      // instead of waiting for the tail kernels to drain a CU (RS_HEAD_CUS overrides; 0 = no mask).
-      uint32_t head_cus = 0;
-      if (const char *hc = getenv("RS_HEAD_CUS")) head_cus = (uint32_t)std::min<unsigned long>(strtoul(hc, nullptr, 10), 64ul);
-      const uint32_t n_cu = (uint32_t)prop.multiProcessorCount;
-      E->n_cu = n_cu;
-      bool masked = false;
-      if (head_cus && n_cu >= 4 * head_cus) {
-        // mask bits go 32 to an XCD, and workgroups are dealt to the XCDs round-robin: the free CUs
-        // are spread evenly (head_cus / #XCD per XCD) so head workgroup i finds one on XCD i % #XCD
-        const uint32_t n_xcd = std::max<uint32_t>(1, n_cu / 32);
-        const uint32_t per = std::max<uint32_t>(1, head_cus / n_xcd);
-        std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
-        for (uint32_t cu = 0; cu < n_cu; ++cu)
-          if (cu % 32 < 32 - per) mask[cu / 32] |= 1u << (cu % 32);
-        masked = hipExtStreamCreateWithCUMask(&E->st, (uint32_t)mask.size(), mask.data()) == hipSuccess;
-        if (masked && g_prof_env) {
-          std::vector<uint32_t> got(mask.size(), 0u);
-          (void)hipExtStreamGetCUMask(E->st, (uint32_t)got.size(), got.data());
-          fprintf(stderr, "[rs-prof] main stream CU mask (%u CUs):", n_cu);
-          for (uint32_t w : got) fprintf(stderr, " %08x", w);
-          fprintf(stderr, "\n");
-        }
-      }
-      if (!masked) HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
-    }
+    E->n_cu = (uint32_t)prop.multiProcessorCount;
+    HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
     {  // the second stream carries the critical path (the largest clusters' chain): high priority
       int lo = 0, hi = 0;
       if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||

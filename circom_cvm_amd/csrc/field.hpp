@@ -173,7 +173,7 @@ __host__ __device__ __forceinline__ Fe fmul256(const FieldP &F, const Fe &A, con
 }
 // The field product every kernel uses: the one-word path for p < 2^64 (the prime is uniform over a
 // launch, so the branch never diverges a wave), else fmul256.  The tail's ordered loop calls fmul256
-// directly, and so does the head's (k_big_main_lds): the branch cost the tail 18 VGPRs and ~5 % of its
+// directly, and so does the head's (k_big_spec): the branch cost the tail 18 VGPRs and ~5 % of its
 // time on the 256-bit primes, the head ~1.5 %; a goldilocks
 // circuit gets the same residues either way.
 __host__ __device__ __forceinline__ Fe fmul(const FieldP &F, const Fe &A, const Fe &B) {

@@ -541,12 +541,11 @@ struct ElimArgs {
   uint32_t *row_len;
   int wide;                   // the k_wide_* kernels prepared this launch's largest p4 clusters
   uint8_t *skip = nullptr;    // per cluster (launch order): k_p3_fast finished it, the ordered loop skips it
-  uint32_t *p3_shadow = nullptr;  // RS_P3_VERIFY diagnostic: k_p3_fast's pivots per slot, checked after the loop
   // split composition (the head's clusters): k_big_finish only normalises and builds each cluster's
   // dependency DAG, k_compose_level composes one Kahn level of every cluster at a time over the
   // whole GPU, k_big_emit finishes
   int split;
-  int compose_sort;         // 1: compositions merge only where the sort cannot (0: RS_COMPOSE=merge)
+  int compose_sort;         // 1: compositions merge only where the sort cannot (0: every composition merges)
   uint64_t *cf_items;         // the first frontier (cluster position << 32 | local slot)
   unsigned long long *cf_n;   // its length
   uint64_t *cf_deg, *cf_dl;   // per cluster: pool offsets of deg[m] (+ dcnt[m+1]) and of the dependents
@@ -588,7 +587,7 @@ __device__ __forceinline__ uint64_t pool_alloc(const ElimArgs &A, Alloc &al, uin
 
 // clear_signal_not_normalized (algebra.rs:1126-1136): to = row minus key, {0: 0} ensured.
 // Every substitution created before or inside the ordered loop is preceded in the pool by a header
-// entry (key = RHS length, value = the coefficient): k_big_main_lds reads a holder's header and its
+// entry (key = RHS length, value = the coefficient): k_big_spec reads a holder's header and its
 // right-hand side in one round trip.
 __device__ __forceinline__ uint32_t d_clear_nn_len(const uint32_t *k, uint32_t n, uint32_t oi) {  // RHS entries
   const bool has0 = n > 0 && k[0] == 0 && oi != 0;
@@ -1376,66 +1375,6 @@ __global__ __launch_bounds__(256) void k_p3_fast(ElimArgs A, const uint32_t *ids
     __syncthreads();
   }
 }
-// RS_P3_VERIFY diagnostic: the pivots k_p3_fast would give every row (pop order) into p3_shadow,
-// the clusters it would take flagged in skip (2); nothing else written
-__global__ __launch_bounds__(256) void k_p3_shadow(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
-  __shared__ uint32_t s_dirty;
-  const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
-    const uint64_t c = ids[ci];
-    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
-    const uint32_t n = (uint32_t)(e - b);
-    if (d_is_p4(A, n)) continue;
-    if (tid == 0) s_dirty = 0;
-    __syncthreads();
-    for (uint32_t pos = tid; pos < n; pos += nt) {
-      const uint64_t ro = A.row_off[b + pos];
-      const uint32_t rl = A.row_len[b + pos];
-      uint32_t m = RS_NONE;
-      for (uint32_t i = rl; i-- > 0;)
-        if (!A.forb[A.rows.key[ro + i]]) { m = A.rows.key[ro + i]; break; }
-      A.tmp[b + pos] = m;
-      if (m != RS_NONE && atomicAdd(&A.occ[m], 1) != -1) s_dirty = 1;
-    }
-    __syncthreads();
-    for (uint32_t pos = tid; pos < n; pos += nt)
-      if (A.tmp[b + pos] != RS_NONE) A.occ[A.tmp[b + pos]] = -1;
-    __syncthreads();
-    if (tid == 0 && !s_dirty) {
-      uint32_t r = 0;
-      for (uint32_t pos = n; pos-- > 0;)
-        if (A.tmp[b + pos] != RS_NONE) A.p3_shadow[b + r++] = A.tmp[b + pos];
-      A.skip[ci] = 2;
-    }
-    __syncthreads();
-  }
-}
-__global__ void k_p3_check(ElimArgs A, const uint32_t *ids, uint64_t n_ids, unsigned int *n_bad) {
-  for (uint64_t ci = gtid(); ci < n_ids; ci += gstride()) {
-    if (A.skip[ci] != 2) continue;
-    const uint64_t c = ids[ci];
-    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
-    const uint32_t n = (uint32_t)(e - b), m = A.n_sub[c];
-    uint32_t cnt = 0;
-    for (uint32_t pos = 0; pos < n; ++pos) cnt += A.tmp[b + pos] != RS_NONE;
-    bool bad = cnt != m;
-    uint32_t at = 0;
-    for (uint32_t i = 0; !bad && i < m; ++i)
-      if (A.h_sig[b + i] != A.p3_shadow[b + i]) { bad = true; at = i; }
-    if (!bad) continue;
-    if (atomicAdd(n_bad, 1u) >= 4) continue;
-    printf("[p3-verify] cluster %llu n %u subs %u shadow %u first diff slot %u: seq %u shadow %u\n",
-           (unsigned long long)c, n, m, cnt, at, at < m ? A.h_sig[b + at] : 0u, A.p3_shadow[b + at]);
-    for (uint32_t pos = n; pos-- > 0 && pos + 12 > n;) {
-      const uint64_t ro = A.row_off[b + pos];
-      const uint32_t rl = A.row_len[b + pos];
-      printf("[p3-verify]   row pos %u len %u:", pos, rl);
-      for (uint32_t i = 0; i < rl && i < 10; ++i) printf(" %u%s", A.rows.key[ro + i], A.forb[A.rows.key[ro + i]] ? "F" : "");
-      printf("\n");
-    }
-  }
-}
-
 // The rest of one row's treat_constraint_3/4 loop on a work list in the pool (single lane; used
 // when a list does not fit the LDS buffers of k_big_main).
 __device__ inline bool d_treat_scalar(const ElimArgs &A, Alloc &al, uint64_t b, const uint32_t *k, const Fe *v,
@@ -1567,7 +1506,7 @@ struct BigSmem {
   unsigned long long s_best;
   uint64_t s_o;
 };
-// One cluster's ordered loop (the body of k_big_main; k_big_main_lds also runs it, on its LDS, for
+// One cluster's ordered loop (the body of k_big_main; k_big_spec also runs it, on wave 0, for
 // the clusters whose signals do not fit its table).
 template <uint32_t CAP>
 __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint32_t *ids, uint64_t ci, BigSmem<CAP> &S,
@@ -1959,533 +1898,11 @@ __global__ __launch_bounds__(64) void k_big_main(ElimArgs A, const uint32_t *ids
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) d_big_main_cluster<CAP>(A, ids, ci, S, al0);
 }
 
-// ---------------------------------------------------------------- the head's ordered loop, LDS state
-// k_big_main with the per-signal state of the cluster in LDS.  The loop of the largest clusters is
-// the critical path of the whole run, and on a loaded chip each of its dependent global round trips
-// costs 0.5-0.8 us; here every signal question -- forbidden? deleted (and where is its holder)? how
-// many occurrences? -- is one LDS hash probe, and a holder's length, coefficient and right-hand side
-// arrive in ONE round trip (the pool header d_clear_nn / this kernel write before every RHS).
-//   table: open addressing over the cluster's non-forbidden signals (k_big_prep's touched list);
-//          key 0xffffffff = empty; a signal not in the table is forbidden.
-//   state (u32): bit 31 set -> deleted, bits 0-30 = pool offset of its holder's header;
-//                else -> occurrences (SignalsInformation, remove_constraint keeps it current).
-// The same row walk, pivot rules (take_signal_3 / take_signal_4), merges and pool writes as
-// k_big_main; the dense global arrays (holder_idx, del, occ) are still written, so the lane-serial
-// spill path (d_treat_scalar) and the kernels after the loop see the same state.  A cluster whose
-// signals do not fit the table runs k_big_main's loop (d_big_main_cluster<512>) on the same LDS.
-constexpr uint32_t kHeadTab = 15360;     // LDS hash slots (60 KB keys + 60 KB states)
-constexpr uint32_t kHeadTabMax = 9216;   // signals per cluster at most (load factor 0.6)
-constexpr uint32_t kHeadCap = 256;       // LDS work-list capacity
+// LDS signal-table encoding of the head's speculative loop (spec_loop.hpp): empty slot / deleted bit
 constexpr uint32_t kTabEmpty = 0xffffffffu, kStDel = 0x80000000u;
-__device__ __forceinline__ uint32_t tab_slot(uint32_t s) {
-  return (uint32_t)(((uint64_t)(s * 0x9E3779B1u) * kHeadTab) >> 32);
-}
-// slot of s, or kTabEmpty when s is not in the table (forbidden)
-__device__ __forceinline__ uint32_t tab_find(const uint32_t *tk, uint32_t s) {
-  if (s == 0) return kTabEmpty;  // the constant: always forbidden
-  uint32_t i = tab_slot(s);
-  for (;;) {
-    const uint32_t k = tk[i];
-    if (k == s) return i;
-    if (k == kTabEmpty) return kTabEmpty;
-    i = i + 1 == kHeadTab ? 0 : i + 1;
-  }
-}
-__device__ __forceinline__ uint32_t tab_state(const uint32_t *tk, const uint32_t *tv, uint32_t s) {
-  const uint32_t i = tab_find(tk, s);
-  return i == kTabEmpty ? kStForb : tv[i];
-}
 
-struct HeadSmem {
-  uint32_t tk[kHeadTab], tv[kHeadTab];
-  uint32_t wk[2][kHeadCap], ws[2][kHeadCap];
-  Fe wv[2][kHeadCap];
-  uint32_t rk[kHeadCap], rs[kHeadCap];
-  Fe rv[kHeadCap];
-  uint32_t fw[kHeadCap], fr[kHeadCap], lbw[kHeadCap], lbr[kHeadCap];
-  uint32_t s_fdel, s_m, s_nl, s_ok;
-  unsigned long long s_best;
-  uint64_t s_o;
-};
-union HeadLds {
-  HeadSmem h;
-  BigSmem<512> b;  // a cluster too large for the table runs k_big_main's loop on the same LDS
-};
-__global__ __launch_bounds__(64) void k_big_main_lds(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
-  constexpr uint32_t CAP = kHeadCap;
-  const FieldP &F = A.F;
-  __shared__ HeadLds U;
-  auto &tk = U.h.tk;
-  auto &tv = U.h.tv;
-  auto &wk = U.h.wk;
-  auto &ws = U.h.ws;
-  auto &wv = U.h.wv;
-  auto &rk = U.h.rk;
-  auto &rs = U.h.rs;
-  auto &rv = U.h.rv;
-  auto &fw = U.h.fw;
-  auto &fr = U.h.fr;
-  auto &lbw = U.h.lbw;
-  auto &lbr = U.h.lbr;
-  uint32_t &s_fdel = U.h.s_fdel, &s_m = U.h.s_m, &s_nl = U.h.s_nl, &s_ok = U.h.s_ok;
-  unsigned long long &s_best = U.h.s_best;
-  uint64_t &s_o = U.h.s_o;
-  const uint32_t tid = threadIdx.x, nt = 64;
-  Alloc al0;  // lane 0's allocator
-  al0.chunk = 4096;
-  auto below = [](uint64_t m, uint32_t k) -> uint32_t { return (uint32_t)__popcll(k >= 64 ? m : (m & ((1ull << k) - 1ull))); };
-  for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
-    const uint64_t c = ids[ci];
-    const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
-    const bool p4 = d_is_p4(A, (uint32_t)(e - b));
-    const uint32_t n_loop = A.big_alive[ci];
-    const uint32_t n_touch = A.big_touch_n[ci];
-    const uint64_t touch_off = A.big_touch_off[ci];
-    if (n_loop == 0) {  // nothing for the ordered loop (every row went to the uniques phase)
-      if (tid == 0) A.n_left[c] = 0;
-      continue;
-    }
-    // process_3 clusters have no touched list (no occurrence bookkeeping, no uniques phase): their
-    // table is built from the rows themselves, bounded by the number of entries
-    unsigned long long n_ent = 0;
-    if (!p4) {
-      for (uint32_t pos = tid; pos < n_loop; pos += nt) n_ent += A.row_len[b + pos];
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) n_ent += __shfl_xor(n_ent, d);
-    }
-    if ((p4 ? n_touch : n_ent) > kHeadTabMax || A.pool_cap >= (uint64_t)kStDel) {
-      __syncthreads();
-      d_big_main_cluster<512>(A, ids, ci, U.b, al0);
-      continue;
-    }
-    const unsigned long long t_1 = A.prof ? wall_clock64() : 0ull;
-    // ---- the cluster's signal table
-    for (uint32_t i = tid; i < kHeadTab; i += nt) tk[i] = kTabEmpty;
-    __syncthreads();
-    if (!p4) {  // every non-forbidden key of the rows, takeable (nothing is deleted yet)
-      for (uint32_t pos = 0; pos < n_loop; ++pos) {
-        const uint64_t ro = A.row_off[b + pos];
-        const uint32_t rl_ = A.row_len[b + pos];
-        for (uint32_t i = tid; i < rl_; i += nt) {
-          const uint32_t s = A.rows.key[ro + i];
-          if (A.forb[s]) continue;
-          uint32_t q = tab_slot(s);
-          for (;;) {
-            const uint32_t old = atomicCAS(&tk[q], kTabEmpty, s);
-            if (old == kTabEmpty) { tv[q] = 0; break; }
-            if (old == s) break;
-            q = q + 1 == kHeadTab ? 0 : q + 1;
-          }
-        }
-      }
-    }
-    for (uint32_t t0 = 0; p4 && t0 < n_touch; t0 += 4 * nt) {
-      uint32_t sg[4], st[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t t = t0 + u * nt + tid;
-        sg[u] = t < n_touch ? A.pk[touch_off + t] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        st[u] = 0;
-        if (!sg[u]) continue;
-        if (A.del[sg[u]]) {
-          const int32_t h = A.holder_idx[sg[u]];
-          st[u] = kStDel | (uint32_t)(A.h_off[h] - 1);
-        } else {
-          const int32_t o = A.occ[sg[u]];
-          st[u] = o < 0 ? 0u : (uint32_t)o;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (!sg[u]) continue;
-        uint32_t i = tab_slot(sg[u]);
-        for (;;) {
-          const uint32_t old = atomicCAS(&tk[i], kTabEmpty, sg[u]);
-          if (old == kTabEmpty || old == sg[u]) break;
-          i = i + 1 == kHeadTab ? 0 : i + 1;
-        }
-        tv[i] = st[u];
-      }
-    }
-    if (tid == 0) { s_m = A.n_sub[c]; s_nl = 0; s_ok = 1; }
-    __syncthreads();
-    unsigned long long rows = 0, by = 0;  // by: algorithmic bytes (lane 0)
-    uint64_t nx_off = A.row_off[b + n_loop - 1];  // the next row, one ahead: descriptor and entries
-    uint32_t nx_len = A.row_len[b + n_loop - 1];
-    uint32_t pf_k = tid < nx_len ? A.rows.key[nx_off + tid] : 0u;
-    Fe pf_v = tid < nx_len ? A.rows.val[nx_off + tid] : fe_zero();
-    for (uint32_t qi = n_loop; qi-- > 0;) {  // rows from the back (Vec::pop)
-      if (!s_ok) break;
-      ++rows;
-      const uint64_t r_off = nx_off;
-      uint32_t len = nx_len;
-      const uint32_t cur_k = pf_k;
-      const Fe cur_v = pf_v;
-      if (qi) {  // prefetch the row after this one
-        nx_off = A.row_off[b + qi - 1];
-        nx_len = A.row_len[b + qi - 1];
-        pf_k = tid < nx_len ? A.rows.key[nx_off + tid] : 0u;
-        pf_v = tid < nx_len ? A.rows.val[nx_off + tid] : fe_zero();
-      }
-      const uint32_t *k = A.rows.key + r_off;
-      const Fe *v = A.rows.val + r_off;
-      by += 36ull * len;
-      if (len > CAP) {  // lane-serial spill path on the global state (kept current)
-        for (uint32_t i = tid; i < len; i += nt) {  // remove_constraint
-          const uint32_t ti = tab_find(tk, k[i]);
-          if (ti != kTabEmpty && !(tv[ti] & kStDel) && tv[ti] > 0) { tv[ti] -= 1; A.occ[k[i]] = (int32_t)tv[ti]; }
-        }
-        __syncthreads();
-        if (tid == 0) {
-          uint32_t m = s_m, nl = s_nl;
-          if (!d_treat_scalar(A, al0, b, k, v, len, m, nl, p4)) s_ok = 0;
-          if (m > s_m) {  // the new substitution's pivot is deleted now
-            const uint32_t p = A.h_sig[b + m - 1];
-            const uint32_t ti = tab_find(tk, p);
-            if (ti != kTabEmpty) tv[ti] = kStDel | (uint32_t)(A.h_off[b + m - 1] - 1);
-          }
-          s_m = m;
-          s_nl = nl;
-        }
-        __syncthreads();
-        continue;
-      }
-      // ---- the row into the work list: keys, values, states; remove_constraint on the way
-      for (uint32_t i = tid; i < len; i += nt) {
-        const uint32_t kk = i < 64 ? cur_k : k[i];
-        const Fe vv = i < 64 ? cur_v : v[i];
-        const uint32_t ti = tab_find(tk, kk);
-        uint32_t st = kStForb;
-        if (ti != kTabEmpty) {
-          st = tv[ti];
-          if (!(st & kStDel) && st > 0) {
-            st -= 1;
-            tv[ti] = st;
-            A.occ[kk] = (int32_t)st;
-          }
-        }
-        wk[0][i] = kk;
-        wv[0][i] = vv;
-        ws[0][i] = st;
-      }
-      uint32_t cur = 0;
-      // the next merge's holder, loaded speculatively while the current merge computes: pf_st is
-      // the holder state it was loaded for (0: none)
-      uint32_t pf_st = 0, hpf_k = 0;
-      Fe hpf_v = fe_zero();
-      __syncthreads();
-      while (len > 0) {
-        // take_signal_4 (:379-409): the first deleted key (ascending), else min occurrences, ties
-        // -> max id.  take_signal_3 (:368-377): the max takeable key; a conflict iff it is deleted.
-        uint32_t oi = RS_NONE;
-        bool conflict = false;
-        uint32_t hst = 0;  // the pivot's state when deleted
-        if (len <= 64) {
-          const uint32_t stv = tid < len ? ws[cur][tid] : kStForb;
-          const bool tk_ = stv != kStForb, dl = tk_ && (stv & kStDel);
-          const uint64_t tm = __ballot(tk_), dm = __ballot(dl);
-          if (tm) {
-            if (!p4) {
-              oi = 63 - __clzll(tm);
-            } else if (dm) {
-              oi = __ffsll((long long)dm) - 1;
-            } else {
-              unsigned long long vv = tk_ ? ((unsigned long long)stv << 32) | (0xffffffffu - tid) : ~0ull;
-#pragma unroll
-              for (int d = 32; d >= 1; d >>= 1) {
-                const unsigned long long w = __shfl_xor(vv, d);
-                vv = w < vv ? w : vv;
-              }
-              oi = 0xffffffffu - (uint32_t)(vv & 0xffffffffu);
-            }
-            conflict = (dm >> oi) & 1ull;
-            hst = (uint32_t)__shfl((int)stv, (int)oi);
-          }
-        } else {
-          if (tid == 0) { s_fdel = RS_NONE; s_best = ~0ull; }
-          __syncthreads();
-          for (uint32_t i = tid; i < len; i += nt) {
-            const uint32_t st = ws[cur][i];
-            if (st == kStForb) continue;
-            if (!p4) { atomicMin(&s_best, 0xffffffffull - i); continue; }
-            if (st & kStDel) { atomicMin(&s_fdel, i); continue; }
-            atomicMin(&s_best, ((unsigned long long)st << 32) | (0xffffffffu - i));  // sorted keys
-          }
-          __syncthreads();
-          const uint32_t fdel = s_fdel;
-          const unsigned long long best = s_best;
-          if (fdel != RS_NONE || best != ~0ull) {
-            oi = fdel != RS_NONE ? fdel : 0xffffffffu - (uint32_t)(best & 0xffffffffu);
-            hst = ws[cur][oi];
-            conflict = (hst & kStDel) != 0;
-          }
-        }
-        if (oi == RS_NONE) {  // nothing takeable: leftover
-          if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
-          __syncthreads();
-          by += 36ull * len;
-          if (s_ok) {
-            const uint64_t o = s_o;
-            for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
-            if (tid == 0) { A.l_off[b + s_nl] = o; A.l_len[b + s_nl] = len; s_nl = s_nl + 1; }
-          }
-          __syncthreads();
-          break;
-        }
-        const uint32_t p = wk[cur][oi];
-        if (!conflict) {  // new substitution p = -(work - v_p p) / v_p (clear_signal_not_normalized)
-          const uint32_t sh = wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
-          const uint32_t mm = len - 1 + sh;
-          by += 36ull * mm;
-          if (tid == 0) { s_o = pool_alloc(A, al0, (uint64_t)mm + 1); if (s_o == RS_NONE) s_ok = 0; }
-          __syncthreads();
-          if (s_ok) {
-            const uint64_t o = s_o + 1;  // after the header
-            for (uint32_t i = tid; i < len; i += nt) {
-              if (i == oi) continue;
-              const uint32_t q = (i < oi ? i : i - 1) + sh;
-              A.pk[o + q] = wk[cur][i];
-              A.pv[o + q] = wv[cur][i];
-            }
-            if (tid == 0) {
-              const Fe cf = fneg(F, wv[cur][oi]);
-              if (sh) { A.pk[o] = 0; A.pv[o] = fe_zero(); }
-              A.pk[o - 1] = mm;
-              A.pv[o - 1] = cf;
-              d_set_holder(A, p, b + s_m, cf, o, mm);
-              s_m = s_m + 1;
-              A.occ[p] = -1;
-              A.del[p] = 1;
-              const uint32_t ti = tab_find(tk, p);
-              if (ti != kTabEmpty) tv[ti] = kStDel | (uint32_t)(o - 1);
-            }
-          }
-          __syncthreads();
-          break;
-        }
-        // conflict with holder(p): work = -v_p * R - c2 * (work - v_p p).  One round trip: lane 0
-        // reads the header (RHS length, coefficient), lane l >= 1 the RHS entry l - 1.
-        const uint64_t ho = hst & ~kStDel;
-        uint32_t hk_;
-        Fe hv_;
-        if (pf_st == hst) {  // prefetched during the previous merge
-          hk_ = hpf_k;
-          hv_ = hpf_v;
-        } else {
-          const bool in_pool = ho + tid < A.pool_cap;
-          hk_ = in_pool ? A.pk[ho + tid] : 0u;
-          hv_ = in_pool ? A.pv[ho + tid] : fe_zero();
-        }
-        pf_st = 0;
-        const uint32_t rl = (uint32_t)__shfl((int)hk_, 0);
-        Fe c2;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) c2.l[w] = __shfl(hv_.l[w], 0);
-        const Fe coef = fneg(F, wv[cur][oi]);
-        const uint32_t nx = cur ^ 1;
-        if (rl > CAP || len + rl > CAP + 1) {  // spill, finish the row on lane 0
-          if (tid == 0) { s_o = pool_alloc(A, al0, len); if (s_o == RS_NONE) s_ok = 0; }
-          __syncthreads();
-          if (s_ok) {
-            const uint64_t o = s_o;
-            for (uint32_t i = tid; i < len; i += nt) { A.pk[o + i] = wk[cur][i]; A.pv[o + i] = wv[cur][i]; }
-            __syncthreads();
-            if (tid == 0) {
-              uint32_t m = s_m, nl = s_nl;
-              if (!d_treat_scalar(A, al0, b, A.pk + o, A.pv + o, len, m, nl, p4)) s_ok = 0;
-              if (m > s_m) {
-                const uint32_t q = A.h_sig[b + m - 1];
-                const uint32_t ti = tab_find(tk, q);
-                if (ti != kTabEmpty) tv[ti] = kStDel | (uint32_t)(A.h_off[b + m - 1] - 1);
-              }
-              s_m = m;
-              s_nl = nl;
-            }
-          }
-          __syncthreads();
-          break;
-        }
-        if (len + rl <= 64) {
-          // ---- packed register merge: lanes [0, len) hold the work, lanes [len, len + rl) the RHS
-          const uint32_t l = tid;
-          const bool isw = l < len, isr = !isw && l < len + rl;
-          const uint32_t j = l - len;
-          const uint32_t src = isr ? j + 1 : 0u;  // RHS entry j sits in lane j + 1
-          const uint32_t rkey = (uint32_t)__shfl((int)hk_, (int)src);
-          Fe rval;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) rval.l[w] = __shfl(hv_.l[w], (int)src);
-          uint32_t key = 0, stv = kStForb;
-          Fe val = fe_zero();
-          if (isw) { key = wk[cur][l]; val = wv[cur][l]; stv = ws[cur][l]; }
-          if (isr) {
-            key = rkey;
-            val = rval;
-            rk[j] = key;
-            stv = tab_state(tk, tv, key);
-          }
-          wave_sync();  // the RHS keys are in LDS
-          const uint32_t *ok = isw ? rk : wk[cur];
-          const uint32_t on = isw ? rl : (isr ? len : 0u);
-          bool hit;
-          const uint32_t lb = lds_lb64(ok, on, key, hit);
-          if (p4) {
-            // take_signal_4's next pivot is the smallest deleted key of the merged list: known from
-            // the keys alone unless a key of both lists cancels (then the prefetch is just unused)
-            const bool cand = ((isw && l != oi) || (isr && !hit)) && stv != kStForb && (stv & kStDel);
-            uint32_t mk = cand ? key : RS_NONE;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-              const uint32_t o2 = (uint32_t)__shfl_xor((int)mk, d);
-              mk = o2 < mk ? o2 : mk;
-            }
-            if (mk != RS_NONE) {
-              const uint64_t own = __ballot(cand && key == mk);
-              const uint32_t pst = (uint32_t)__shfl((int)stv, __ffsll((long long)own) - 1);
-              const uint64_t pho = pst & ~kStDel;
-              const bool inp = pho + tid < A.pool_cap;
-              hpf_k = inp ? A.pk[pho + tid] : 0u;
-              hpf_v = inp ? A.pv[pho + tid] : fe_zero();
-              pf_st = pst;
-            }
-          }
-          val = fmul256(F, isw ? c2 : coef, val);
-          if (isr) rv[j] = val;
-          wave_sync();
-          bool keep = false;
-          if (isw) {  // -c2*v (+ coef*rv when the RHS has the key)
-            if (l != oi) {
-              val = hit ? fsub(F, rv[lb], val) : fneg(F, val);
-              keep = !fe_is_zero(val);
-            }
-          } else if (isr) {  // RHS-only keys: coef*rv
-            keep = !hit && !fe_is_zero(val);
-          }
-          const uint64_t km = __ballot(keep);
-          const uint64_t wmk = len >= 64 ? km : (km & ((1ull << len) - 1ull)), rmk = km >> len;
-          if (keep) {
-            const uint32_t q = isw ? below(wmk, l) + below(rmk, lb) : below(rmk, j) + below(wmk, lb);
-            wk[nx][q] = key;
-            wv[nx][q] = val;
-            ws[nx][q] = stv;
-          }
-          wave_sync();
-          const uint32_t nlen = (uint32_t)__popcll(km);
-          cur = nx;
-          by += 36ull * (len + rl + nlen);
-          len = nlen;
-          continue;
-        }
-        // ---- general LDS merge: the RHS into rk/rv/rs (the first 63 entries from the round trip)
-        if (tid >= 1 && tid <= rl) {  // lane l >= 1 already holds entry l - 1
-          rk[tid - 1] = hk_;
-          rv[tid - 1] = hv_;
-          rs[tid - 1] = tab_state(tk, tv, hk_);
-        }
-        for (uint32_t jj = 63 + tid; jj < rl; jj += nt) {
-          const uint32_t kk = A.pk[ho + 1 + jj];
-          rk[jj] = kk;
-          rv[jj] = A.pv[ho + 1 + jj];
-          rs[jj] = tab_state(tk, tv, kk);
-        }
-        __syncthreads();
-        // one product per entry, all lanes at once: work entries c2*v, RHS entries coef*rv
-        for (uint32_t q = tid; q < len + rl; q += nt) {
-          if (q < len) wv[cur][q] = fmul256(F, c2, wv[cur][q]);
-          else rv[q - len] = fmul256(F, coef, rv[q - len]);
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < len; i += nt) {  // work keys: -c2*v (+ coef*rv when the RHS has the key)
-          if (i == oi) { fw[i] = 0; continue; }
-          const uint32_t key = wk[cur][i];
-          const uint32_t lb = lds_lower_bound(rk, rl, key);
-          Fe x = fneg(F, wv[cur][i]);
-          if (lb < rl && rk[lb] == key) x = fadd(F, rv[lb], x);
-          wv[cur][i] = x;
-          lbw[i] = lb;
-          fw[i] = fe_is_zero(x) ? 0 : 1;
-        }
-        for (uint32_t jj = tid; jj < rl; jj += nt) {  // RHS-only keys: coef*rv
-          const uint32_t key = rk[jj];
-          const uint32_t lb = lds_lower_bound(wk[cur], len, key);
-          if (lb < len && wk[cur][lb] == key) { fr[jj] = 0; lbr[jj] = RS_NONE; continue; }
-          lbr[jj] = lb;
-          fr[jj] = fe_is_zero(rv[jj]) ? 0 : 1;
-        }
-        __syncthreads();
-        const uint32_t tw = wave_excl_scan(fw, len);
-        const uint32_t tr = wave_excl_scan(fr, rl);
-        for (uint32_t i = tid; i < len; i += nt) {
-          if (i == oi || fe_is_zero(wv[cur][i])) continue;
-          const uint32_t lb = lbw[i];
-          const uint32_t q = fw[i] + (lb < rl ? fr[lb] : tr);
-          wk[nx][q] = wk[cur][i];
-          wv[nx][q] = wv[cur][i];
-          ws[nx][q] = ws[cur][i];
-        }
-        for (uint32_t jj = tid; jj < rl; jj += nt) {
-          const uint32_t lb = lbr[jj];
-          if (lb == RS_NONE || fe_is_zero(rv[jj])) continue;
-          const uint32_t q = fr[jj] + (lb < len ? fw[lb] : tw);
-          wk[nx][q] = rk[jj];
-          wv[nx][q] = rv[jj];
-          ws[nx][q] = rs[jj];
-        }
-        __syncthreads();
-        cur = nx;
-        by += 36ull * (len + rl + tw + tr);
-        len = tw + tr;
-      }
-    }
-    if (tid == 0) {
-      A.n_sub[c] = s_m;
-      A.n_left[c] = s_nl;
-      atomicAdd(A.bytes_main, by);
-      if (!s_ok) atomicOr(A.err, 8);
-      if (A.prof) {
-        unsigned long long *P = A.prof + kProfWords * ci;
-        P[2] = rows;
-        P[5] = wall_clock64() - t_1;
-        P[22] = t_1;  // absolute start (100 MHz)
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// multi_inv (modular_arithmetic.rs:71-91) of the pivot coefficients of every workgroup cluster,
-// before normalisation: one block per cluster, each lane inverts chunks of 64 slots with one
-// inversion per chunk (Montgomery's trick), so no cluster waits on an inversion chain of its own.
-// ftmp[slot] <- h_coef[slot]^-1.
-// Batch inversion of the pivot coefficients (multi_inv, modular_arithmetic.rs:71-91; exact inverses,
-// so the chunking is free): chains of 16 products per lane, blockIdx.y = cluster, blockIdx.x
-// spreads a large cluster's chains over many workgroups (the head's clusters, thousands of
-// substitutions each: short chains are the short critical path).
-__global__ __launch_bounds__(256) void k_batch_inv(ElimArgs A, const uint32_t *ids, uint64_t n_ids) {
-  const FieldP &F = A.F;
-  constexpr uint32_t C = 16;
-  for (uint64_t ci = blockIdx.y; ci < n_ids; ci += gridDim.y) {
-    const uint64_t c = ids[ci];
-    const uint64_t b = A.cl_off[c];
-    const uint32_t m = A.n_sub[c];
-    for (uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * C; c0 < m; c0 += (uint64_t)gridDim.x * blockDim.x * C) {
-      const uint32_t c1 = (uint32_t)min<uint64_t>(m, c0 + C);
-      Fe acc = A.h_coef[b + c0];
-      A.ftmp[b + c0] = acc;
-      for (uint32_t i = (uint32_t)c0 + 1; i < c1; ++i) { acc = fmul(F, acc, A.h_coef[b + i]); A.ftmp[b + i] = acc; }
-      Fe inv = finv(F, acc);
-      for (uint32_t i = c1 - 1; i > c0; --i) {
-        const Fe inv_i = fmul(F, A.ftmp[b + i - 1], inv);
-        inv = fmul(F, inv, A.h_coef[b + i]);
-        A.ftmp[b + i] = inv_i;
-      }
-      A.ftmp[b + c0] = inv;
-    }
-  }
-}
+// multi_inv (modular_arithmetic.rs:71-91) of the pivot coefficients, before normalisation (exact
+// inverses, so the chunking is free).
 // The same inverses with one Fermat inversion per cluster (one workgroup each): thread t takes a
 // contiguous chunk of the pivots, the chunks' products are scanned across the workgroup both ways
 // (prefix X_t, suffix S_t) in LDS, and the inverse of the whole product -- the only inversion --
@@ -2586,23 +2003,6 @@ __global__ void k_batch_inv_flat(ElimArgs A, const uint32_t *cid, const uint8_t 
     }
     A.ftmp[cur] = inv;
   }
-}
-
-// normalize_substitutions (:414-437) over the slot space of the flagged clusters (cls == 1), one
-// lane per substitution: the tail stream's clusters when their composition runs level by level
-// over the whole GPU (k_compose_level) instead of inside k_big_finish
-__global__ void k_normalize_flat(ElimArgs A, const uint32_t *cid, const uint8_t *cls, uint64_t n_slots) {
-  const FieldP &F = A.F;
-  unsigned long long by = 0;
-  for (uint64_t sl = gtid(); sl < n_slots; sl += gstride()) {
-    if (!d_inv_slot(A, cid, cls, sl)) continue;
-    const Fe inv_i = A.ftmp[sl];
-    Fe *vv = A.pv + A.h_off[sl];
-    const uint32_t l = A.h_len[sl];
-    for (uint32_t t = 0; t < l; ++t) vv[t] = fmul(F, vv[t], inv_i);
-    by += 64ull * (l + 1);
-  }
-  wave_atomic_add(A.bytes_fin, by);
 }
 
 // Lane-serial composition of slot `sl` (raw_substitution key by key, ascending): the fallback for

@@ -27,7 +27,7 @@
 // beyond that finishes at its turn on lane 0 (d_treat_scalar over the global state, kept current).
 //
 // LDS: the cluster's signal table (open addressing over the touched signals; state = bit 31 deleted +
-// the holder's header offset, else the occurrence count -- as k_big_main_lds), per wave the merge's
+// the holder's header offset, else the occurrence count), per wave the merge's
 // key lists and the recorded keys, the commit ring.  A cluster whose signals do not fit runs
 // k_big_main's loop on wave 0.
 #pragma once
@@ -709,7 +709,14 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
       const bool ok = lds_ld(&S.s_ok) != 0;
       uint32_t piv = RS_NONE;
       // row j's ring slots were row j - 64's: its stores must be known complete before they are reused
-      for (uint32_t it = 0; lds_ld_sc(&S.s_vis) + kSpecRing <= j && it <= kSpecSpin; ++it) __builtin_amdgcn_s_sleep(1);
+      {
+        uint32_t it = 0;
+        for (; lds_ld_sc(&S.s_vis) + kSpecRing <= j && it <= kSpecSpin; ++it) __builtin_amdgcn_s_sleep(1);
+        if (it > kSpecSpin) {  // out of budget: the slot is not safe to reuse -- abort (err bit 64)
+          lds_st(&S.s_abort, 1);
+          break;
+        }
+      }
       if (lane == 0) {
         lds_st_sc(&S.hoff[j % kSpecRing], RS_NONE);
         lds_st_sc(&S.hrow[j % kSpecRing], j);
@@ -740,7 +747,14 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
       if (!done && R.serial) {  // lane 0 finishes the row on the global state (d_treat_scalar)
         pc[1]++;
         // every earlier row's global stores, and this row's occurrence writes, complete
-        for (uint32_t it = 0; lds_ld_sc(&S.s_vis) < j && it <= kSpecSpin; ++it) __builtin_amdgcn_s_sleep(1);
+        {
+          uint32_t it = 0;
+          for (; lds_ld_sc(&S.s_vis) < j && it <= kSpecSpin; ++it) __builtin_amdgcn_s_sleep(1);
+          if (it > kSpecSpin) {  // out of budget: the global state may be incomplete -- abort (err bit 64)
+            lds_st(&S.s_abort, 1);
+            break;
+          }
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         if (lane == 0) {
           uint32_t m = S.s_m, nl = S.s_nl;

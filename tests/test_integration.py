@@ -158,3 +158,33 @@ def test_rust_glue_uses_only_reference_bigint_calls():
 def test_rust_lib_doc_abi_matches_header():
     ver = re.search(r"#define RS_ABI_VERSION (\d+)", open(HDR).read()).group(1)
     assert f"(ABI {ver})" in open(RS).read().splitlines()[0]
+
+
+PATCH = os.path.join(ROOT, "integration", "rust", "circom_algebra_new_unchecked.patch")
+REF_ALGEBRA = "/root/reference/circom_algebra/src/algebra.rs"
+
+
+def test_rust_glue_constraint_calls_come_from_reference_or_patch(tmp_path):
+    """The drop-in is complete as committed: every Constraint associated function the glue calls is
+    public in the reference's circom_algebra (algebra.rs) or added by the committed patch
+    (integration/rust/circom_algebra_new_unchecked.patch: `pub fn new_unchecked`, next to the private
+    Constraint::new of algebra.rs:1012), and the patch applies to the reference's file."""
+    src = re.sub(r"//[^\n]*", "", open(GLUE).read())
+    calls = set(re.findall(r"\bC::(\w+)\(", src)) | set(re.findall(r"\bConstraint::(\w+)\(", src))
+    patch = open(PATCH).read()
+    added = set(re.findall(r"^\+[ \t]*pub fn (\w+)\(", patch, flags=re.M))
+    assert added == {"new_unchecked"}
+    assert re.search(r"^\+\s*pub fn new_unchecked\(a: HashMap<C, BigInt>, b: HashMap<C, BigInt>, c: HashMap<C, BigInt>\)"
+                     r" -> Constraint<C> \{\n\+\s*Constraint::new\(a, b, c\)", patch, flags=re.M)
+    assert "new_unchecked" in calls
+    if not os.path.exists(REF_ALGEBRA):  # the GPU box has no reference tree
+        assert calls <= added
+        return
+    public = set(re.findall(r"^\s*pub fn (\w+)\(", open(REF_ALGEBRA).read(), flags=re.M))
+    assert "new_unchecked" not in public
+    assert calls <= public | added, calls - public - added
+    dst = tmp_path / "circom_algebra" / "src"
+    dst.mkdir(parents=True)
+    (dst / "algebra.rs").write_bytes(open(REF_ALGEBRA, "rb").read())
+    r = subprocess.run(["patch", "-p1", "--dry-run", "-d", str(tmp_path), "-i", PATCH], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -246,3 +246,20 @@ def test_asan_ubsan_check(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "asan_check: OK" in r.stdout
+
+
+def test_map_lists_across_rounds(tmp_path):
+    """The lazily built row lists of the non-linear signal map (csrc/maplists.hpp; the appends of
+    apply_substitution_to_map, constraint_simplification.rs:369-377) equal the plain recursion over
+    the rounds' substitution batches, with ONE memo living through 8 rounds as in the engine: a list
+    memoised in an earlier round must never answer for another (signal, bound) pair after more
+    batches arrive (round-3 advisor finding: the memo key depended on the batch count)."""
+    import subprocess
+    root = os.path.dirname(HERE)
+    exe = str(tmp_path / "maplists_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "circom_cvm_amd", "csrc"),
+                           os.path.join(HERE, "maplists_check.cpp"), "-o", exe])
+    for seed in range(1, 13):
+        for rounds, signals in ((8, 40), (5, 200), (12, 25)):
+            out = subprocess.run([exe, str(seed), str(rounds), str(signals)], capture_output=True, text=True)
+            assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
