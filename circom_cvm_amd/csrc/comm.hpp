@@ -14,7 +14,10 @@
 //                one-GPU box, and it is what rs_simplify_multi uses when a device is listed twice.
 #pragma once
 
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <cstring>
@@ -41,20 +44,79 @@ struct Comm {
   virtual uint64_t max_u64(uint64_t v, hipStream_t st) = 0;
   // host vector gather: out[q] = rank q's v
   virtual std::vector<uint64_t> gather_u64(uint64_t v, hipStream_t st) = 0;
+  // every rank has arrived (and its work on `st` before the call is complete)
+  virtual void barrier(hipStream_t st) { (void)gather_u64(0, st); }
+  // Collective: host memory every rank of the group sees at the same bytes (page-locked, registered
+  // with HIP, so each rank's D2H of its own part of the result lands there directly over its own
+  // PCIe link).  Slot `slot` grows only; every rank passes the same size.  nullptr if unavailable.
+  virtual void *shared_host(int slot, size_t bytes, hipStream_t st) = 0;
 };
 
 // ------------------------------------------------------------------ RCCL
+// one process per rank: the shared host region is a POSIX shared-memory segment each rank maps and
+// registers; its name carries a tag rank 0 chose (sent with the first gather) and a generation
+struct ShmSeg {
+  void *p = nullptr;
+  size_t cap = 0;
+  bool registered = false;
+};
 struct RcclComm : Comm {
   ncclComm_t c = nullptr;
   uint64_t *d_scalar = nullptr;  // W u64 of device scratch for the scalar collectives
+  ShmSeg shm[4];
+  uint64_t shm_tag = 0, shm_gen = 0;
   RcclComm(ncclComm_t comm, int r, int w) : c(comm) {
     rank = r;
     world = w;
     HC(hipMalloc((void **)&d_scalar, 8 * (size_t)w));
   }
   ~RcclComm() override {
+    for (ShmSeg &g : shm) unmap(g);
     if (d_scalar) (void)hipFree(d_scalar);
     if (c) (void)ncclCommDestroy(c);
+  }
+  static void unmap(ShmSeg &g) {
+    if (!g.p) return;
+    if (g.registered) (void)hipHostUnregister(g.p);
+    munmap(g.p, g.cap);
+    g = ShmSeg{};
+  }
+  void *shared_host(int slot, size_t bytes, hipStream_t st) override {
+    ShmSeg &g = shm[slot];
+    if (g.p && g.cap >= bytes) return g.p;
+    if (!shm_tag) shm_tag = gather_u64(rank == 0 ? ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)this : 0, st)[0] | 1;
+    const size_t cap = std::max(bytes, g.cap + g.cap / 4);
+    unmap(g);
+    char name[96];
+    snprintf(name, sizeof name, "/rs_simplify_%llx_%d_%llu", (unsigned long long)shm_tag, slot, (unsigned long long)++shm_gen);
+    int ok = 1;
+    if (rank == 0) {
+      const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+      ok = fd >= 0 && ftruncate(fd, (off_t)cap) == 0;
+      if (fd >= 0) close(fd);
+    }
+    ok = (int)max_u64(ok ? 0 : 1, st) == 0;  // rank 0 created it (also the barrier before the opens)
+    void *p = MAP_FAILED;
+    if (ok) {
+      const int fd = shm_open(name, O_RDWR, 0600);
+      if (fd >= 0) {
+        p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+      }
+    }
+    const bool mine = p != MAP_FAILED && hipHostRegister(p, cap, hipHostRegisterDefault) == hipSuccess;
+    ok = (int)max_u64(mine ? 0 : 1, st) == 0;  // every rank mapped it: the name can go
+    if (rank == 0) shm_unlink(name);
+    if (p != MAP_FAILED) {
+      g.p = p;
+      g.cap = cap;
+      g.registered = mine;
+    }
+    if (!ok) {
+      unmap(g);
+      return nullptr;
+    }
+    return g.p;
   }
   void allgatherv(const void *send, void *recv, const std::vector<uint64_t> &counts, hipStream_t st) override {
     uint64_t off = 0;
@@ -97,7 +159,15 @@ struct LocalGroup {
   uint64_t gen = 0;
   int arrived = 0;
   std::vector<std::vector<uint8_t>> slot;
+  struct Host {
+    void *p = nullptr;
+    size_t cap = 0;
+  } host[4];  // the group's shared host regions (one process: one pinned allocation each)
   explicit LocalGroup(int w) : world(w), slot(w) {}
+  ~LocalGroup() {
+    for (Host &h : host)
+      if (h.p) (void)hipHostFree(h.p);
+  }
   void barrier() {
     std::unique_lock<std::mutex> lk(m);
     uint64_t g = gen;
@@ -166,6 +236,25 @@ struct LocalComm : Comm {
     uint64_t m = 0;
     for (uint64_t x : gather_u64(v, st)) m = std::max(m, x);
     return m;
+  }
+  void barrier(hipStream_t st) override {
+    HC(hipStreamSynchronize(st));
+    g->barrier();
+  }
+  void *shared_host(int slot, size_t bytes, hipStream_t st) override {
+    HC(hipStreamSynchronize(st));
+    g->barrier();  // nobody still uses the old region
+    LocalGroup::Host &h = g->host[slot];
+    if (rank == 0 && h.cap < bytes) {
+      const size_t cap = std::max(bytes, h.cap + h.cap / 4);
+      if (h.p) (void)hipHostFree(h.p);
+      h.p = nullptr;
+      h.cap = 0;
+      if (hipHostMalloc(&h.p, cap, hipHostMallocDefault) == hipSuccess) h.cap = cap;
+      else h.p = nullptr;
+    }
+    g->barrier();
+    return h.cap >= bytes ? h.p : nullptr;
   }
 };
 

@@ -2,9 +2,8 @@
 //
 // Host orchestration of constraint_list/src/constraint_simplification.rs:442-730 around the HIP
 // kernels of kernels.hpp.  Every step says which part of simplification() it restates.  All
-// field arithmetic runs on the GPU; the host keeps the ordered bookkeeping the reference keeps
-// in Rust collections (cluster arena order, the non-linear signal map of rounds >= 2) and the
-// lists of forbidden-only constraints (lconst), which only ever need fix_constraint.
+// field arithmetic and every constraint row stay on the GPU; the host keeps the ordered
+// bookkeeping the reference keeps in Rust collections (the non-linear signal map of rounds >= 2).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -149,17 +148,7 @@ static void launch(hipStream_t st, K kernel, uint64_t n, Args... args) {
 #include "comm.hpp"
 namespace rs {
 
-// host view of ragged rows (keys only unless vals requested)
-struct HostRows {
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> len;
-  std::vector<uint32_t> key;
-};
 
-struct HostCon {  // canonical, sorted keys
-  std::vector<uint32_t> k[3];
-  std::vector<uint64_t> v[3];
-};
 
 }  // namespace rs
 
@@ -191,7 +180,6 @@ struct rs_engine {
   // result
   uint64_t out_n_dev = 0;  // constraints gathered on device
   uint64_t out_nnz[3] = {0, 0, 0};
-  std::vector<HostCon> out_host_tail;  // lconst rows appended after the device rows
   uint64_t n_wires = 0, npiw = 0;
   rs_stats stats{};
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr, ev5 = nullptr, ev6 = nullptr, ev7 = nullptr;
@@ -232,6 +220,16 @@ struct rs_engine {
   bool snap_on = false;     // the early region was taken in this run
   uint64_t snap_e[3] = {0, 0, 0};  // early-region entries per part
   uint64_t out_ext[3] = {0, 0, 0};  // streamed layout: early + late entries per part
+  // Sharded host -> host result: every rank holds the whole result on its device and
+  // copies only ITS share -- the storage rows of non-linear rows [nl_lo, nl_hi), the last rank also the
+  // linear tail -- into host memory all ranks share (Comm::shared_host), so the D2H leg is split over
+  // the ranks' PCIe links.  Entries of part q: rank r's [early | late] at r * sh_cap[q] (capacities
+  // agreed over the ranks; gaps allowed by ABI 7); rows: the shared ptr / end arrays at global rows.
+  uint64_t nl_lo = 0, nl_hi = UINT64_MAX;
+  uint64_t sh_cap[3] = {0, 0, 0};
+  void *sh_ent = nullptr;       // shared slot 0: col of a, b, c then val of a, b, c
+  bool sh_full = false;         // the region was regrown at the end: the whole [early | late] is copied
+  uint64_t sh_klo = 0, sh_khi = 0;  // this rank's run of the keep list (global output rows)
   hipEvent_t ev_snap = nullptr, ev_snap0 = nullptr;  // early gather done / its inputs ready
   // The early region's D2H runs on its own host thread, in chunks, one in flight at a time: the
   // copy engine serves transfers in order, so one large transfer would hold every small D2H the run
@@ -252,12 +250,12 @@ struct rs_engine {
   // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
   // when the streamed run skipped it
   bool csr_ready = false;
-  // Invariant: these point into arena buffers (sv.*, fin.keep, fin.lvids, fin.zlen) and the storage
+  // Invariant: these point into arena buffers (sv.*, fin.*, lc.*) and the storage
   // heap as the run left them; nothing between the run and ensure_csr may move them (fin_gen = the
   // arena generation then; ensure_csr refuses a stale view instead of gathering from freed memory).
-  DRows fin_parts[3] = {}, fin_lvq[3] = {};
-  const uint32_t *fin_keep_ids = nullptr, *fin_lv_ids = nullptr;
-  uint64_t fin_keep = 0, fin_lvn = 0, fin_gen = 0;
+  DRows fin_parts[3] = {}, fin_xq[2][3] = {};  // storage rows; extras: leftover linear rows, lconst
+  const uint32_t *fin_keep_ids = nullptr, *fin_x_ids[2] = {nullptr, nullptr};
+  uint64_t fin_keep = 0, fin_xn[2] = {0, 0}, fin_gen = 0;
 };
 
 namespace rs {
@@ -267,6 +265,39 @@ namespace rs {
 // anything reads a row.
 // what of a block to send: everything, the row pointers + keys, or the values alone
 enum UpPart { kUpAll = 0, kUpKeys = 1, kUpVals = 2 };
+
+// A sharded engine uploads only its share of every block over its own PCIe link --
+// rows [lo[r], lo[r + 1]) and their entries [ptr[lo[r]], ptr[lo[r + 1]]) -- and the ranks complete
+// each other's blocks over xGMI: the shares are contiguous in rank order, so one allgatherv per
+// array puts every array together in place.  Row bounds balance the entries.  The host reads the
+// (still unvalidated) row pointers only at the W + 1 bounds, and every rank computes the same bounds
+// from the same input, so a malformed input is rejected by all ranks before any collective.
+struct RowSplit {
+  std::vector<uint64_t> lo, e;  // W + 1 row bounds, their entry offsets
+};
+static RowSplit split_rows(const rs_lc &src, int W, const char *name) {
+  RowSplit sp;
+  const uint64_t n = src.n_rows, nnz = n ? src.nnz : 0;
+  sp.lo.assign(W + 1, 0);
+  sp.e.assign(W + 1, 0);
+  sp.lo[W] = n;
+  sp.e[W] = nnz;
+  if (n && (src.ptr[0] != 0 || src.ptr[n] != nnz))
+    throw RsError(RS_E_INVALID, std::string(name) + " block: bad row pointers (ptr[0] != 0 or ptr[n_rows] != nnz)");
+  for (int q = 1; q < W; ++q) {
+    const uint64_t want = (unsigned __int128)nnz * q / W;
+    uint64_t a = sp.lo[q - 1], b = n;  // first row whose pointer reaches `want`
+    while (a < b) {
+      const uint64_t m = a + (b - a) / 2;
+      if (src.ptr[m] < want) a = m + 1; else b = m;
+    }
+    sp.lo[q] = a;
+    sp.e[q] = src.ptr[a];
+    if (sp.e[q] < sp.e[q - 1] || sp.e[q] > nnz)
+      throw RsError(RS_E_INVALID, std::string(name) + " block: bad row pointers (decreasing)");
+  }
+  return sp;
+}
 static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, const char *name, int part = kUpAll) {
   if (src.n_rows && !src.ptr) throw RsError(RS_E_INVALID, std::string(name) + ": rows without a ptr array");
   if (src.nnz && (!src.col || !src.val)) throw RsError(RS_E_INVALID, std::string(name) + ": entries without col/val");
@@ -278,12 +309,36 @@ static void upload_block(rs_engine *E, const rs_lc &src, rs_engine::Blk &dst, co
   dst.key = E->A.get<uint32_t>(nm + ".key", dst.nnz);
   dst.val = E->A.get<Fe>(nm + ".val", dst.nnz);
   hipStream_t s = E->stc;
-  if (part != kUpVals) {
-    if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, s));
-    else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), s));
-    if (dst.nnz) HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, s));
+  Comm *CM = E->comm.get();
+  const int W = CM ? CM->world : 1, r = CM ? CM->rank : 0;
+  if (W == 1 || !dst.n) {
+    if (part != kUpVals) {
+      if (dst.n) HC(hipMemcpyAsync(dst.ptr, src.ptr, sizeof(uint64_t) * (dst.n + 1), hipMemcpyHostToDevice, s));
+      else HC(hipMemsetAsync(dst.ptr, 0, sizeof(uint64_t), s));
+      if (dst.nnz) HC(hipMemcpyAsync(dst.key, src.col, sizeof(uint32_t) * dst.nnz, hipMemcpyHostToDevice, s));
+    }
+    if (part != kUpKeys && dst.nnz) HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, s));
+    return;
   }
-  if (part != kUpKeys && dst.nnz) HC(hipMemcpyAsync(dst.val, src.val, 32 * dst.nnz, hipMemcpyHostToDevice, s));
+  // sharded: this rank's share, then the allgathervs (row pointers: the last share also carries ptr[n])
+  const RowSplit sp = split_rows(src, W, name);
+  const uint64_t r0 = sp.lo[r], r1 = sp.lo[r + 1] + (r == W - 1 ? 1 : 0), e0 = sp.e[r], e1 = sp.e[r + 1];
+  std::vector<uint64_t> cp(W), ck(W), cv(W);
+  for (int q = 0; q < W; ++q) {
+    cp[q] = 8 * (sp.lo[q + 1] - sp.lo[q] + (q == W - 1 ? 1 : 0));
+    ck[q] = 4 * (sp.e[q + 1] - sp.e[q]);
+    cv[q] = 32 * (sp.e[q + 1] - sp.e[q]);
+  }
+  if (part != kUpVals) {
+    if (r1 > r0) HC(hipMemcpyAsync(dst.ptr + r0, src.ptr + r0, 8 * (r1 - r0), hipMemcpyHostToDevice, s));
+    if (e1 > e0) HC(hipMemcpyAsync(dst.key + e0, src.col + e0, 4 * (e1 - e0), hipMemcpyHostToDevice, s));
+    CM->allgatherv(dst.ptr + r0, dst.ptr, cp, s);
+    CM->allgatherv(dst.key + e0, dst.key, ck, s);
+  }
+  if (part != kUpKeys) {
+    if (e1 > e0) HC(hipMemcpyAsync(dst.val + e0, src.val + 4 * e0, 32 * (e1 - e0), hipMemcpyHostToDevice, s));
+    CM->allgatherv(dst.val + e0, dst.val, cv, s);
+  }
 }
 
 // ---------------------------------------------------------------- pipelined load
@@ -327,6 +382,31 @@ static void load_enqueue(rs_engine *E, const rs_input *in, bool staged) {
   E->h2d_wait_ms = 0;
   E->staged = staged;
   E->hin = staged ? in : nullptr;
+  E->nl_lo = 0;
+  E->nl_hi = UINT64_MAX;
+  if (E->comm && E->comm->world > 1 && in->nl_a.n_rows) {
+    // this rank's share of the non-linear rows for the result's D2H: entries of A + B + C balanced
+    const int W = E->comm->world, r = E->comm->rank;
+    const rs_lc *b3[3] = {&in->nl_a, &in->nl_b, &in->nl_c};
+    const uint64_t n = in->nl_a.n_rows;
+    for (const rs_lc *L : b3)
+      if (!L->ptr) throw RsError(RS_E_INVALID, "non-linear block: rows without a ptr array");
+    auto cum = [&](uint64_t row) { return b3[0]->ptr[row] + b3[1]->ptr[row] + b3[2]->ptr[row]; };
+    const uint64_t tot = cum(n);
+    auto bound = [&](int q) -> uint64_t {
+      if (q <= 0) return 0;
+      if (q >= W) return n;
+      const uint64_t want = (unsigned __int128)tot * q / W;
+      uint64_t a = 0, b = n;
+      while (a < b) {
+        const uint64_t m = a + (b - a) / 2;
+        if (cum(m) < want) a = m + 1; else b = m;
+      }
+      return a;
+    };
+    E->nl_lo = bound(r);
+    E->nl_hi = std::max(E->nl_lo, bound(r + 1));
+  }
   int *vf = E->A.get<int>("vflag", 10);
   HC(hipMemsetAsync(vf, 0, 40, E->stc));
   hipStream_t s = E->stc;
@@ -405,6 +485,13 @@ static void load_wait(rs_engine *E, int g) {
 }
 static void load_wait_all(rs_engine *E) {
   for (int g = 0; g < 4; ++g) load_wait(E, g);
+}
+// Sharded: the main stream's collectives (the exchange) run after every input group's allgathervs
+// on the copy stream have completed on this rank -- so no rank has collectives of both streams of
+// one communicator in flight at once.  Device-side ordering only: the verdicts are read later.
+static void load_order_collectives(rs_engine *E) {
+  for (int g = 0; g < 4; ++g)
+    if (E->pending[g]) HC(hipStreamWaitEvent(E->st, E->ev_grp[g], 0));
 }
 // After a failed call: the copy stream may still be reading the caller's buffers.
 static void snap_join(rs_engine *E);
@@ -497,6 +584,15 @@ static void sort_pairs(rs_engine *E, const K *kin, K *kout, const V *vin, V *vou
   HC(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, E->st));
   void *tmp = E->A.get<uint8_t>(std::string("sort.tmp.") + tag, tb);
   HC(rocprim::radix_sort_pairs(tmp, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, E->st));
+}
+
+template <class K>
+static void sort_keys(rs_engine *E, const K *kin, K *kout, uint64_t n, int end_bit, const char *tag) {
+  if (!n) return;
+  size_t tb = 0;
+  HC(rocprim::radix_sort_keys(nullptr, tb, kin, kout, (size_t)n, 0, end_bit, E->st));
+  void *tmp = E->A.get<uint8_t>(std::string("sortk.tmp.") + tag, tb);
+  HC(rocprim::radix_sort_keys(tmp, tb, kin, kout, (size_t)n, 0, end_bit, E->st));
 }
 
 __global__ void k_u32_to_u64(const uint32_t *in, uint64_t *out, uint64_t n) {
@@ -599,11 +695,6 @@ __global__ void k_zero_c(const uint32_t *ids, uint64_t n, uint32_t *clen) {
 }
 __global__ void k_nonempty_flags(const uint32_t *la, const uint32_t *lb, const uint32_t *lc, uint64_t n, uint64_t *flag) {
   for (uint64_t i = gtid(); i < n; i += gstride()) flag[i] = (la[i] | lb[i] | lc[i]) ? 1 : 0;
-}
-
-__global__ void k_compact_keys(DRows V, const uint64_t *doff, uint32_t *out) {
-  for (uint64_t r = gtid(); r < V.n; r += gstride())
-    for (uint32_t i = 0; i < V.len[r]; ++i) out[doff[r] + i] = V.key[V.off[r] + i];
 }
 
 // (signal, row) pairs of the round-1 storage rows for the flagged signals: the initial lists of
@@ -763,31 +854,52 @@ __global__ void k_mark_relevant(DRows R, const int32_t *eq_rep, const uint8_t *c
     }
 }
 
-// ---------------------------------------------------------------- host clustering
-// build_clusters (constraint_simplification.rs:45-99): arena order + dest ++ src lists.
-// D2H of the keys of a ragged view (C parts)
-static void fetch_keys(rs_engine *E, const DRows &V, HostRows &H) {
-  H.off.resize(V.n);
-  H.len.resize(V.n);
-  if (V.n == 0) return;
-  HC(hipMemcpyAsync(H.off.data(), V.off, 8 * V.n, hipMemcpyDeviceToHost, E->st));
-  HC(hipMemcpyAsync(H.len.data(), V.len, 4 * V.n, hipMemcpyDeviceToHost, E->st));
-  HC(hipStreamSynchronize(E->st));
-  // compact into a dense key array: gather on device
-  uint64_t tot = 0;
-  std::vector<uint64_t> doff(V.n);
-  for (uint64_t r = 0; r < V.n; ++r) { doff[r] = tot; tot += H.len[r]; }
-  H.key.resize(tot);
-  if (tot == 0) { for (uint64_t r = 0; r < V.n; ++r) H.off[r] = doff[r]; return; }
-  uint64_t *d_doff = E->A.get<uint64_t>("fk.doff", V.n);
-  uint32_t *d_key = E->A.get<uint32_t>("fk.key", tot);
-  h2d(E, d_doff, doff.data(), 8 * V.n);
-  launch(E->st, k_compact_keys, V.n, V, (const uint64_t *)d_doff, d_key);
-  HC(hipMemcpyAsync(H.key.data(), d_key, 4 * tot, hipMemcpyDeviceToHost, E->st));
-  HC(hipStreamSynchronize(E->st));
-  H.off = doff;
+// ---------------------------------------------------------------- lconst on the device
+// The forbidden-only constraints the reference collects in `lconst` -- eq_simplification's pair rows
+// (:181-187), constant_eq_simplification's kept rows (:253-273), every round's cluster leftovers
+// (:318-323, :629-634) and at --O1 the linear rows themselves (:575-577) -- as C-only rows of one
+// device heap, in lconst order.  fix_constraint (algebra.rs:1155-1157; for a row with A = B = empty
+// it only removes zero coefficients) is applied as they are copied in; a row it empties stays with
+// length 0 and is dropped with the other empty rows at the end (extract_with(is_empty), :697).
+// Rows of a source view (ids == nullptr: rows 0..n) -- cnt[i]: its non-zero entries.
+__global__ void k_lc_count(DRows src, const uint32_t *ids, uint64_t n, uint64_t *cnt) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint64_t r = ids ? ids[i] : i;
+    const uint64_t o = src.off[r];
+    uint64_t c = 0;
+    for (uint32_t t = 0; t < src.len[r]; ++t) c += fe_is_zero(src.val[o + t]) ? 0 : 1;
+    cnt[i] = c;
+  }
+}
+// ... copied to the heap: row row0 + i at entry base + pos[i]
+__global__ void k_lc_copy(DRows src, const uint32_t *ids, uint64_t n, const uint64_t *pos, uint64_t base, uint64_t row0,
+                          DRows lc) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint64_t r = ids ? ids[i] : i;
+    const uint64_t o = src.off[r], w0 = base + pos[i];
+    uint64_t w = w0;
+    for (uint32_t t = 0; t < src.len[r]; ++t) {
+      const Fe v = src.val[o + t];
+      if (fe_is_zero(v)) continue;
+      lc.key[w] = src.key[o + t];
+      lc.val[w] = v;
+      ++w;
+    }
+    lc.off[row0 + i] = w0;
+    lc.len[row0 + i] = (uint32_t)(w - w0);
+  }
+}
+// the leftover slots of a round in lconst order (cluster index, then push order): flag[s] = s is a
+// leftover slot of its cluster
+__global__ void k_left_flags(const uint32_t *cid, const uint64_t *cl_off, const uint32_t *n_left, uint64_t n, uint64_t *flag) {
+  for (uint64_t s = gtid(); s < n; s += gstride()) {
+    const uint32_t c = cid[s];
+    flag[s] = s - cl_off[c] < n_left[c] ? 1 : 0;
+  }
 }
 
+// ---------------------------------------------------------------- host clustering
+// build_clusters (constraint_simplification.rs:45-99): arena order + dest ++ src lists.
 // D2H canonical content of pool maps (leftovers or RHS)
 static void fetch_pool_maps(rs_engine *E, const std::vector<uint64_t> &off, const std::vector<uint32_t> &len,
                             const uint32_t *pk, const Fe *pv, std::vector<uint32_t> &keys, std::vector<uint64_t> &vals,
@@ -837,24 +949,6 @@ static void fetch_pool_keys(rs_engine *E, const std::vector<uint64_t> &off, cons
 
 static bool is_zero4(const uint64_t *v) { return (v[0] | v[1] | v[2] | v[3]) == 0; }
 
-// fix_constraint for a host lconst row (always linear: only zero removal)
-static void host_fix(HostCon &c) {
-  for (int q = 0; q < 3; ++q) {
-    size_t w = 0;
-    for (size_t i = 0; i < c.k[q].size(); ++i)
-      if (!is_zero4(&c.v[q][4 * i])) {
-        c.k[q][w] = c.k[q][i];
-        for (int t = 0; t < 4; ++t) c.v[q][4 * w + t] = c.v[q][4 * i + t];
-        ++w;
-      }
-    c.k[q].resize(w);
-    c.v[q].resize(4 * w);
-  }
-  if (c.k[0].empty() || c.k[1].empty()) {
-    c.k[0].clear(); c.v[0].clear();
-    c.k[1].clear(); c.v[1].clear();
-  }
-}
 
 // ---------------------------------------------------------------- elimination driver
 struct ElimOut {
@@ -1630,30 +1724,57 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   throw RsError(RS_E_OOM_DEVICE, "substitution pool exhausted");
 }
 
-// leftovers (cluster order, then push order) -> host lconst
-static void collect_leftovers(rs_engine *E, const ElimOut &eo, const Pool &P, std::vector<HostCon> &lconst) {
-  std::vector<uint64_t> slots;
-  for (uint64_t c = 0; c < eo.n_clusters; ++c)
-    for (uint32_t i = 0; i < eo.n_left[c]; ++i) slots.push_back(eo.cl_off[c] + i);
-  if (slots.empty()) return;
-  uint64_t n = slots.size();
-  std::vector<uint64_t> all_off(eo.cl_off.back());
-  std::vector<uint32_t> all_len(eo.cl_off.back());
-  HC(hipMemcpyAsync(all_off.data(), E->A.get<uint64_t>("el.l_off", 1), 8 * all_off.size(), hipMemcpyDeviceToHost, E->st));
-  HC(hipMemcpyAsync(all_len.data(), E->A.get<uint32_t>("el.l_len", 1), 4 * all_len.size(), hipMemcpyDeviceToHost, E->st));
-  HC(hipStreamSynchronize(E->st));
-  std::vector<uint64_t> off(n);
-  std::vector<uint32_t> len(n);
-  for (uint64_t i = 0; i < n; ++i) { off[i] = all_off[slots[i]]; len[i] = all_len[slots[i]]; }
-  std::vector<uint32_t> keys;
-  std::vector<uint64_t> vals, optr;
-  fetch_pool_maps(E, off, len, P.pk, P.pv, keys, vals, optr);
-  for (uint64_t i = 0; i < n; ++i) {
-    HostCon c;
-    c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
-    c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
-    lconst.push_back(std::move(c));
+// The device lconst heap (see k_lc_count): rows appended in lconst order, C-only, Montgomery form.
+struct LcHeap {
+  uint64_t n = 0, top = 0;  // rows, entries
+  DRows view(Arena &A) {
+    DRows v{};
+    v.n = n;
+    v.off = A.get<uint64_t>("lc.off", 1);
+    v.len = A.get<uint32_t>("lc.len", 1);
+    v.key = A.get<uint32_t>("lc.key", 1);
+    v.val = A.get<Fe>("lc.val", 1);
+    return v;
   }
+  // rows ids[0..m) (ids == nullptr: 0..m) of `src`, fixed (zeros dropped)
+  void append(rs_engine *E, const DRows &src, const uint32_t *ids, uint64_t m) {
+    if (!m) return;
+    Arena &A = E->A;
+    hipStream_t st = E->st;
+    uint64_t *cnt = A.get<uint64_t>("lc.cnt", m), *pos = A.get<uint64_t>("lc.pos", m);
+    launch(st, k_lc_count, m, src, ids, m, cnt);
+    const uint64_t tot = excl_scan_u64(E, cnt, pos, m, "lc");
+    A.grow_keep<uint64_t>("lc.off", n + m, n, st, st);
+    A.grow_keep<uint32_t>("lc.len", n + m, n, st, st);
+    A.grow_keep<uint32_t>("lc.key", top + tot, top, st, st);
+    A.grow_keep<Fe>("lc.val", top + tot, top, st, st);
+    launch(st, k_lc_copy, m, src, ids, m, (const uint64_t *)pos, top, n, view(A));
+    n += m;
+    top += tot;
+  }
+};
+
+// a round's leftovers (cluster order, then push order) -> the lconst heap
+static void collect_leftovers(rs_engine *E, const ElimOut &eo, const Pool &P, LcHeap &lc) {
+  const uint64_t n_slots = eo.cl_off.empty() ? 0 : eo.cl_off.back();
+  uint64_t nl = 0;
+  for (uint32_t x : eo.n_left) nl += x;
+  if (!nl || !n_slots) return;
+  Arena &A = E->A;
+  uint64_t *f = A.get<uint64_t>("lc.lf", n_slots), *fp = A.get<uint64_t>("lc.lp", n_slots);
+  uint32_t *slots = A.get<uint32_t>("lc.slots", nl);
+  launch(E->st, k_left_flags, n_slots, (const uint32_t *)A.get<uint32_t>("cl.cid", 1), (const uint64_t *)A.get<uint64_t>("el.cl", 1),
+         (const uint32_t *)A.get<uint32_t>("el.n_left", 1), n_slots, f);
+  const uint64_t m = excl_scan_u64(E, f, fp, n_slots, "lcl");
+  if (m != nl) throw RsError(RS_E_INTERNAL, "leftover count mismatch");
+  launch(E->st, k_scatter_ids, n_slots, (const uint64_t *)f, (const uint64_t *)fp, n_slots, slots);
+  DRows src{};
+  src.n = n_slots;
+  src.off = A.get<uint64_t>("el.l_off", 1);
+  src.len = A.get<uint32_t>("el.l_len", 1);
+  src.key = P.pk;
+  src.val = P.pv;
+  lc.append(E, src, slots, m);
 }
 
 // ---------------------------------------------------------------- substitution log
@@ -1833,6 +1954,24 @@ static void *pin_get(rs_engine *E, int slot, size_t bytes) {
   return b.p;
 }
 
+// the shared entry region of a sharded result: col of a, b, c (W x sh_cap[q] each), then val of a, b, c
+static uint64_t sh_ent_bytes(rs_engine *E) {
+  const uint64_t W = E->comm->world;
+  return 36 * W * (E->sh_cap[0] + E->sh_cap[1] + E->sh_cap[2]);
+}
+static uint32_t *sh_col(rs_engine *E, int q) {
+  const uint64_t W = E->comm->world;
+  uint64_t off = 0;
+  for (int p = 0; p < q; ++p) off += 4 * W * E->sh_cap[p];
+  return (uint32_t *)((uint8_t *)E->sh_ent + off);
+}
+static uint64_t *sh_val(rs_engine *E, int q) {
+  const uint64_t W = E->comm->world;
+  uint64_t off = 4 * W * (E->sh_cap[0] + E->sh_cap[1] + E->sh_cap[2]);
+  for (int p = 0; p < q; ++p) off += 32 * W * E->sh_cap[p];
+  return (uint64_t *)((uint8_t *)E->sh_ent + off);
+}
+
 // The compact CSR of the result on the device (out.{a,b,c}.{ptr,col,val}): built by every run that
 // does not stream, and on demand (rs_engine_fetch, the .r1cs writer) after one that does.
 static void ensure_csr(rs_engine *E) {
@@ -1841,14 +1980,17 @@ static void ensure_csr(rs_engine *E) {
   if (A.gen != E->fin_gen) throw RsError(RS_E_INTERNAL, "result views are stale: a buffer moved after the run");
   hipStream_t st = E->st;
   const char *nm[3] = {"out.a", "out.b", "out.c"};
-  const uint64_t n_keep = E->fin_keep, n_lv = E->fin_lvn, n_out = n_keep + n_lv;
+  const uint64_t n_keep = E->fin_keep, n_out = E->out_n_dev;
   for (int q = 0; q < 3; ++q) {
     const uint64_t tot = E->out_nnz[q];
     const uint64_t *ptr = A.get<uint64_t>(std::string(nm[q]) + ".ptr", n_out + 1);
     uint32_t *col = A.get<uint32_t>(std::string(nm[q]) + ".col", tot);
     uint64_t *val = A.get<uint64_t>(std::string(nm[q]) + ".val", 4 * tot);
     if (n_keep) launch(st, k_gather_rows, n_keep, E->F, E->fin_parts[q], E->fin_keep_ids, n_keep, ptr, col, val);
-    if (n_lv) launch(st, k_gather_rows, n_lv, E->F, E->fin_lvq[q], E->fin_lv_ids, n_lv, ptr + n_keep, col, val);
+    for (int x = 0; x < 2; ++x) {
+      const uint64_t o = n_keep + (x ? E->fin_xn[0] : 0);
+      if (E->fin_xn[x]) launch(st, k_gather_rows, E->fin_xn[x], E->F, E->fin_xq[x][q], E->fin_x_ids[x], E->fin_xn[x], ptr + o, col, val);
+    }
   }
   E->csr_ready = true;
 }
@@ -1881,7 +2023,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   int32_t *sub_of = A.get<int32_t>("sub_of", S);
   HC(hipMemsetAsync(sub_of, 0xff, 4 * S, st));
 
-  std::vector<HostCon> lconst;
+  LcHeap lc;  // lconst (device)
   snap_join(E);
   E->snap_on = false;
   E->csr_ready = false;
@@ -1947,10 +2089,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     uint32_t nbf = 0;
     HC(hipMemcpyAsync(&nbf, bfn, 4, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
-    struct EqCon {
+    struct EqCon {  // a row of C: keys ascending, canonical values
       int64_t order;
       uint32_t f;
-      HostCon c;
+      std::vector<uint32_t> k;
+      std::vector<uint64_t> v;
     };
     std::vector<EqCon> eqc;
     // per forbidden signal: in an eq cluster?  cluster size, min forbidden, max row (one gather)
@@ -1975,14 +2118,14 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint64_t one[4] = {1, 0, 0, 0}, m1[4];
       memcpy(m1, E->prime, 32);
       m1[0] -= 1;
-      e.c.k[2] = {0};
-      e.c.v[2] = {0, 0, 0, 0};
+      e.k = {0};
+      e.v = {0, 0, 0, 0};
       if (mf < f) {
-        e.c.k[2].push_back(mf); e.c.v[2].insert(e.c.v[2].end(), one, one + 4);
-        e.c.k[2].push_back(f); e.c.v[2].insert(e.c.v[2].end(), m1, m1 + 4);
+        e.k.push_back(mf); e.v.insert(e.v.end(), one, one + 4);
+        e.k.push_back(f); e.v.insert(e.v.end(), m1, m1 + 4);
       } else {
-        e.c.k[2].push_back(f); e.c.v[2].insert(e.c.v[2].end(), m1, m1 + 4);
-        e.c.k[2].push_back(mf); e.c.v[2].insert(e.c.v[2].end(), one, one + 4);
+        e.k.push_back(f); e.v.insert(e.v.end(), m1, m1 + 4);
+        e.k.push_back(mf); e.v.insert(e.v.end(), one, one + 4);
       }
       eqc.push_back(std::move(e));
     }
@@ -2015,15 +2158,38 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         EqCon e;
         e.order = (int64_t)x[0];
         e.f = 0;
-        e.c.k[2] = {(uint32_t)x[1], (uint32_t)(x[1] >> 32)};
-        e.c.v[2].assign(x + 3, x + 11);
+        e.k = {(uint32_t)x[1], (uint32_t)(x[1] >> 32)};
+        e.v.assign(x + 3, x + 11);
         eqc.push_back(std::move(e));
       }
     }
     std::sort(eqc.begin(), eqc.end(), [](const EqCon &x, const EqCon &y) {
       return x.order != y.order ? x.order < y.order : x.f < y.f;
     });
-    for (auto &e : eqc) lconst.push_back(std::move(e.c));
+    if (!eqc.empty()) {  // to the device (canonical -> Montgomery), then into the lconst heap
+      const uint64_t ne = eqc.size();
+      std::vector<uint64_t> ho(ne);
+      std::vector<uint32_t> hl(ne), hk;
+      std::vector<uint64_t> hv;
+      for (uint64_t i = 0; i < ne; ++i) {
+        ho[i] = hk.size();
+        hl[i] = (uint32_t)eqc[i].k.size();
+        hk.insert(hk.end(), eqc[i].k.begin(), eqc[i].k.end());
+        hv.insert(hv.end(), eqc[i].v.begin(), eqc[i].v.end());
+      }
+      DRows src{};
+      src.n = ne;
+      src.off = A.get<uint64_t>("lc.eo", ne);
+      src.len = A.get<uint32_t>("lc.el", ne);
+      src.key = A.get<uint32_t>("lc.ek", hk.size());
+      src.val = A.get<Fe>("lc.ev", hk.size());
+      h2d(E, src.off, ho.data(), 8 * ne);
+      h2d(E, src.len, hl.data(), 4 * ne);
+      h2d(E, src.key, hk.data(), 4 * hk.size());
+      h2d(E, src.val, hv.data(), 8 * hv.size());
+      launch(st, k_to_mont, hk.size(), E->F, (const Fe *)src.val, src.val, (uint64_t)hk.size());
+      lc.append(E, src, nullptr, ne);
+    }
   }
 
   // working copies (Montgomery): cons_eq (C), linear (C, one spare slot per row)
@@ -2072,26 +2238,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     uint32_t ncons = 0;
     HC(hipMemcpyAsync(&ncons, cn, 4, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
-    if (ncons) {
-      std::vector<uint32_t> ids(ncons);
-      HC(hipMemcpyAsync(ids.data(), cl, 4 * ncons, hipMemcpyDeviceToHost, st));
-      HC(hipStreamSynchronize(st));
-      std::sort(ids.begin(), ids.end());
-      std::vector<uint64_t> off(ncons), hoff(ce.n);
-      std::vector<uint32_t> len(ncons), hlen(ce.n);
-      HC(hipMemcpyAsync(hoff.data(), ce.off, 8 * ce.n, hipMemcpyDeviceToHost, st));
-      HC(hipMemcpyAsync(hlen.data(), ce.len, 4 * ce.n, hipMemcpyDeviceToHost, st));
-      HC(hipStreamSynchronize(st));
-      for (uint32_t i = 0; i < ncons; ++i) { off[i] = hoff[ids[i]]; len[i] = hlen[ids[i]]; }
-      std::vector<uint32_t> keys;
-      std::vector<uint64_t> vals, optr;
-      fetch_pool_maps(E, off, len, ce.key, ce.val, keys, vals, optr);
-      for (uint32_t i = 0; i < ncons; ++i) {
-        HostCon c;
-        c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
-        c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
-        lconst.push_back(std::move(c));
-      }
+    if (ncons) {  // the kept rows in row order (k_const_pick listed them in any order)
+      uint32_t *sorted = A.get<uint32_t>("ce.cons_sorted", ncons);
+      sort_keys(E, (const uint32_t *)cl, sorted, ncons, 32, "ce");
+      lc.append(E, ce, sorted, ncons);
     }
   }
   // the linear rows: keys first when their values are still on the way (staged load, sorted rows,
@@ -2250,9 +2400,17 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     so_early = A.get<uint8_t>("so.early", n_nl);
     so_eoff = A.get<U3>("so.eoff", n_nl);
     U3 *elen = A.get<U3>("so.elen", n_nl);
-    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, so_early, elen);
+    Comm *CM = E->comm.get();
+    const bool shard = CM && CM->world > 1;
+    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, shard ? E->nl_lo : (uint64_t)0, shard ? E->nl_hi : n_nl, so_early, elen);
     const U3 et = excl_scan_u3(E, elen, so_eoff, n_nl, "so");
     const uint64_t ev[3] = {et.a, et.b, et.c};
+    E->sh_full = false;
+    if (shard) {  // every rank's share of each part gets the same capacity in the shared region
+      for (int q = 0; q < 3; ++q) E->sh_cap[q] = CM->max_u64(std::max<uint64_t>(ev[q] + ev[q] / 4 + 65536, E->sh_cap[q]), st);
+      E->sh_ent = CM->shared_host(0, sh_ent_bytes(E), st);
+      if (!E->sh_ent) throw RsError(RS_E_RCCL, "no shared host memory for the sharded result");
+    }
     // the gather reads copies of the row views: the second pass and later rounds re-point rows
     const DRows *src[3] = {&sa, &sb, &sc};
     const char *nm[3] = {"so.a", "so.b", "so.c"};
@@ -2274,7 +2432,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint32_t *col = A.get<uint32_t>(xn + ".xcol", cap);
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
       if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val);
-      void *hc = pin_get(E, 3 + q, 4 * cap), *hv = pin_get(E, 6 + q, 32 * cap);
+      void *hc = shard ? (void *)(sh_col(E, q) + CM->rank * E->sh_cap[q]) : pin_get(E, 3 + q, 4 * cap);
+      void *hv = shard ? (void *)(sh_val(E, q) + 4 * CM->rank * E->sh_cap[q]) : pin_get(E, 6 + q, 32 * cap);
       if (ev[q]) {  // a part's copies start once its own gather is done
         HC(hipEventRecord(E->ev_snapq[q], E->stc));
         E->snap_jobs.push_back({hc, col, 4 * ev[q], q});
@@ -2406,29 +2565,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
           launch(st, k_mark_relevant, R->n, *R, (const int32_t *)eq_rep, (const uint8_t *)ce_has, relevant);
       }
     }
+    if (E->comm && E->comm->world > 1) load_order_collectives(E);
     run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted,
                               n_nl && !E->comm ? &overlap : nullptr, keys_first ? &linear_values : nullptr, relevant);
     if (E->log_on) log_linear_round(E, eo, P);
-    collect_leftovers(E, eo, P, lconst);
+    collect_leftovers(E, eo, P, lc);
     E->stats.rounds++;
   } else {
-    // --O1: the linear rows join lconst unchanged (:575-577)
-    HostRows H;
-    fetch_keys(E, lin, H);
-    std::vector<uint64_t> hoff(lin.n);
-    if (lin.n) {
-      HC(hipMemcpyAsync(hoff.data(), lin.off, 8 * lin.n, hipMemcpyDeviceToHost, st));
-      HC(hipStreamSynchronize(st));
-    }
-    std::vector<uint32_t> keys;
-    std::vector<uint64_t> vals, optr;
-    fetch_pool_maps(E, hoff, H.len, lin.key, lin.val, keys, vals, optr);
-    for (uint64_t i = 0; i < lin.n; ++i) {
-      HostCon c;
-      c.k[2].assign(keys.begin() + optr[i], keys.begin() + optr[i + 1]);
-      c.v[2].assign(vals.begin() + 4 * optr[i], vals.begin() + 4 * optr[i + 1]);
-      lconst.push_back(std::move(c));
-    }
+    // --O1: the linear rows join lconst as they are after the eq / constant frames (:575-577)
+    if (!keys_first) lc.append(E, lin, nullptr, lin.n);
+    else throw RsError(RS_E_INTERNAL, "--O1 with keys-first linear rows");
   }
 
   // ======================= obtain_and_simplify_non_linear (non_linear_utils.rs:6-31)
@@ -2587,7 +2733,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       Marks MK;
       MK.st = st;
       MK.mark("start");
-      collect_leftovers(E, er, P, lconst);
+      collect_leftovers(E, er, P, lc);
       MK.mark("leftovers");
       double Tr = now_ms();
       // ordered substitutions of the round: cluster order, ascending `from` -- one sort of the
@@ -2907,20 +3053,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   }
   // ======================= final assembly (:648-729)
   double Tf = now_ms();
-  // leftover linear rows (rounds exhausted): appended after the storage rows
+  // leftover linear rows (rounds exhausted) and lconst: appended after the storage rows; their
+  // signals join the non-linear map (:648-686)
+  const DRows lcv = lc.view(A);
   if (lv.n) launch(st, k_mark_keys, lv.n, lv, nlmap);
-  for (auto &c : lconst) host_fix(c);
-  {
-    std::vector<uint32_t> lk;
-    for (auto &c : lconst)
-      for (int q = 0; q < 3; ++q)
-        for (uint32_t k : c.k[q]) lk.push_back(k);
-    if (!lk.empty()) {
-      uint32_t *d_x = A.get<uint32_t>("fin.lk", lk.size());
-      h2d(E, d_x, lk.data(), 4 * lk.size());
-      launch(st, k_mark_list, lk.size(), (const uint32_t *)d_x, (uint64_t)lk.size(), nlmap);
-    }
-  }
+  if (lcv.n) launch(st, k_mark_keys, lcv.n, lcv, nlmap);
   HC(hipMemsetAsync(nlmap, 0, 1, st));  // the constant key is not a signal
   uint32_t *kept = A.get<uint32_t>("fin.kept", S);
   uint64_t *kept64 = A.get<uint64_t>("fin.kept64", S);
@@ -2942,7 +3079,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
     E->npiw = E->n_priv_in - del_in;
   }
-  // output rows: storage (non-empty) ++ leftover linear ++ lconst (host)
+  // output rows: storage (non-empty) ++ leftover linear ++ lconst, empty rows dropped
+  // (extract_with(is_empty), :697); the last two are C-only ("extras")
   {
     uint64_t *nef = A.get<uint64_t>("fin.nef", n_st), *nep = A.get<uint64_t>("fin.nep", n_st);
     uint64_t n_keep = 0;
@@ -2952,52 +3090,93 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
     uint32_t *keep_ids = A.get<uint32_t>("fin.keep", n_keep);
     if (n_keep) launch(st, k_scatter_ids, n_st, (const uint64_t *)nef, (const uint64_t *)nep, n_st, keep_ids);
-    // leftover linear rows keep their list order; empty ones are dropped (extract_with(is_empty))
-    uint64_t n_lv = 0;
-    uint32_t *lv_ids = A.get<uint32_t>("fin.lvids", lv.n);
-    uint32_t *zero_len = A.get<uint32_t>("fin.zlen", lv.n);
-    if (lv.n) {
-      HC(hipMemsetAsync(zero_len, 0, 4 * lv.n, st));
-      uint64_t *lf = A.get<uint64_t>("fin.lvf", lv.n), *lp = A.get<uint64_t>("fin.lvp", lv.n);
-      launch(st, k_nonempty_flags, lv.n, (const uint32_t *)zero_len, (const uint32_t *)zero_len, (const uint32_t *)lv.len, lv.n, lf);
-      n_lv = excl_scan_u64(E, lf, lp, lv.n, "lvf");
-      launch(st, k_scatter_ids, lv.n, (const uint64_t *)lf, (const uint64_t *)lp, lv.n, lv_ids);
+    const DRows xsrc[2] = {lv, lcv};
+    const uint64_t zn = std::max<uint64_t>(lv.n, lcv.n);
+    uint32_t *zero_len = A.get<uint32_t>("fin.zlen", zn);
+    if (zn) HC(hipMemsetAsync(zero_len, 0, 4 * zn, st));
+    uint32_t *x_ids[2];
+    uint64_t n_x[2] = {0, 0}, x_at[2];
+    for (int x = 0; x < 2; ++x) {
+      const DRows &V = xsrc[x];
+      x_ids[x] = A.get<uint32_t>(x ? "fin.lcids" : "fin.lvids", V.n);
+      if (!V.n) continue;
+      uint64_t *lf = A.get<uint64_t>("fin.xf", V.n), *lp = A.get<uint64_t>("fin.xp", V.n);
+      launch(st, k_nonempty_flags, V.n, (const uint32_t *)zero_len, (const uint32_t *)zero_len, (const uint32_t *)V.len, V.n, lf);
+      n_x[x] = excl_scan_u64(E, lf, lp, V.n, "xf");
+      launch(st, k_scatter_ids, V.n, (const uint64_t *)lf, (const uint64_t *)lp, V.n, x_ids[x]);
     }
-    uint64_t n_out = n_keep + n_lv;
+    x_at[0] = n_keep;
+    x_at[1] = n_keep + n_x[0];
+    const uint64_t n_out = n_keep + n_x[0] + n_x[1];
     E->out_n_dev = n_out;
     const DRows *parts[3] = {&ta_, &tb_, &tc_};
     const char *nm[3] = {"out.a", "out.b", "out.c"};
-    DRows empty_lv = lv;
+    // the streamed layout covers this engine's rows: all of them, or sharded its share -- the kept
+    // storage rows of its non-linear rows (a run [k_lo, k_hi) of the keep list), the last rank also
+    // the two C-only tails
+    Comm *CMf = E->comm.get();
+    const bool shard = E->snap_on && CMf && CMf->world > 1;
+    uint64_t k_lo = 0, k_hi = n_keep;
+    bool with_x = true;
+    if (shard) {
+      uint64_t kr[2] = {0, 0};
+      if (n_keep) {
+        uint64_t *d_kr = A.get<uint64_t>("fin.krange", 2);
+        launch(st, k_keep_range, 2, (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids, E->nl_lo, E->nl_hi, d_kr);
+        HC(hipMemcpyAsync(kr, d_kr, 16, hipMemcpyDeviceToHost, st));
+        HC(hipStreamSynchronize(st));
+      }
+      k_lo = kr[0];
+      k_hi = std::max(kr[0], kr[1]);
+      with_x = CMf->rank == CMf->world - 1;
+    }
+    E->sh_klo = k_lo;
+    E->sh_khi = k_hi;
+    const uint64_t own = k_hi - k_lo;
+    const uint32_t *own_ids = keep_ids + k_lo;
+    const uint64_t xl_at[2] = {own, own + (with_x ? n_x[0] : 0)};
+    const uint64_t xl_n[2] = {with_x ? n_x[0] : 0, with_x ? n_x[1] : 0};
+    const uint64_t m_loc = own + xl_n[0] + xl_n[1];
     for (int q = 0; q < 3; ++q) {
       uint64_t *lens = A.get<uint64_t>(std::string(nm[q]) + ".lens", n_out + 1);
       uint64_t *ptr = A.get<uint64_t>(std::string(nm[q]) + ".ptr", n_out + 1);
       if (n_keep) launch(st, k_row_lens, n_keep, *parts[q], (const uint32_t *)keep_ids, n_keep, lens);
-      DRows lvq = empty_lv;
-      if (q < 2) lvq.len = zero_len;
-      if (n_lv) launch(st, k_row_lens, n_lv, lvq, (const uint32_t *)lv_ids, n_lv, lens + n_keep);
+      DRows xq[2];
+      for (int x = 0; x < 2; ++x) {
+        xq[x] = xsrc[x];
+        if (q < 2) xq[x].len = zero_len;
+        if (n_x[x]) launch(st, k_row_lens, n_x[x], xq[x], (const uint32_t *)x_ids[x], n_x[x], lens + x_at[x]);
+        E->fin_xq[x][q] = xq[x];
+      }
       HC(hipMemsetAsync(lens + n_out, 0, 8, st));
       uint64_t tot = excl_scan_u64(E, lens, ptr, n_out + 1, nm[q]);
       E->out_nnz[q] = tot;
       E->fin_parts[q] = *parts[q];
-      E->fin_lvq[q] = lvq;
       if (!E->snap_on) continue;
       // streamed layout: the rows not reused from the early region, after it
-      uint64_t *late = A.get<uint64_t>(std::string(nm[q]) + ".late", n_out + 1);
-      uint64_t *lptr = A.get<uint64_t>(std::string(nm[q]) + ".lptr", n_out + 1);
-      if (n_keep) launch(st, k_out_late_lens, n_keep, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids,
-                         (const uint8_t *)so_early, (const uint8_t *)so_dirty, late);
-      if (n_lv) launch(st, k_row_lens, n_lv, lvq, (const uint32_t *)lv_ids, n_lv, late + n_keep);
-      HC(hipMemsetAsync(late + n_out, 0, 8, st));
-      const uint64_t L = excl_scan_u64(E, late, lptr, n_out + 1, "late");
+      uint64_t *late = A.get<uint64_t>(std::string(nm[q]) + ".late", m_loc + 1);
+      uint64_t *lptr = A.get<uint64_t>(std::string(nm[q]) + ".lptr", m_loc + 1);
+      if (own) launch(st, k_out_late_lens, own, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
+                      (const uint8_t *)so_dirty, late);
+      for (int x = 0; x < 2; ++x)
+        if (xl_n[x]) launch(st, k_row_lens, xl_n[x], xq[x], (const uint32_t *)x_ids[x], xl_n[x], late + xl_at[x]);
+      HC(hipMemsetAsync(late + m_loc, 0, 8, st));
+      const uint64_t L = excl_scan_u64(E, late, lptr, m_loc + 1, "late");
       const uint64_t base = E->snap_e[q], ext = base + L;
       E->out_ext[q] = ext;
-      uint64_t *beg = A.get<uint64_t>(std::string(nm[q]) + ".beg", n_out + 1);
-      uint64_t *end = A.get<uint64_t>(std::string(nm[q]) + ".end", n_out + 1);
-      if (n_keep) launch(st, k_out_extent, n_keep, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids,
-                         (const uint8_t *)so_early, (const uint8_t *)so_dirty, (const U3 *)so_eoff, q, base, (const uint64_t *)lptr, beg, end);
-      if (n_lv) launch(st, k_out_extent, n_lv, lvq, (const uint32_t *)lv_ids, n_lv, (const uint32_t *)nullptr, (const uint8_t *)nullptr,
-                       (const uint8_t *)nullptr, (const U3 *)nullptr, q, base, (const uint64_t *)(lptr + n_keep), beg + n_keep, end + n_keep);
-      launch(st, k_set_u64, 1, beg + n_out, ext);
+      uint64_t *beg = A.get<uint64_t>(std::string(nm[q]) + ".beg", m_loc + 1);
+      uint64_t *end = A.get<uint64_t>(std::string(nm[q]) + ".end", m_loc + 1);
+      if (shard) {  // fetch_result_shared's rebased copies (allocated here: nothing may move after the run)
+        (void)A.get<uint64_t>(std::string(nm[q]) + ".begx", m_loc);
+        (void)A.get<uint64_t>(std::string(nm[q]) + ".endx", m_loc);
+      }
+      if (own) launch(st, k_out_extent, own, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
+                      (const uint8_t *)so_dirty, (const U3 *)so_eoff, q, base, (const uint64_t *)lptr, beg, end);
+      for (int x = 0; x < 2; ++x)
+        if (xl_n[x])
+          launch(st, k_out_extent, xl_n[x], xq[x], (const uint32_t *)x_ids[x], xl_n[x], (const uint32_t *)nullptr, (const uint8_t *)nullptr,
+                 (const uint8_t *)nullptr, (const U3 *)nullptr, q, base, (const uint64_t *)(lptr + xl_at[x]), beg + xl_at[x], end + xl_at[x]);
+      launch(st, k_set_u64, 1, beg + m_loc, ext);
       // the device copy of the whole layout grows past the early region when it must (the
       // early region is copied along once its gather is done)
       const std::string xc = std::string(nm[q]) + ".xcol", xv = std::string(nm[q]) + ".xval";
@@ -3006,18 +3185,32 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       A.grow_keep<uint64_t>(xv, 4 * ext, 4 * base, E->stc, st);
       uint32_t *col = A.get<uint32_t>(xc, ext);
       uint64_t *val = A.get<uint64_t>(xv, 4 * ext);
-      if (n_keep) launch(st, k_gather_late, n_keep, E->F, *parts[q], (const uint32_t *)keep_ids, n_keep, (const uint32_t *)st_ids,
-                         (const uint8_t *)so_early, (const uint8_t *)so_dirty, (const uint64_t *)lptr, col + base, val + 4 * base);
-      if (n_lv) launch(st, k_gather_late, n_lv, E->F, lvq, (const uint32_t *)lv_ids, n_lv, (const uint32_t *)nullptr,
-                       (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + n_keep), col + base, val + 4 * base);
+      if (own) launch(st, k_gather_late, own, E->F, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
+                      (const uint8_t *)so_dirty, (const uint64_t *)lptr, col + base, val + 4 * base);
+      for (int x = 0; x < 2; ++x)
+        if (xl_n[x])
+          launch(st, k_gather_late, xl_n[x], E->F, xq[x], (const uint32_t *)x_ids[x], xl_n[x], (const uint32_t *)nullptr,
+                 (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + xl_at[x]), col + base, val + 4 * base);
+    }
+    if (shard) {  // a share past its capacity: the region regrows and every rank copies its whole layout
+      uint64_t over = 0;
+      for (int q = 0; q < 3; ++q) over |= E->out_ext[q] > E->sh_cap[q];
+      if (CMf->max_u64(over, st)) {
+        snap_join(E);  // the early copies into the old region are done (they are redone below)
+        for (int q = 0; q < 3; ++q) E->sh_cap[q] = CMf->max_u64(E->out_ext[q] + E->out_ext[q] / 4 + 65536, st);
+        E->sh_ent = CMf->shared_host(0, sh_ent_bytes(E), st);
+        if (!E->sh_ent) throw RsError(RS_E_RCCL, "no shared host memory for the sharded result");
+        E->sh_full = true;
+      }
     }
     E->fin_keep = n_keep;
-    E->fin_lvn = n_lv;
-    E->fin_gen = A.gen;
     E->fin_keep_ids = keep_ids;
-    E->fin_lv_ids = lv_ids;
+    for (int x = 0; x < 2; ++x) {
+      E->fin_xn[x] = n_x[x];
+      E->fin_x_ids[x] = x_ids[x];
+    }
+    E->fin_gen = A.gen;
     if (!E->snap_on) ensure_csr(E);
-    E->out_host_tail = std::move(lconst);
   }
   load_wait_all(E);  // a group the path never needed (e.g. no non-linear rows) is still checked
   int err = 0, fw_err = 0;
@@ -3032,12 +3225,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   {  // B_alg: the in-kernel counters + input / output entries and rows + the label map
     const uint64_t z_in = E->ce.nnz + E->eq.nnz + E->lin.nnz + E->na.nnz + E->nb.nnz + E->nc.nnz;
     const uint64_t r_in = E->ce.n + E->eq.n + E->lin.n + E->na.n;
-    uint64_t z_out = E->out_nnz[0] + E->out_nnz[1] + E->out_nnz[2], r_out = E->out_n_dev;
-    for (auto &c : E->out_host_tail) {
-      const uint64_t m = c.k[0].size() + c.k[1].size() + c.k[2].size();
-      z_out += m;
-      r_out += m ? 1 : 0;
-    }
+    const uint64_t z_out = E->out_nnz[0] + E->out_nnz[1] + E->out_nnz[2], r_out = E->out_n_dev;
     const rs_stats &s = E->stats;
     E->stats.alg_bytes = s.elim_bytes + s.big_main_bytes + s.big_finish_bytes + s.apply_bytes + s.round_fill_bytes +
                          36 * (z_in + z_out) + 8 * (r_in + r_out) + 8 * S;
@@ -3196,8 +3384,8 @@ int rs_engine_stats(rs_engine *E, rs_stats *s) {
 namespace rs {
 // The result in host memory.  buf(slot, bytes) supplies the destination of each array -- slots
 // 0-2 ptr of a/b/c, 3-5 col, 6-8 val, 9 label_to_wire -- (malloc for rs_engine_fetch, the engine's
-// pinned buffers for rs_engine_simplify).  Every D2H is enqueued first and waited for once; the
-// host-side lconst rows are then appended after the device rows.  The substitution log is copied
+// pinned buffers for rs_engine_simplify).  Every D2H is enqueued first and waited for once.  The
+// substitution log is copied
 // (own = true) or pointed at (the engine's vectors, rs_engine_simplify's view).
 // grows pinned slot `slot` keeping its first `keep` bytes (the early region, once its D2H is done)
 static void *pin_grow_keep(rs_engine *E, int slot, size_t bytes, size_t keep) {
@@ -3219,46 +3407,36 @@ static void *pin_grow_keep(rs_engine *E, int slot, size_t bytes, size_t keep) {
 // row gets [beg, end) (rs_output.{a,b,c}_end).  Otherwise the compact CSR.
 static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(int, size_t)> &buf, bool own_log, bool streamed) {
   const uint64_t nd = E->out_n_dev;
-  // non-empty host rows (lconst after fix may be empty: extract_with removes them)
-  std::vector<const HostCon *> hrows;
-  for (auto &c : E->out_host_tail)
-    if (!(c.k[0].empty() && c.k[1].empty() && c.k[2].empty())) hrows.push_back(&c);
-  const uint64_t nh = hrows.size();
-  o->n_constraints = nd + nh;
+  o->n_constraints = nd;
   const char *nm[3] = {"out.a", "out.b", "out.c"};
   rs_lc *dst[3] = {&o->a, &o->b, &o->c};
   uint64_t **ends[3] = {&o->a_end, &o->b_end, &o->c_end};
-  uint64_t base[3];  // where the host rows start in col / val
   if (!streamed) ensure_csr(E);
   for (int q = 0; q < 3; ++q) {
-    uint64_t hn = 0;
-    for (auto *c : hrows) hn += c->k[q].size();
     rs_lc &L = *dst[q];
     const std::string n(nm[q]);
+    L.n_rows = nd;
     if (!streamed) {
-      const uint64_t tot = E->out_nnz[q] + hn;
-      L.n_rows = nd + nh;
+      const uint64_t tot = E->out_nnz[q];
       L.nnz = tot;
-      L.ptr = (uint64_t *)buf(q, 8 * (nd + nh + 1));
+      L.ptr = (uint64_t *)buf(q, 8 * (nd + 1));
       L.col = (uint32_t *)buf(3 + q, 4 * (tot ? tot : 1));
       L.val = (uint64_t *)buf(6 + q, 32 * (tot ? tot : 1));
       *ends[q] = nullptr;
       if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(n + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
       else L.ptr[0] = 0;
-      if (E->out_nnz[q]) {
-        HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(n + ".col", 1), 4 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
-        HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(n + ".val", 1), 32 * E->out_nnz[q], hipMemcpyDeviceToHost, E->st));
+      if (tot) {
+        HC(hipMemcpyAsync(L.col, E->A.get<uint32_t>(n + ".col", 1), 4 * tot, hipMemcpyDeviceToHost, E->st));
+        HC(hipMemcpyAsync(L.val, E->A.get<uint64_t>(n + ".val", 1), 32 * tot, hipMemcpyDeviceToHost, E->st));
       }
-      base[q] = E->out_nnz[q];
       continue;
     }
-    const uint64_t early = E->snap_e[q], ext = E->out_ext[q], tot = ext + hn;
-    L.n_rows = nd + nh;
-    L.nnz = tot;
-    L.ptr = (uint64_t *)pin_get(E, q, 8 * (nd + nh + 1));
-    *ends[q] = (uint64_t *)pin_get(E, 13 + q, 8 * (nd + nh + 1));
-    L.col = (uint32_t *)pin_grow_keep(E, 3 + q, 4 * (tot ? tot : 1), 4 * early);
-    L.val = (uint64_t *)pin_grow_keep(E, 6 + q, 32 * (tot ? tot : 1), 32 * early);
+    const uint64_t early = E->snap_e[q], ext = E->out_ext[q];
+    L.nnz = ext;
+    L.ptr = (uint64_t *)pin_get(E, q, 8 * (nd + 1));
+    *ends[q] = (uint64_t *)pin_get(E, 13 + q, 8 * (nd + 1));
+    L.col = (uint32_t *)pin_grow_keep(E, 3 + q, 4 * (ext ? ext : 1), 4 * early);
+    L.val = (uint64_t *)pin_grow_keep(E, 6 + q, 32 * (ext ? ext : 1), 32 * early);
     if (nd) {
       HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(n + ".beg", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
       HC(hipMemcpyAsync(*ends[q], E->A.get<uint64_t>(n + ".end", 1), 8 * nd, hipMemcpyDeviceToHost, E->st));
@@ -3270,7 +3448,6 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
       HC(hipMemcpyAsync(L.val + 4 * early, E->A.get<uint64_t>(n + ".xval", 1) + 4 * early, 32 * (ext - early),
                         hipMemcpyDeviceToHost, E->st));
     }
-    base[q] = ext;
   }
   o->n_labels = E->S;
   o->label_to_wire = (int32_t *)buf(9, 4 * E->S);
@@ -3279,25 +3456,6 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
   if (streamed) {
     snap_join(E);
     if (E->snap_rc) throw RsError(RS_E_HIP, "D2H of the streamed rows failed");
-  }
-  for (int q = 0; q < 3; ++q) {
-    rs_lc &L = *dst[q];
-    uint64_t e = base[q];
-    uint64_t *end = *ends[q];
-    for (uint64_t i = 0; i < nh; ++i) {
-      const HostCon &c = *hrows[i];
-      const size_t m = c.k[q].size();
-      if (m) {
-        memcpy(L.col + e, c.k[q].data(), 4 * m);
-        memcpy(L.val + 4 * e, c.v[q].data(), 32 * m);
-      }
-      if (end) {
-        L.ptr[nd + i] = e;
-        end[nd + i] = e + m;
-      }
-      e += m;
-      L.ptr[nd + i + 1] = e;
-    }
   }
   o->n_wires = E->n_wires;
   o->no_private_inputs_witness = E->npiw;
@@ -3326,6 +3484,85 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
       o->log_to.col = E->log_key.data();
       o->log_to.val = E->log_val.data();
     }
+  }
+}
+
+// The sharded host -> host result: every rank copies its share (its rows' extents at their global
+// row numbers, its late entries after its early ones, its slice of label_to_wire) into the shared
+// host regions; after a barrier each rank's *o describes the whole result there (the view is the
+// same on every rank).  Row extents of part q are rank-based: rank r's entries start at r * sh_cap[q].
+static void fetch_result_shared(rs_engine *E, rs_output *o, bool own_log) {
+  Comm &CM = *E->comm;
+  Arena &A = E->A;
+  hipStream_t st = E->st;
+  const uint64_t W = CM.world, r = CM.rank, nd = E->out_n_dev, S = E->S;
+  const uint64_t k_lo = E->sh_klo, own = E->sh_khi - E->sh_klo, n_keep = E->fin_keep;
+  const bool with_x = r == W - 1;
+  const uint64_t m_loc = own + (with_x ? nd - n_keep : 0);
+  // rows region: ptr, end of a, b, c, then label_to_wire
+  const uint64_t rows_bytes = 3 * 8 * (2 * nd + 1) + 4 * S;
+  uint8_t *rb = (uint8_t *)CM.shared_host(1, rows_bytes, st);
+  if (!rb) throw RsError(RS_E_RCCL, "no shared host memory for the sharded result");
+  const char *nm[3] = {"out.a", "out.b", "out.c"};
+  rs_lc *dst[3] = {&o->a, &o->b, &o->c};
+  uint64_t **ends[3] = {&o->a_end, &o->b_end, &o->c_end};
+  o->n_constraints = nd;
+  for (int q = 0; q < 3; ++q) {
+    uint64_t *ptr = (uint64_t *)(rb + 8 * (2 * nd + 1) * q), *end = ptr + nd + 1;
+    const std::string n(nm[q]);
+    const uint64_t rbase = r * E->sh_cap[q], early = E->snap_e[q], ext = E->out_ext[q];
+    if (m_loc) {  // this rank's extents, moved to its base, to their global rows
+      uint64_t *bx = A.get<uint64_t>(n + ".begx", 1), *ex = A.get<uint64_t>(n + ".endx", 1);  // sized by the run
+      launch(st, k_add_u64, m_loc, (const uint64_t *)A.get<uint64_t>(n + ".beg", 1), m_loc, rbase, bx);
+      launch(st, k_add_u64, m_loc, (const uint64_t *)A.get<uint64_t>(n + ".end", 1), m_loc, rbase, ex);
+      if (own) {
+        HC(hipMemcpyAsync(ptr + k_lo, bx, 8 * own, hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(end + k_lo, ex, 8 * own, hipMemcpyDeviceToHost, st));
+      }
+      if (m_loc > own) {
+        HC(hipMemcpyAsync(ptr + n_keep, bx + own, 8 * (m_loc - own), hipMemcpyDeviceToHost, st));
+        HC(hipMemcpyAsync(end + n_keep, ex + own, 8 * (m_loc - own), hipMemcpyDeviceToHost, st));
+      }
+    }
+    if (with_x) ptr[nd] = W * E->sh_cap[q];
+    const uint64_t from = E->sh_full ? 0 : early;  // the early entries are on their way (snap thread)
+    if (ext > from) {
+      HC(hipMemcpyAsync(sh_col(E, q) + rbase + from, A.get<uint32_t>(n + ".xcol", 1) + from, 4 * (ext - from), hipMemcpyDeviceToHost, st));
+      HC(hipMemcpyAsync(sh_val(E, q) + 4 * (rbase + from), A.get<uint64_t>(n + ".xval", 1) + 4 * from, 32 * (ext - from),
+                        hipMemcpyDeviceToHost, st));
+    }
+    rs_lc &L = *dst[q];
+    L.n_rows = nd;
+    L.nnz = W * E->sh_cap[q];
+    L.ptr = ptr;
+    L.col = sh_col(E, q);
+    L.val = sh_val(E, q);
+    *ends[q] = end;
+  }
+  int32_t *l2w = (int32_t *)(rb + 3 * 8 * (2 * nd + 1));
+  const uint64_t s0 = S * r / W, s1 = S * (r + 1) / W;
+  if (s1 > s0) HC(hipMemcpyAsync(l2w + s0, A.get<int32_t>("fin.l2w", 1) + s0, 4 * (s1 - s0), hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  snap_join(E);
+  const uint64_t bad = CM.max_u64(E->snap_rc ? 1 : 0, st);  // also the barrier: every share has landed
+  if (bad) throw RsError(RS_E_HIP, "D2H of the streamed rows failed");
+  o->n_labels = S;
+  o->label_to_wire = l2w;
+  o->n_wires = E->n_wires;
+  o->no_private_inputs_witness = E->npiw;
+  o->n_log = 0;
+  o->log_from = nullptr;
+  o->log_to = rs_lc{};
+  if (E->log_on) {
+    const uint64_t n = E->log_from.size(), nnz = E->log_key.size();
+    o->n_log = n;
+    o->log_to.n_rows = n;
+    o->log_to.nnz = nnz;
+    (void)own_log;
+    o->log_from = E->log_from.data();
+    o->log_to.ptr = E->log_ptr.data();
+    o->log_to.col = E->log_key.data();
+    o->log_to.val = E->log_val.data();
   }
 }
 
@@ -3370,7 +3607,8 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
     E->hin = nullptr;
     const double t1 = now_ms();
     E->view = rs_output{};
-    fetch_result(E, &E->view, [E](int slot, size_t bytes) { return pin_get(E, slot, bytes); }, false, E->snap_on);
+    if (E->snap_on && E->comm && E->comm->world > 1) fetch_result_shared(E, &E->view, false);
+    else fetch_result(E, &E->view, [E](int slot, size_t bytes) { return pin_get(E, slot, bytes); }, false, E->snap_on);
     const double t2 = now_ms();
     E->stats.d2h_ms = t2 - t1;
     E->stats.host_total_ms = t2 - t0;
@@ -3391,8 +3629,7 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
 
 // The last result as a .r1cs file (constraint_list/src/r1cs_porting.rs:4-124, the same bytes as
 // rs_write_r1cs on the fetched output): the constraint section is built on the device (writer.hpp)
-// and streamed to the file through two pinned staging buffers; the host-side tail rows (lconst) and
-// the small sections follow.  o0_r1cs (optional): custom-gate sections as rs_write_r1cs_gates.
+// and streamed to the file through two pinned staging buffers; the small sections follow.  o0_r1cs (optional): custom-gate sections as rs_write_r1cs_gates.
 int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
   FILE *f = nullptr;
   try {
@@ -3459,35 +3696,6 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
     HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
     if (err) throw RsError(RS_E_INTERNAL, "constraint mentions a removed signal (apply_raw_correspondence panics)");
-    // the host-side tail rows, serialised like the device records
-    std::vector<uint8_t> tail;
-    uint64_t n_tail = 0;
-    for (const HostCon &c : E->out_host_tail) {
-      if (c.k[0].empty() && c.k[1].empty() && c.k[2].empty()) continue;
-      ++n_tail;
-      for (int q = 0; q < 3; ++q) {
-        std::vector<std::pair<uint64_t, uint32_t>> ord;
-        for (uint32_t i = 0; i < c.k[q].size(); ++i) {
-          const uint32_t k = c.k[q][i];
-          const int32_t w = k == 0 ? 0 : hl2w[k];
-          if (w < 0) throw RsError(RS_E_INTERNAL, "constraint mentions a removed signal (apply_raw_correspondence panics)");
-          uint64_t key = 0;  // the LE-byte-string key (injective in w)
-          const int len = w == 0 ? 1 : (32 - __builtin_clz((uint32_t)w) + 7) / 8;
-          for (int b = 0; b < 4; ++b) key = (key << 9) | (b < len ? ((((uint32_t)w) >> (8 * b)) & 0xffu) + 1 : 0);
-          ord.push_back({key, i});
-        }
-        std::sort(ord.begin(), ord.end());
-        const uint32_t m = (uint32_t)ord.size();
-        tail.insert(tail.end(), (const uint8_t *)&m, (const uint8_t *)&m + 4);
-        for (auto &x : ord) {
-          const uint32_t k = c.k[q][x.second];
-          const uint32_t w = k == 0 ? 0u : (uint32_t)hl2w[k];
-          tail.insert(tail.end(), (const uint8_t *)&w, (const uint8_t *)&w + 4);
-          const uint8_t *v = (const uint8_t *)&c.v[q][4 * x.second];
-          tail.insert(tail.end(), v, v + fs);
-        }
-      }
-    }
     std::vector<uint8_t> gates;
     bool with_gates = false;
     if (o0_r1cs && !r1cs_gate_sections(o0_r1cs, hl2w.data(), S, gates, with_gates)) return RS_E_INVALID;
@@ -3497,7 +3705,7 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
     auto put64 = [&](uint64_t v) { fwrite(&v, 8, 1, f); };
     fwrite(with_gates ? "r1cs\x01\x00\x00\x00\x05\x00\x00\x00" : "r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
     put32(2);
-    put64(dev_bytes + tail.size());
+    put64(dev_bytes);
     // the device image in chunks: D2H of chunk i + 1 overlaps the write of chunk i
     constexpr uint64_t kChunk = 64ull << 20;
     void *pb[2] = {pin_get(E, 11, kChunk), pin_get(E, 12, kChunk)};
@@ -3521,7 +3729,6 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
       done = nx;
       cur ^= 1;
     }
-    if (!tail.empty()) fwrite(tail.data(), 1, tail.size(), f);
     // header (r1cs_writer.rs:246-269)
     put32(1);
     put64(4 + fs + 4 * 4 + 8 + 4);
@@ -3532,7 +3739,7 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
     put32((uint32_t)E->n_pub_in);
     put32((uint32_t)E->n_priv_in);
     put64(S);
-    put32((uint32_t)(n + n_tail));
+    put32((uint32_t)n);
     // wire -> label
     put32(3);
     put64(8 * E->n_wires);

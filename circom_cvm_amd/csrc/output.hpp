@@ -15,10 +15,11 @@ __device__ __forceinline__ uint64_t u3_sel(const U3 &x, int q) { return q == 0 ?
 
 // early[i]: non-linear row i is done (not left to a second pass) and stayed non-linear -- a
 // storage row (non_linear_utils.rs:6-31: A or B non-empty); elen[i]: its part lengths (0
-// when not early)
-__global__ void k_snap_flags(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, uint8_t *early, U3 *elen) {
+// when not early).  Sharded: only the rows [lo, hi) this rank copies to the host count.
+__global__ void k_snap_flags(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, uint64_t lo, uint64_t hi, uint8_t *early,
+                             U3 *elen) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
-    const bool done = !late || !late[i];
+    const bool done = (!late || !late[i]) && i >= lo && i < hi;
     const uint32_t la = done ? a.len[i] : 0, lb = done ? b.len[i] : 0, lc = done ? c.len[i] : 0;
     const bool ok = (la | lb) != 0;  // k_flag_linear: linear iff A and B are both empty
     early[i] = ok ? 1 : 0;
@@ -102,5 +103,22 @@ __global__ void k_to_host(const uint4 *src, uint4 *dst, uint64_t n16) {
 
 __global__ void k_set_u64(uint64_t *p, uint64_t v) {
   if (gtid() == 0) *p = v;
+}
+
+// sharded result: this rank's output rows are the kept storage rows whose non-linear row lies in
+// [lo, hi) -- a contiguous run of the (ascending) keep list: out[0] = its first index, out[1] = its end
+__global__ void k_keep_range(const uint32_t *keep, uint64_t n_keep, const uint32_t *nl_of, uint64_t lo, uint64_t hi, uint64_t *out) {
+  const uint64_t t = gtid();
+  if (t >= 2) return;
+  const uint64_t bound = t ? hi : lo;
+  uint64_t a = 0, b = n_keep;
+  while (a < b) {
+    const uint64_t m = (a + b) / 2;
+    if (nl_of[keep[m]] < bound) a = m + 1; else b = m;
+  }
+  out[t] = a;
+}
+__global__ void k_add_u64(const uint64_t *in, uint64_t n, uint64_t add, uint64_t *out) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = in[i] + add;
 }
 

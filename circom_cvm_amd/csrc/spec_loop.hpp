@@ -239,7 +239,8 @@ __device__ __forceinline__ void sp_stage(const ElimArgs &A, uint32_t lane, uint3
 // merge's products.
 template <int E, int NW>
 __device__ __forceinline__ void sp_reduce(const ElimArgs &A, SpecSmem<NW> &S, uint32_t wv, uint32_t lane, bool p4,
-                                          uint64_t r_off, uint32_t olen, uint32_t okey, uint32_t osl, SpecRow<E> &R) {
+                                          uint64_t r_off, uint32_t olen, uint32_t okey, uint32_t osl, SpecRow<E> &R,
+                                          uint32_t j) {
   const FieldP &F = A.F;
   constexpr uint32_t CAPL = 64 * E;
   R.len = olen;
@@ -265,6 +266,9 @@ __device__ __forceinline__ void sp_reduce(const ElimArgs &A, SpecSmem<NW> &S, ui
   Fe sv[E];
   for (;;) {
     if (lds_ld(&S.s_abort)) return;
+    // a row still reducing when its turn comes is the critical path: its wave wins the SIMD's issue
+    // arbitration from then on (the turn lowers it again)
+    if (rdlane(lds_ld(&S.s_turn), 0) == j) __builtin_amdgcn_s_setprio(2);
     const uint32_t len = R.len;
     uint32_t st[E];
     uint64_t tm[E], dm[E];
@@ -678,7 +682,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
       const uint32_t osl = lane < olen ? sp_find(S.tk, okey) : kTabEmpty;
       // ---- speculate
       uint32_t c0 = rdlane(lds_ld_sc(&S.s_turn), 0);
-      sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R);
+      sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R, j);
       // ---- wait for the turn, validating the commits that land meanwhile; a conflict found
       // before the turn is reduced again right away (against the newer state)
       bool conflict = false, first = true, late = false;
@@ -691,19 +695,22 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
         first = false;
         if (conflict) {
           pc[3] += R.merges;
-          sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R);
+          sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R, j);
           conflict = false;
           continue;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      // ---- the turn: the state is final for this row
+      // ---- the turn: the state is final for this row.  The committing wave is the critical path of
+      // the whole loop: it takes the SIMD's issue arbitration from the speculating wave beside it
+      // (MI355X_MICROARCH.md: VALU issue goes by priority, then age) until it passes the turn on.
+      __builtin_amdgcn_s_setprio(3);
       const unsigned long long t_a = prof ? wall_clock64() : 0ull;
       if (prof && late) { pc[6]++; pc[7] += t_a - __hip_atomic_load(&S.s_tend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
       if (conflict) {
         pc[0]++;
         pc[3] += R.merges;
-        sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R);
+        sp_reduce<1, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R, j);
       }
       if (lds_ld(&S.s_abort)) break;  // a wait ran out of budget: every wave leaves, err bit 64
       const bool ok = lds_ld(&S.s_ok) != 0;
@@ -736,7 +743,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
       bool done = !ok;
       if (!done && R.serial && olen <= 128) {  // two entries per lane, now that nothing else commits
         SpecRow<2> R2;
-        sp_reduce<2, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R2);
+        sp_reduce<2, NW>(A, S, wv, lane, p4, r_off, olen, okey, osl, R2, j);
         if (!R2.serial) {
           pc[2] += R2.merges;
           by += R2.by;
@@ -795,6 +802,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
         lds_st_sc(&S.ring[j % kSpecRing], piv);
         lds_st_sc(&S.s_turn, j + 1);
       }
+      __builtin_amdgcn_s_setprio(0);
       // then this row's global stores complete, and the watermark moves on (in row order: whoever
       // finds the next row's mark set advances it)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -807,6 +815,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
         }
       }
     }
+    __builtin_amdgcn_s_setprio(0);  // an aborted turn may leave the loop at priority 3
     if (lane == 0) {
       atomicAdd(A.bytes_main, by);
       if (prof)

@@ -135,3 +135,84 @@ def test_rccl_world1_join():
     assert rsio.diff_output_arrays(got, ref) is None
     assert e.stats().world == 1
     e.close()
+
+
+# ---------------------------------------------------------------- host -> host, split PCIe legs
+def sharded_simplify(inp, fl, world, engs=None, arrays=True, reps=1):
+    """rs_engine_simplify on every rank at once: each rank uploads its share of the input (the ranks
+    complete the blocks over the group's allgathervs) and copies its share of the result into the
+    group's shared host region; every rank's returned view must be the whole result."""
+    engs = engs or group(world)
+    outs, errs = [None] * world, [None] * world
+
+    def work(r):
+        try:
+            for _ in range(reps):
+                out = engs[r].simplify(inp, fl)
+            outs[r] = (rsio.output_arrays(out) if arrays else rsio.output_to_py(out), engs[r].stats())
+        except Exception as ex:  # noqa: BLE001 -- reported below
+            errs[r] = ex
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=280)
+        assert not t.is_alive(), "sharded simplify hung"
+    for e in errs:
+        if e is not None:
+            raise e
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_hosthost_random_small(world):
+    """Split input / output legs on small random systems (every flag level, two primes): each rank's
+    view equals the single-GPU oracle's result."""
+    for p in (257, R.PRIMES["bn128"]):
+        for seed in range(8):
+            sys_ = rsio.gen_system(300 + seed, p, n_sig=60 + seed % 40, n_rows=90 + seed % 60)
+            h = rsio.InputHolder(sys_)
+            for lvl, rd in (("O1", None), ("O2", None), ("O2", 1)):
+                fl = rsio.flags(lvl, rd)
+                ref, _, _ = rsio.oracle_run(h.inp, fl)
+                for r, (got, st) in enumerate(sharded_simplify(h.inp, fl, world, arrays=False)):
+                    if got != ref:
+                        raise AssertionError(f"rank {r}/{world} {lvl}/{rd}: {rsio.same_result(R.Result(ref[0], ref[1], ref[3]), got)}")
+
+
+@pytest.mark.parametrize("kind,rows,world", [(0, 300_000, 2), (0, 400_000, 4), (2, 60_000, 3), (1, 100_000, 4), (5, 200_000, 2)])
+def test_sharded_hosthost_synth_arrays(kind, rows, world):
+    """Synthetic workloads host -> host over 2-4 ranks, array for array on every rank, three calls on
+    the same engines (the shared region is reused and grows as needed)."""
+    inp = M.Input.synth(kind, rows, 42)
+    fl = rsio.flags("O2")
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=8)
+    for r, (got, st) in enumerate(sharded_simplify(inp.c, fl, world, reps=3)):
+        assert rsio.diff_output_arrays(got, ref) is None, f"rank {r}/{world}"
+        assert st.world == world
+
+
+def test_sharded_hosthost_bls12381_20m_world8():
+    """BASELINE configs[4] at its stated size: --prime bls12381, the 20 M-row mixed circuit, ONE circuit
+    over 8 ranks host -> host (split upload, sharded elimination with the exchange, split result
+    copy), every rank array for array equal to the single-GPU oracle.  In one process on one GPU
+    (8 engines), so the group is made for this test and closed after it."""
+    world = 8
+    inp = M.Input.synth(0, 20_000_000, 42, "bls12381")
+    pin = M.PinnedInput(inp.c)
+    fl = rsio.flags("O2")
+    g = M.Group(world)
+    engs = [M.Engine(0) for _ in range(world)]
+    try:
+        for r, e in enumerate(engs):
+            e.join_group(g, r)
+        outs = sharded_simplify(pin.c, fl, world, engs=engs)
+        ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
+        for r, (got, st) in enumerate(outs):
+            assert rsio.diff_output_arrays(got, ref) is None, f"rank {r}/{world}"
+            assert st.world == world and st.exchange_bytes > 0
+    finally:
+        for e in engs:
+            e.close()
+        pin.free()
