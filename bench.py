@@ -227,6 +227,7 @@ def main():
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the independent-shard extra run")
     ap.add_argument("--no-flatten", action="store_true", help="skip the rs_flatten_dag extra measurement")
     ap.add_argument("--no-templated", action="store_true", help="skip the template-replicated extra circuit")
+    ap.add_argument("--no-o1", action="store_true", help="skip the --O1 extra (the metric circuit at circom's default level)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,6 +297,21 @@ def main():
                             f"(SURVEY 8(d) config 5's replication), host -> host"}
         tpin.free()
         tinp.free()
+    # ---- extra: --O1, circom's default since 2.2.0 (circom/src/input_user.rs:304): the same circuit,
+    # host -> host; no linear elimination, the linear rows join lconst (constraint_simplification.rs:575-577)
+    o1 = None
+    if rank == 0 and world == 1 and not args.no_o1:
+        fl1 = M.make_flags("O1", device=local)
+        for _ in range(2):
+            eng.simplify(pin.c, fl1)
+        k1 = min(args.steps, 20)
+        o1dt, _, _, o1out, _ = timed_steps(eng, pin.c, fl1, k1, lambda: None)
+        o1 = {"value": round(n_rows * k1 / o1dt, 1), "unit": "constraints/s", "ms_per_step": round(o1dt * 1000.0 / k1, 3),
+              "steps": k1, "constraints": n_rows, "n_constraints_out": int(o1out.n_constraints),
+              "workload": f"synth_mixed rows={args.rows} seed={args.seed} {args.prime} --O1, host -> host"}
+        if not args.no_cpu:
+            import rsio
+            o1["_arrays"] = rsio.output_arrays(o1out)  # checked against the oracle below, then dropped
     # ---- extra: the same engine with the input resident in HBM (rs_engine_run only)
     eng.load(pin.c)
     barrier()
@@ -387,6 +403,14 @@ def main():
             line["flatten_dag"] = flat
         if tmpl is not None:
             line["templated"] = tmpl
+        if o1 is not None:
+            got1 = o1.pop("_arrays", None)
+            if got1 is not None:
+                import rsio
+                ref1, ms1 = rsio.oracle_arrays(inp.c, rsio.flags("O1"), threads=args.cpu_threads or cpu_threads())
+                o1["bit_exact"] = rsio.diff_output_arrays(got1, ref1) is None
+                o1["cpu_oracle_ms"] = round(ms1, 1)
+            line["o1"] = o1
         if weak is not None:
             line["weak_shards"] = weak
         if not args.no_cpu:

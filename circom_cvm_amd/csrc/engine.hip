@@ -9,7 +9,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
+#include <mutex>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -211,8 +214,8 @@ struct rs_engine {
     void *p = nullptr;
     size_t cap = 0;
   };
-  Pin pin[16];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers;
-                // a/b/c row ends (streamed result)
+  Pin pin[20];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers;
+                // a/b/c row ends (streamed result); [16..17] the host replay's staging
   rs_output view{};
   // streamed result (output.hpp; rs_engine_simplify): the storage rows final after round 1 go to
   // pin[3..8] on the copy stream during the later rounds (ev_snap: their D2H is done)
@@ -231,6 +234,9 @@ struct rs_engine {
   bool sh_full = false;         // the region was regrown at the end: the whole [early | late] is copied
   uint64_t sh_klo = 0, sh_khi = 0;  // this rank's run of the keep list (global output rows)
   hipEvent_t ev_snap = nullptr, ev_snap0 = nullptr;  // early gather done / its inputs ready
+  uint64_t snap_cap[3] = {0, 0, 0};   // capacity (entries) of the device and host early regions this run
+  uint64_t snap_hint[3] = {0, 0, 0};  // the largest early region (both snapshots) of the runs so far
+  void *snap_host[6] = {};            // the host early regions: col / val of a, b, c
   // The early region's D2H runs on its own host thread, in chunks, one in flight at a time: the
   // copy engine serves transfers in order, so one large transfer would hold every small D2H the run
   // still issues (scan totals, flags, the head's frontier counts) behind it for ~15 ms.
@@ -238,10 +244,13 @@ struct rs_engine {
     void *dst;
     const void *src;
     size_t bytes;
-    int part;  // ev_snapq[part] marks its gather done
+    hipEvent_t ready;  // its gather is done
   };
-  hipEvent_t ev_snapq[3] = {};
-  std::vector<SnapJob> snap_jobs;
+  hipEvent_t ev_snapq[6] = {};  // the parts' gathers of the first / second snapshot
+  std::mutex snap_m;
+  std::condition_variable snap_cv;
+  std::deque<SnapJob> snap_q;  // jobs the D2H thread has not started; closed: no more will come
+  bool snap_closed = true;
   std::thread snap_thread;
   hipStream_t stx = nullptr;  // the early region's D2H stream
   hipStream_t str = nullptr;  // the host replay's copies (small; never behind the bulk copies)
@@ -495,6 +504,7 @@ static void load_order_collectives(rs_engine *E) {
 }
 // After a failed call: the copy stream may still be reading the caller's buffers.
 static void snap_join(rs_engine *E);
+static void *pin_get(rs_engine *E, int slot, size_t bytes);
 static void load_abort(rs_engine *E) {
   if (E->stc) (void)hipStreamSynchronize(E->stc);
   snap_join(E);
@@ -951,11 +961,19 @@ static bool is_zero4(const uint64_t *v) { return (v[0] | v[1] | v[2] | v[3]) == 
 
 
 // ---------------------------------------------------------------- elimination driver
-struct ElimOut {
-  uint64_t n_clusters = 0;
-  std::vector<uint64_t> cl_off;
-  std::vector<uint32_t> n_sub, n_left;
+struct ElimOut {  // what the host keeps of a round's elimination (the rest stays on the device)
+  uint64_t n_clusters = 0, n_slots = 0;
+  uint64_t n_sub = 0, n_left = 0;  // totals over the clusters
 };
+__global__ void k_sum_counts(const uint32_t *n_sub, const uint32_t *n_left, uint64_t n, unsigned long long *sums) {
+  unsigned long long a = 0, b = 0;
+  for (uint64_t c = gtid(); c < n; c += gstride()) {
+    a += n_sub[c];
+    b += n_left[c];
+  }
+  wave_atomic_add(sums, a);
+  wave_atomic_add(sums + 1, b);
+}
 
 struct Pool {
   uint32_t *pk = nullptr;
@@ -1031,8 +1049,10 @@ struct LevelLoop {
 // Kahn levels of the head's composition launched over the whole GPU before k_compose_rest takes the
 // rest per cluster in one workgroup each (level 0's items need no composition)
 constexpr uint32_t kHeadGpuLevels = 8;
-// the number of largest clusters eliminated on the second stream (16 / 32 / 64 measured equal)
-constexpr uint64_t kHeadLimit = 16;
+// the number of largest clusters eliminated on the second stream by the speculative loop: the next
+// size class (1,100-1,700 rows on the metric circuit) took 7-8 ms each in the tail's one-wave loop,
+// which held the first frames pass -- and so the result stream -- back until the tail was done
+constexpr uint64_t kHeadLimit = 48;
 // The arena replay of one cluster on the host (k_cl_replay_lane's walk): rows in index order, each
 // pair's previous row found by path halving and its root's list appended to the row's.  A serial
 // union-find of dependent accesses: ~20 ns a pair in a host cache against ~0.3 us in LDS, and the
@@ -1069,8 +1089,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   hipStream_t st = E->st;
   DevClusters D;
   const uint64_t n = V.n;
-  eo.cl_off.assign(1, 0);
-  eo.n_clusters = 0;
+  eo = ElimOut{};
   D.cl_off = A.get<uint64_t>("el.cl", 1);
   HC(hipMemsetAsync(D.cl_off, 0, 8, st));
   if (n == 0) return D;
@@ -1153,73 +1172,76 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
       HC(hipGetLastError());
     }
     const double th0 = now_ms();
-    // every input of the replays is complete (the stream was synchronised above): two copy rounds on
-    // str -- each cluster's (first row, rows, first pair, pairs, ordered rows), then its offsets,
-    // pair stream and rows
+    // every input of the replays is complete (the stream was synchronised above).  Per cluster (first
+    // row, rows, first pair, pairs, ordered rows) into pinned memory; an order-free cluster's list is
+    // its row order (d_cl_order_free), copied on the device; the rest are replayed on the host (their
+    // offsets, pair streams and rows in one pinned staging block, the orders back from it)
     const uint64_t nh = hc[4];
     uint64_t *d_meta = A.get<uint64_t>("cl.rmeta", 5 * nh);
     launch(E->str, k_replay_meta, nh, (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), nh,
            (const uint64_t *)q_off, (const uint32_t *)n_ordered, d_meta);
-    std::vector<uint64_t> meta(5 * nh);
-    HC(hipMemcpyAsync(meta.data(), d_meta, 40 * nh, hipMemcpyDeviceToHost, E->str));
+    uint64_t *meta = (uint64_t *)pin_get(E, 16, 40 * nh);
+    HC(hipMemcpyAsync(meta, d_meta, 40 * nh, hipMemcpyDeviceToHost, E->str));
     HC(hipStreamSynchronize(E->str));
-    std::vector<uint64_t> qn(nh), rb(nh);
-    std::vector<uint32_t> hord(nh);
+    HC(hipEventRecord(E->evx[6], st));
+    HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
+    std::vector<uint64_t> todo;
     uint64_t tot_q = 0, tot_n = 0;
     for (uint64_t i = 0; i < nh; ++i) {
-      rb[i] = meta[5 * i];
-      qn[i] = meta[5 * i + 1];
-      hord[i] = (uint32_t)meta[5 * i + 4];
-      tot_n += qn[i];
+      const uint64_t rb = meta[5 * i], qn = meta[5 * i + 1];
+      if (qn >= 350 && qn < 1000000 && !old_heur && meta[5 * i + 4] == 0) {  // d_cl_order_free
+        HC(hipMemcpyAsync(D.perm + rb, srow + rb, 4 * qn, hipMemcpyDeviceToDevice, E->st2));
+        continue;
+      }
+      todo.push_back(i);
+      tot_n += qn;
       tot_q += meta[5 * i + 3];
     }
-    std::vector<uint64_t> qo(tot_n + nh);
-    std::vector<uint32_t> hst(tot_q), hsrow(tot_n), hperm(tot_n);
-    for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += meta[5 * i + 3], on += qn[i], o += qn[i] + 1, ++i) {
-      HC(hipMemcpyAsync(qo.data() + o, q_off + rb[i], 8 * (qn[i] + 1), hipMemcpyDeviceToHost, E->str));
-      if (meta[5 * i + 3])
-        HC(hipMemcpyAsync(hst.data() + oq, stream + meta[5 * i + 2], 4 * meta[5 * i + 3], hipMemcpyDeviceToHost, E->str));
-      HC(hipMemcpyAsync(hsrow.data() + on, srow + rb[i], 4 * qn[i], hipMemcpyDeviceToHost, E->str));
-    }
-    HC(hipStreamSynchronize(E->str));
-    {  // the clusters over a few host threads (largest first: the list is size-ordered)
-      std::vector<uint64_t> o_q(nh), o_n(nh), o_o(nh);
-      for (uint64_t i = 0, oq = 0, on = 0, o = 0; i < nh; oq += meta[5 * i + 3], on += qn[i], o += qn[i] + 1, ++i) {
-        o_q[i] = oq;
-        o_n[i] = on;
-        o_o[i] = o;
+    const uint64_t nt = todo.size();
+    if (nt) {
+      // staging: qo (tot_n + nt u64), pairs (tot_q u32), rows (tot_n u32), orders (tot_n u32)
+      uint8_t *stg = (uint8_t *)pin_get(E, 17, 8 * (tot_n + nt) + 4 * (tot_q + 2 * tot_n));
+      uint64_t *qo = (uint64_t *)stg;
+      uint32_t *hst = (uint32_t *)(qo + tot_n + nt), *hsrow = hst + tot_q, *hperm = hsrow + tot_n;
+      std::vector<uint64_t> o_q(nt), o_n(nt), o_o(nt);
+      for (uint64_t t = 0, oq = 0, on = 0, o = 0; t < nt; ++t) {
+        const uint64_t i = todo[t], rb = meta[5 * i], qn = meta[5 * i + 1], np = meta[5 * i + 3];
+        o_q[t] = oq;
+        o_n[t] = on;
+        o_o[t] = o;
+        HC(hipMemcpyAsync(qo + o, q_off + rb, 8 * (qn + 1), hipMemcpyDeviceToHost, E->str));
+        if (np) HC(hipMemcpyAsync(hst + oq, stream + meta[5 * i + 2], 4 * np, hipMemcpyDeviceToHost, E->str));
+        HC(hipMemcpyAsync(hsrow + on, srow + rb, 4 * qn, hipMemcpyDeviceToHost, E->str));
+        oq += np;
+        on += qn;
+        o += qn + 1;
       }
-      std::atomic<uint64_t> next_i{0};
-      auto work = [&] {
-        for (uint64_t i; (i = next_i.fetch_add(1)) < nh;) {
-          const uint64_t *qoi = qo.data() + o_o[i], q0 = qoi[0];
-          const uint32_t n_i = (uint32_t)qn[i];
-          uint32_t *out = hperm.data() + o_n[i];
-          const uint32_t *sr = hsrow.data() + o_n[i], *sq = hst.data() + o_q[i];
-          if (n_i >= 350 && n_i < 1000000 && !old_heur && hord[i] == 0) {  // d_cl_order_free
-            std::copy(sr, sr + n_i, out);
-            continue;
-          }
+      HC(hipStreamSynchronize(E->str));
+      std::atomic<uint64_t> next_t{0};
+      auto work = [&] {  // a few host threads, largest cluster first (the list is size-ordered)
+        for (uint64_t t; (t = next_t.fetch_add(1)) < nt;) {
+          const uint64_t *qoi = qo + o_o[t], q0 = qoi[0];
+          const uint32_t n_i = (uint32_t)meta[5 * todo[t] + 1];
           std::vector<uint64_t> rel(n_i + 1);
-          for (uint32_t t = 0; t <= n_i; ++t) rel[t] = qoi[t] - q0;
-          host_replay(n_i, rel.data(), sq, sr, out);
+          for (uint32_t k = 0; k <= n_i; ++k) rel[k] = qoi[k] - q0;
+          host_replay(n_i, rel.data(), hst + o_q[t], hsrow + o_n[t], hperm + o_n[t]);
         }
       };
       const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-      const uint64_t n_th = std::min<uint64_t>({nh, (uint64_t)hw, 16});
+      const uint64_t n_th = std::min<uint64_t>({nt, (uint64_t)hw, 16});
       std::vector<std::thread> th;
       for (uint64_t k = 1; k < n_th; ++k) th.emplace_back(work);
       work();
       for (auto &t : th) t.join();
+      for (uint64_t t = 0; t < nt; ++t) {
+        const uint64_t i = todo[t];
+        HC(hipMemcpyAsync(D.perm + meta[5 * i], hperm + o_n[t], 4 * meta[5 * i + 1], hipMemcpyHostToDevice, E->st2));
+      }
+      HC(hipStreamSynchronize(E->st2));  // the staging block is reused by the next round's replay
     }
-    HC(hipEventRecord(E->evx[6], st));
-    HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
-    for (uint64_t i = 0, on = 0; i < nh; on += qn[i], ++i)
-      HC(hipMemcpyAsync(D.perm + rb[i], hperm.data() + on, 4 * qn[i], hipMemcpyHostToDevice, E->st2));
-    HC(hipStreamSynchronize(E->st2));  // the pageable sources go out of scope
     if (g_prof_env)
-      fprintf(stderr, "[rs-prof] host replay: %llu clusters, %llu rows, %llu pairs, %.2f ms\n", (unsigned long long)nh,
-              (unsigned long long)tot_n, (unsigned long long)tot_q, now_ms() - th0);
+      fprintf(stderr, "[rs-prof] host replay: %llu clusters (%llu order-free), %llu rows, %llu pairs, %.2f ms\n", (unsigned long long)nh,
+              (unsigned long long)(nh - nt), (unsigned long long)tot_n, (unsigned long long)tot_q, now_ms() - th0);
   }
   if (hc[2] && !hc[4]) {  // (kClSmall, kClMid] (launched above when there is a host replay)
     const uint64_t nm = hc[2] - hc[4];
@@ -1248,9 +1270,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   D.n_slots = n_act;
   D.cid = cid;
   eo.n_clusters = n_cl;
-  eo.cl_off.resize(n_cl + 1);
-  HC(hipMemcpyAsync(eo.cl_off.data(), D.cl_off, 8 * (n_cl + 1), hipMemcpyDeviceToHost, st));
-  HC(hipStreamSynchronize(st));
+  eo.n_slots = n_act;
   E->stats.n_clusters += n_cl;
   E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, (0xffffffffull - (first >> 32)) & 0x7fffffffull);
   return D;
@@ -1555,7 +1575,17 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
       HC(hipEventRecord(E->ev3, E->st));
     }
+    // the verdict and the substitution / leftover totals in one read-back
+    unsigned long long *d_sums = E->A.get<unsigned long long>("el.sums", 2);
+    auto sum_counts = [&](unsigned long long *h) {
+      HC(hipMemsetAsync(d_sums, 0, 16, E->st));
+      if (eo.n_clusters) launch_capped(E->st, k_sum_counts, eo.n_clusters, 256, (const uint32_t *)a.n_sub, (const uint32_t *)a.n_left,
+                                       eo.n_clusters, d_sums);
+      HC(hipMemcpyAsync(h, d_sums, 16, hipMemcpyDeviceToHost, E->st));
+    };
+    unsigned long long sums[2] = {0, 0};
     int err = 0;
+    sum_counts(sums);
     HC(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, E->st));
     HC(hipStreamSynchronize(E->st));
     if (W > 1) {  // every rank takes the same retry / failure decision
@@ -1710,14 +1740,13 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
                 p[15] / 100.0, p[16] / 100.0, p[17] / 100.0, p[18] / 100.0, p[19] / 100.0, p[11] / 100.0, p[20], p[21]);
       }
     }
-    eo.n_sub.resize(eo.n_clusters);
-    eo.n_left.resize(eo.n_clusters);
-    if (eo.n_clusters) {
-      HC(hipMemcpyAsync(eo.n_sub.data(), a.n_sub, 4 * eo.n_clusters, hipMemcpyDeviceToHost, E->st));
-      HC(hipMemcpyAsync(eo.n_left.data(), a.n_left, 4 * eo.n_clusters, hipMemcpyDeviceToHost, E->st));
+    if (W > 1 && eo.n_clusters) {  // the exchange rebuilt the per-cluster counts from every rank's records
+      sum_counts(sums);
       HC(hipStreamSynchronize(E->st));
     }
-    for (auto x : eo.n_sub) E->stats.n_substitutions += x;
+    eo.n_sub = sums[0];
+    eo.n_left = sums[1];
+    E->stats.n_substitutions += eo.n_sub;
     E->stats.elim_ms += now_ms() - t1;
     return;
   }
@@ -1756,9 +1785,7 @@ struct LcHeap {
 
 // a round's leftovers (cluster order, then push order) -> the lconst heap
 static void collect_leftovers(rs_engine *E, const ElimOut &eo, const Pool &P, LcHeap &lc) {
-  const uint64_t n_slots = eo.cl_off.empty() ? 0 : eo.cl_off.back();
-  uint64_t nl = 0;
-  for (uint32_t x : eo.n_left) nl += x;
+  const uint64_t n_slots = eo.n_slots, nl = eo.n_left;
   if (!nl || !n_slots) return;
   Arena &A = E->A;
   uint64_t *f = A.get<uint64_t>("lc.lf", n_slots), *fp = A.get<uint64_t>("lc.lp", n_slots);
@@ -1790,7 +1817,7 @@ static void log_push(rs_engine *E, uint32_t from, const uint32_t *k, const uint6
 static void log_linear_round(rs_engine *E, const ElimOut &eo, const Pool &P) {
   Arena &A = E->A;
   hipStream_t st = E->st;
-  const uint64_t n_slots = eo.cl_off.empty() ? 0 : eo.cl_off.back();
+  const uint64_t n_slots = eo.n_slots;
   if (!n_slots) return;
   uint64_t *vf = A.get<uint64_t>("lg.vf", n_slots), *vp = A.get<uint64_t>("lg.vp", n_slots);
   const uint32_t *cid = A.get<uint32_t>("cl.cid", 1);
@@ -1906,34 +1933,52 @@ static void debug_check_round(rs_engine *E, const RoundArgs &ra, uint64_t n, uin
 }
 
 // ---------------------------------------------------------------- the run
-// the early region's D2H (see rs_engine::SnapJob): chunks of kSnapChunk bytes, each waited for
+// the early region's D2H (see rs_engine::SnapJob) on its own thread, fed with jobs as snapshots are
+// taken: each job waits for its gather, then goes in 16 MB chunks, two in flight (8 / 16 / 64 MB
+// chunks measured 53.0 / 52.2 / 55.0 ms host -> host)
 static void snap_join(rs_engine *E) {
+  {
+    std::lock_guard<std::mutex> lk(E->snap_m);
+    E->snap_closed = true;
+  }
+  E->snap_cv.notify_all();
   if (E->snap_thread.joinable()) E->snap_thread.join();
-  E->snap_jobs.clear();
+  E->snap_q.clear();
+}
+static void snap_push(rs_engine *E, const rs_engine::SnapJob &j) {
+  {
+    std::lock_guard<std::mutex> lk(E->snap_m);
+    E->snap_q.push_back(j);
+  }
+  E->snap_cv.notify_all();
 }
 static void snap_start(rs_engine *E) {
-  if (E->snap_thread.joinable()) E->snap_thread.join();
+  if (E->snap_thread.joinable()) return;  // running: jobs are pushed to it
   E->snap_rc = 0;
-  std::vector<rs_engine::SnapJob> jobs = E->snap_jobs;
-  E->snap_thread = std::thread([E, jobs]() {
-    // 16 MB chunks (8 / 16 / 64 MB measured 53.0 / 52.2 / 55.0 ms host -> host)
+  E->snap_closed = false;
+  E->snap_thread = std::thread([E]() {
     constexpr size_t chunk = 16ull << 20;
     if (hipSetDevice(E->device) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
-    // two chunks in flight: no gap between them, and a transfer another stream enqueues waits for
-    // at most two
-    int k = 0, part = -1;
-    for (const auto &j : jobs) {
-      if (j.part != part) {
-        part = j.part;
-        if (hipEventSynchronize(E->ev_snapq[part]) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
+    int k = 0;
+    for (;;) {
+      rs_engine::SnapJob j;
+      {
+        std::unique_lock<std::mutex> lk(E->snap_m);
+        E->snap_cv.wait(lk, [E] { return E->snap_closed || !E->snap_q.empty(); });
+        if (E->snap_q.empty()) break;  // closed and drained
+        j = E->snap_q.front();
+        E->snap_q.pop_front();
       }
+      if (E->snap_rc) continue;
+      // (an event a later snapshot records again is waited for at its newer point: still after this gather)
+      if (hipEventSynchronize(j.ready) != hipSuccess) { E->snap_rc = RS_E_HIP; continue; }
       for (size_t o = 0; o < j.bytes; o += chunk, ++k) {
         const size_t n = std::min(chunk, j.bytes - o);
-        if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
+        if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
         if (hipMemcpyAsync((uint8_t *)j.dst + o, (const uint8_t *)j.src + o, n, hipMemcpyDeviceToHost, E->stx) != hipSuccess ||
             hipEventRecord(E->ev_chunk[k & 1], E->stx) != hipSuccess) {
           E->snap_rc = RS_E_HIP;
-          return;
+          break;
         }
       }
     }
@@ -2426,26 +2471,77 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
     for (int q = 0; q < 3; ++q) {
       E->snap_e[q] = ev[q];
+      E->snap_hint[q] = std::max(E->snap_hint[q], ev[q]);
       // the device early region = the head of the layout's arrays; the late rows follow it
-      const uint64_t cap = ev[q] + std::max<uint64_t>(ev[q] / 4, 1 << 16);
+      // room for the second snapshot's rows too (the largest early region so far, else a margin)
+      const uint64_t cap = std::max<uint64_t>(ev[q] + std::max<uint64_t>(ev[q] / 4, 1 << 16), E->snap_hint[q]);
       const std::string xn = std::string("out.") + "abc"[q];
       uint32_t *col = A.get<uint32_t>(xn + ".xcol", cap);
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
-      if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val);
+      if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
+                        (const uint64_t *)nullptr);
       void *hc = shard ? (void *)(sh_col(E, q) + CM->rank * E->sh_cap[q]) : pin_get(E, 3 + q, 4 * cap);
       void *hv = shard ? (void *)(sh_val(E, q) + 4 * CM->rank * E->sh_cap[q]) : pin_get(E, 6 + q, 32 * cap);
+      E->snap_cap[q] = cap;
+      E->snap_host[2 * q] = hc;
+      E->snap_host[2 * q + 1] = hv;
       if (ev[q]) {  // a part's copies start once its own gather is done
         HC(hipEventRecord(E->ev_snapq[q], E->stc));
-        E->snap_jobs.push_back({hc, col, 4 * ev[q], q});
-        E->snap_jobs.push_back({hv, val, 32 * ev[q], q});
+        snap_start(E);
+        snap_push(E, {hc, col, 4 * ev[q], E->ev_snapq[q]});
+        snap_push(E, {hv, val, 32 * ev[q], E->ev_snapq[q]});
       }
     }
     HC(hipEventRecord(E->ev_snap, E->stc));
     E->snap_on = true;
-    snap_start(E);
     if (g_prof_env)
       fprintf(stderr, "[rs-prof] stream: early region %llu / %llu / %llu entries (%.1f MB)%s\n", (unsigned long long)ev[0],
               (unsigned long long)ev[1], (unsigned long long)ev[2], 36e-6 * (ev[0] + ev[1] + ev[2]), late ? " after the first pass" : "");
+  };
+  // The second snapshot (single engine): the rows of the second frames pass -- those touching the head
+  // clusters -- that stayed storage rows go behind the first snapshot's, when they fit the regions
+  // sized at the first (else they stay late), so they stream during the later rounds too.
+  auto snap_take2 = [&]() {
+    if (!E->snap_on || !nl_late || !n_late || (E->comm && E->comm->world > 1)) return;
+    HC(hipStreamWaitEvent(st, E->ev_snap, 0));  // the first snapshot's gathers read the flags rewritten here
+    U3 *elen = A.get<U3>("so.elen", n_nl), *eoff2 = A.get<U3>("so.eoff2", n_nl);
+    launch(st, k_snap_lens2, n_nl, sa, sb, sc, (const uint64_t *)nl_late, n_nl, elen);
+    const U3 et = excl_scan_u3(E, elen, eoff2, n_nl, "so2");
+    const uint64_t e2[3] = {et.a, et.b, et.c};
+    for (int q = 0; q < 3; ++q) E->snap_hint[q] = std::max(E->snap_hint[q], E->snap_e[q] + e2[q]);
+    for (int q = 0; q < 3; ++q)
+      if (E->snap_e[q] + e2[q] > E->snap_cap[q]) return;  // no room this time (the hint grows the next run's)
+    launch(st, k_snap_mark2, n_nl, (const uint64_t *)nl_late, (const U3 *)elen, (const U3 *)eoff2,
+           U3{E->snap_e[0], E->snap_e[1], E->snap_e[2]}, n_nl, so_early, so_eoff);
+    const DRows *src[3] = {&sa, &sb, &sc};
+    const char *nm[3] = {"so2.a", "so2.b", "so2.c"};
+    DRows cp[3];
+    for (int q = 0; q < 3; ++q) {  // copies of the row views (the rounds re-point rows)
+      cp[q] = *src[q];
+      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
+      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
+      HC(hipMemcpyAsync(cp[q].off, src[q]->off, 8 * n_nl, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(cp[q].len, src[q]->len, 4 * n_nl, hipMemcpyDeviceToDevice, st));
+    }
+    HC(hipEventRecord(E->ev_snap0, st));
+    HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
+    for (int q = 0; q < 3; ++q) {
+      const uint64_t b = E->snap_e[q];
+      const std::string xn = std::string("out.") + "abc"[q];
+      uint32_t *col = A.get<uint32_t>(xn + ".xcol", 1);
+      uint64_t *val = A.get<uint64_t>(xn + ".xval", 1);
+      if (!e2[q]) continue;
+      launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
+             (const uint64_t *)nl_late);
+      HC(hipEventRecord(E->ev_snapq[3 + q], E->stc));
+      snap_push(E, {(uint32_t *)E->snap_host[2 * q] + b, col + b, 4 * e2[q], E->ev_snapq[3 + q]});
+      snap_push(E, {(uint64_t *)E->snap_host[2 * q + 1] + 4 * b, val + 4 * b, 32 * e2[q], E->ev_snapq[3 + q]});
+      E->snap_e[q] = b + e2[q];
+    }
+    HC(hipEventRecord(E->ev_snap, E->stc));
+    if (g_prof_env)
+      fprintf(stderr, "[rs-prof] stream: second snapshot %llu / %llu / %llu entries (%.1f MB)\n", (unsigned long long)e2[0],
+              (unsigned long long)e2[1], (unsigned long long)e2[2], 36e-6 * (e2[0] + e2[1] + e2[2]));
   };
   auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1) {
     stage_nl();
@@ -2591,6 +2687,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       nl_ms(E->ev0, E->ev1);
     } else if (n_late) {
       nl_phase(2, nl_lids, n_late, E->ev0, E->ev1);
+      snap_take2();
       nl_ms(E->ev0, E->ev1);
     }
   }
@@ -2650,6 +2747,55 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     so_dirty = A.get<uint8_t>("so.dirty", n_st ? n_st : 1);
     if (n_st) HC(hipMemsetAsync(so_dirty, 0, n_st, st));
   }
+  // A round's snapshot (single engine): the storage rows the round rewrote that stay storage rows go
+  // behind the early region right away -- final unless a later round rewrites them again (dirty once
+  // more: late at the end) -- so a round that rewrites most rows (the templated circuit's round 2)
+  // streams them while the run goes on instead of after it.  Skipped when the regions sized at the first
+  // snapshot cannot take them (the capacity hint grows for the next run).
+  auto snap_round = [&](const uint8_t *touched, const int32_t *turn, const DRows &pa, const DRows &pb, const DRows &pc) {
+    if (!so_dirty || !n_st || (E->comm && E->comm->world > 1)) return;
+    // the earlier snapshots' gathers read the early flags / offsets this one rewrites, and its own buffers
+    HC(hipStreamWaitEvent(st, E->ev_snap, 0));
+    U3 *elen = A.get<U3>("so.rlen", n_st), *eoff3 = A.get<U3>("so.roff", n_st);
+    launch(st, k_snap_lens_round, n_st, pa, pb, pc, touched, turn, n_st, elen);
+    const U3 et = excl_scan_u3(E, elen, eoff3, n_st, "sor");
+    const uint64_t e3[3] = {et.a, et.b, et.c};
+    if (!(e3[0] | e3[1] | e3[2])) return;
+    for (int q = 0; q < 3; ++q) E->snap_hint[q] = std::max(E->snap_hint[q], E->snap_e[q] + e3[q]);
+    for (int q = 0; q < 3; ++q)
+      if (E->snap_e[q] + e3[q] > E->snap_cap[q]) return;
+    launch(st, k_snap_mark_round, n_st, (const uint32_t *)st_ids, (const U3 *)elen, (const U3 *)eoff3,
+           U3{E->snap_e[0], E->snap_e[1], E->snap_e[2]}, n_st, so_early, so_eoff, so_dirty);
+    const DRows *src[3] = {&pa, &pb, &pc};
+    const char *nm[3] = {"sor.a", "sor.b", "sor.c"};
+    DRows cp[3];
+    for (int q = 0; q < 3; ++q) {  // copies of the row views (a later round re-points rows)
+      cp[q] = *src[q];
+      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_st);
+      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_st);
+      HC(hipMemcpyAsync(cp[q].off, src[q]->off, 8 * n_st, hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(cp[q].len, src[q]->len, 4 * n_st, hipMemcpyDeviceToDevice, st));
+    }
+    // the previous snapshot's gathers still read their view copies and elen / offsets (stc is in order)
+    HC(hipEventRecord(E->ev_snap0, st));
+    HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
+    for (int q = 0; q < 3; ++q) {
+      const uint64_t b = E->snap_e[q];
+      const std::string xn = std::string("out.") + "abc"[q];
+      uint32_t *col = A.get<uint32_t>(xn + ".xcol", 1);
+      uint64_t *val = A.get<uint64_t>(xn + ".xval", 1);
+      if (!e3[q]) continue;
+      launch(E->stc, k_snap_gather_st, n_st, E->F, cp[q], (const U3 *)elen, (const U3 *)eoff3, b, q, n_st, col, val);
+      HC(hipEventRecord(E->ev_snapq[3 + q], E->stc));
+      snap_push(E, {(uint32_t *)E->snap_host[2 * q] + b, col + b, 4 * e3[q], E->ev_snapq[3 + q]});
+      snap_push(E, {(uint64_t *)E->snap_host[2 * q + 1] + 4 * b, val + 4 * b, 32 * e3[q], E->ev_snapq[3 + q]});
+      E->snap_e[q] = b + e3[q];
+    }
+    HC(hipEventRecord(E->ev_snap, E->stc));
+    if (g_prof_env)
+      fprintf(stderr, "[rs-prof] stream: round snapshot %llu / %llu / %llu entries (%.1f MB)\n", (unsigned long long)e3[0],
+              (unsigned long long)e3[1], (unsigned long long)e3[2], 36e-6 * (e3[0] + e3[1] + e3[2]));
+  };
   if (getenv("RS_DEBUG")) {
     HC(hipStreamSynchronize(st));
     fprintf(stderr, "[rs-debug] heap %p cap %llu top %llu n_st %llu n_wl %llu\n", (void *)heap_k,
@@ -2739,7 +2885,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       // ordered substitutions of the round: cluster order, ascending `from` -- one sort of the
       // (cluster, from) keys of the valid slots on the device; the host fetches the list only when
       // a row turned linear or another round follows
-      const uint64_t n_slots = er.cl_off.back();
+      const uint64_t n_slots = er.n_slots;
       uint64_t nU = 0;
       uint32_t *d_us = A.get<uint32_t>("r.us", 1), *d_U = A.get<uint32_t>("r.U", 1), *d_ulen = A.get<uint32_t>("r.ulen", 1);
       uint64_t *d_uoff = A.get<uint64_t>("r.uoff", 1);
@@ -2910,6 +3056,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         if (getenv("RS_DEBUG")) debug_check_round(E, ra, n_st, qt);
         launch(st, k_commit_round, n_st, (const uint8_t *)ra.touched, (const int32_t *)ra.turn, n_st, ta_, tb_, tc_, oa, ob, oc);
         if (so_dirty) launch(st, k_or_u8, n_st, (const uint8_t *)ra.touched, n_st, so_dirty);
+        snap_round(ra.touched, ra.turn, ta_, tb_, tc_);
         // turned rows
         uint64_t *tf = A.get<uint64_t>("r.tf", n_st), *tp = A.get<uint64_t>("r.tp", n_st);
         launch(st, k_turn_flags, n_st, (const int32_t *)ra.turn, n_st, tf);

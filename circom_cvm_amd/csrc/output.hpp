@@ -27,13 +27,68 @@ __global__ void k_snap_flags(DRows a, DRows b, DRows c, const uint64_t *late, ui
   }
 }
 
+// The second snapshot: the rows the second frames pass did (late[i]) that stayed storage rows --
+// elen[i] their part lengths (else 0); once they fit behind the first snapshot, k_snap_mark2 makes
+// them early at base + their offsets.
+__global__ void k_snap_lens2(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, U3 *elen) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const bool ok = late[i] && (a.len[i] | b.len[i]) != 0;
+    elen[i] = ok ? U3{a.len[i], b.len[i], c.len[i]} : U3{0, 0, 0};
+  }
+}
+__global__ void k_snap_mark2(const uint64_t *late, const U3 *elen, const U3 *eoff2, U3 base, uint64_t n, uint8_t *early,
+                             U3 *eoff) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    if (!late[i] || (elen[i].a | elen[i].b) == 0) continue;
+    early[i] = 1;
+    eoff[i] = U3{base.a + eoff2[i].a, base.b + eoff2[i].b, base.c + eoff2[i].c};
+  }
+}
+
 // the early rows of one part, canonical, at their early-region offsets (R: a copy of the row views
-// taken at the snapshot, so later rounds may move the rows meanwhile)
+// taken at the snapshot, so later rounds may move the rows meanwhile; only: the second snapshot's
+// rows, else every early row)
 __global__ void k_snap_gather(FieldP F, DRows R, const uint8_t *early, const U3 *eoff, int q, uint64_t n, uint32_t *col,
-                              uint64_t *val) {
+                              uint64_t *val, const uint64_t *only) {
   for (uint64_t r = gtid(); r < n; r += gstride()) {
-    if (!early[r]) continue;
+    if (!early[r] || (only && !only[r])) continue;
     const uint64_t o = u3_sel(eoff[r], q), s = R.off[r];
+    const uint32_t len = R.len[r];
+    for (uint32_t t = 0; t < len; ++t) {
+      col[o + t] = R.key[s + t];
+      const Fe c = ffrom_mont(F, R.val[s + t]);
+      val[4 * (o + t) + 0] = c.l[0];
+      val[4 * (o + t) + 1] = c.l[1];
+      val[4 * (o + t) + 2] = c.l[2];
+      val[4 * (o + t) + 3] = c.l[3];
+    }
+  }
+}
+
+// A round's snapshot: the storage rows the round rewrote (touched) that stay storage rows (turn < 0)
+// -- elen[r] their part lengths by storage id (else 0); k_snap_mark_round makes them early at base +
+// their offsets (by non-linear row nl_of[r]) and clean again; k_snap_gather_st copies them.
+__global__ void k_snap_lens_round(DRows a, DRows b, DRows c, const uint8_t *touched, const int32_t *turn, uint64_t n, U3 *elen) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    const bool ok = touched[r] && turn[r] < 0 && (a.len[r] | b.len[r]) != 0;
+    elen[r] = ok ? U3{a.len[r], b.len[r], c.len[r]} : U3{0, 0, 0};
+  }
+}
+__global__ void k_snap_mark_round(const uint32_t *nl_of, const U3 *elen, const U3 *eoff3, U3 base, uint64_t n, uint8_t *early,
+                                  U3 *eoff, uint8_t *dirty) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    if ((elen[r].a | elen[r].b) == 0) continue;
+    const uint32_t i = nl_of[r];
+    early[i] = 1;
+    eoff[i] = U3{base.a + eoff3[r].a, base.b + eoff3[r].b, base.c + eoff3[r].c};
+    dirty[r] = 0;
+  }
+}
+__global__ void k_snap_gather_st(FieldP F, DRows R, const U3 *elen, const U3 *eoff3, uint64_t base, int q, uint64_t n,
+                                 uint32_t *col, uint64_t *val) {
+  for (uint64_t r = gtid(); r < n; r += gstride()) {
+    if ((elen[r].a | elen[r].b) == 0) continue;
+    const uint64_t o = base + u3_sel(eoff3[r], q), s = R.off[r];
     const uint32_t len = R.len[r];
     for (uint32_t t = 0; t < len; ++t) {
       col[o + t] = R.key[s + t];

@@ -198,8 +198,15 @@ def test_sharded_hosthost_bls12381_20m_world8():
     over 8 ranks host -> host (split upload, sharded elimination with the exchange, split result
     copy), every rank array for array equal to the single-GPU oracle.  In one process on one GPU
     (8 engines), so the group is made for this test and closed after it."""
+    import sys
+    import time
     world = 8
+    t0 = time.time()
+
+    def say(what):  # progress past the output capture (a quiet minute reads as a hang on the GPU box)
+        print(f"[20M world 8] {what} at {time.time() - t0:.0f} s", file=sys.__stderr__, flush=True)
     inp = M.Input.synth(0, 20_000_000, 42, "bls12381")
+    say("input generated")
     pin = M.PinnedInput(inp.c)
     fl = rsio.flags("O2")
     g = M.Group(world)
@@ -208,7 +215,9 @@ def test_sharded_hosthost_bls12381_20m_world8():
         for r, e in enumerate(engs):
             e.join_group(g, r)
         outs = sharded_simplify(pin.c, fl, world, engs=engs)
+        say("sharded run done")
         ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
+        say("oracle done")
         for r, (got, st) in enumerate(outs):
             assert rsio.diff_output_arrays(got, ref) is None, f"rank {r}/{world}"
             assert st.world == world and st.exchange_bytes > 0
