@@ -233,6 +233,7 @@ struct rs_engine {
   void *sh_ent = nullptr;       // shared slot 0: col of a, b, c then val of a, b, c
   bool sh_full = false;         // the region was regrown at the end: the whole [early | late] is copied
   uint64_t sh_klo = 0, sh_khi = 0;  // this rank's run of the keep list (global output rows)
+  uint64_t lc_snap_n = 0, lc_snap_base = 0;  // lconst rows in the first early region, where their C part starts
   hipEvent_t ev_snap = nullptr, ev_snap0 = nullptr;  // early gather done / its inputs ready
   uint64_t snap_cap[3] = {0, 0, 0};   // capacity (entries) of the device and host early regions this run
   uint64_t snap_hint[3] = {0, 0, 0};  // the largest early region (both snapshots) of the runs so far
@@ -775,6 +776,9 @@ __host__ __device__ inline int snake_rank(uint64_t pos, int W) {
   uint64_t p = pos % (2 * (uint64_t)W);
   return p < (uint64_t)W ? (int)p : (int)(2 * (uint64_t)W - 1 - p);
 }
+__global__ void k_fill_u8_ids(const uint32_t *ids, uint64_t n, uint8_t v, uint8_t *out) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) out[ids[i]] = v;
+}
 // number of positions < n that rank r owns
 static uint64_t snake_count(uint64_t n, int W, int r) {
   uint64_t per = 2 * (uint64_t)W, k = n / per, rem = n % per;
@@ -1282,8 +1286,27 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
 // substitution log), every leftover -- in a pool made of every rank's packed entries.  Four
 // allgathervs of packed records and entries replace the round-1 design's zero-padded per-slot
 // sum-allreduce and whole-pool gather.
-static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D, const uint8_t *owner, Pool &P,
-                           const uint8_t *need) {
+// Replicated clusters (owner == W: the head, which every rank eliminates itself) are not exchanged
+// and keep their counts; the received records land in a pool of their own (G), since the head may
+// still be allocating from the local one.
+__global__ void k_zero_owned(const uint8_t *owner, int W, uint64_t n, uint32_t *n_sub, uint32_t *n_left) {
+  for (uint64_t c = gtid(); c < n; c += gstride())
+    if (owner[c] < W) {
+      n_sub[c] = 0;
+      n_left[c] = 0;
+    }
+}
+// shift the pool offsets of the replicated clusters' slots by `by` (their entries moved into G)
+__global__ void k_shift_owned(const uint32_t *cid, const uint8_t *owner, int W, uint64_t n_slots, uint64_t by, uint64_t *h_off,
+                              uint64_t *l_off) {
+  for (uint64_t s = gtid(); s < n_slots; s += gstride())
+    if (owner[cid[s]] == W) {
+      h_off[s] += by;
+      l_off[s] += by;
+    }
+}
+static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D, const uint8_t *owner, const Pool &P,
+                           const uint8_t *need, Pool &G) {
   Comm &CM = *E->comm;
   Arena &A = E->A;
   hipStream_t st = E->st;
@@ -1321,8 +1344,7 @@ static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D
   CM.allgatherv(lrec, gl, cl, st);
   CM.allgatherv(ek, gk, ck, st);
   CM.allgatherv(ev, gv, cv, st);
-  HC(hipMemsetAsync(a.n_sub, 0, 4 * n_cl, st));
-  HC(hipMemsetAsync(a.n_left, 0, 4 * n_cl, st));
+  launch(st, k_zero_owned, n_cl, owner, CM.world, n_cl, a.n_sub, a.n_left);
   uint64_t os = 0, ol = 0, oe = 0;
   for (int q = 0; q < CM.world; ++q) {
     if (ns[q] + nl[q])
@@ -1331,8 +1353,10 @@ static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D
     os += ns[q]; ol += nl[q]; oe += ne[q];
   }
   HC(hipStreamSynchronize(st));
-  P.pk = gk;
-  P.pv = gv;
+  G.pk = gk;
+  G.pv = gv;
+  G.top = nullptr;
+  G.cap = te;  // entries in use
   E->stats.exchange_ms += now_ms() - t0;
   E->stats.exchange_bytes += sizeof(XRec) * (ts + tl) + 36 * te + 24 * CM.world;
 }
@@ -1362,22 +1386,32 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   Comm *CM = E->comm.get();
   const int W = CM ? CM->world : 1, RK = CM ? CM->rank : 0;
   uint8_t *d_owner = nullptr;
+  // Sharded: the head -- the kHeadLimit largest clusters, the critical path no exchange can shorten --
+  // is eliminated by every rank (owner W, nothing exchanged); every other cluster belongs to one rank
+  // (snake order over the size-ordered lists) and reaches the others through the exchange, which runs
+  // as soon as the tail is done, while the head is still going.
+  const uint64_t n_rep = std::min<uint64_t>(n_big, kHeadLimit);
   if (W > 1 && eo.n_clusters) {
     d_owner = E->A.get<uint8_t>("sh.owner", eo.n_clusters);
-    if (n_big) launch(E->st, k_shard_owner, n_big, (const uint32_t *)d_big, n_big, W, d_owner);
+    const uint64_t n_tb = n_big - n_rep;
+    if (n_rep) launch(E->st, k_fill_u8_ids, n_rep, (const uint32_t *)d_big, n_rep, (uint8_t)W, d_owner);
+    if (n_tb) launch(E->st, k_shard_owner, n_tb, (const uint32_t *)(d_big + n_rep), n_tb, W, d_owner);
     if (n_small) launch(E->st, k_shard_owner, n_small, (const uint32_t *)d_small, n_small, W, d_owner);
-    const uint64_t nb = snake_count(n_big, W, RK), ns = snake_count(n_small, W, RK);
-    uint32_t *bb = E->A.get<uint32_t>("sh.big", nb), *ss = E->A.get<uint32_t>("sh.small", ns);
-    if (nb) launch(E->st, k_shard_pick, nb, (const uint32_t *)d_big, nb, W, RK, bb);
+    const uint64_t nb = snake_count(n_tb, W, RK), ns = snake_count(n_small, W, RK);
+    uint32_t *bb = E->A.get<uint32_t>("sh.big", n_rep + nb), *ss = E->A.get<uint32_t>("sh.small", ns);
+    if (n_rep) HC(hipMemcpyAsync(bb, d_big, 4 * n_rep, hipMemcpyDeviceToDevice, E->st));
+    if (nb) launch(E->st, k_shard_pick, nb, (const uint32_t *)(d_big + n_rep), nb, W, RK, bb + n_rep);
     if (ns) launch(E->st, k_shard_pick, ns, (const uint32_t *)d_small, ns, W, RK, ss);
     d_big = bb;
     d_small = ss;
-    n_big = nb;
+    n_big = n_rep + nb;
     n_small = ns;
   }
   uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots)), E->pool_want);
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
+    Pool G{};  // sharded: every rank's exchanged entries (shard_exchange)
+    bool exchanged = false;
     HC(hipMemsetAsync(P.top, 0, 8, E->st));
     HC(hipMemsetAsync(d_err, 0, 4, E->st));
     ElimArgs a;
@@ -1548,7 +1582,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         hl.n_slots = n_slots;
         hl.h = E->h_lvl;
         hl.ev = E->ev_lvl;
-        if (overlap && W == 1) hl.run(std::min(kHeadGpuLevels, kHeadLevels), false);
+        if (overlap) hl.run(std::min(kHeadGpuLevels, kHeadLevels), false);
       }
       HC(hipEventRecord(E->ev7, E->st));
       if (D.join_pending) {  // the main stream reads the head clusters' orders from here on
@@ -1571,7 +1605,23 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         if (g_prof_env) fprintf(stderr, "[rs-prof] head composition: %u level launches\n", hl.levels);
       };
       if (n_head) finish_head();
-      if (n_head && overlap && W == 1) (*overlap)(d_big, n_head, a);
+      // sharded: the clusters this rank owns are done (the main stream is past the tail): the exchange,
+      // while the head -- every rank's own -- is still being eliminated
+      if (W > 1) {
+        int e0 = 0;
+        HC(hipMemcpyAsync(&e0, d_err, 4, hipMemcpyDeviceToHost, E->st));
+        HC(hipStreamSynchronize(E->st));
+        exchanged = CM->max_u64((uint32_t)e0, E->st) == 0;  // else the attempt fails below, every rank alike
+        if (exchanged) shard_exchange(E, a, D, d_owner, P, need, G);
+      }
+      if (n_head && overlap && (W == 1 || exchanged)) {
+        ElimArgs ao = a;  // the frames read the substitutions of the clusters done: the gathered pool
+        if (W > 1) {
+          ao.pk = G.pk;
+          ao.pv = G.pv;
+        }
+        (*overlap)(d_big, n_head, ao);
+      }
       if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[4], 0));
       HC(hipEventRecord(E->ev3, E->st));
     }
@@ -1607,7 +1657,25 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
     E->pool_want = std::max(E->pool_want, want);  // the next run starts from a size that fitted
-    if (W > 1 && eo.n_clusters) shard_exchange(E, a, D, d_owner, P, need);
+    if (W > 1 && eo.n_clusters) {
+      // the head's entries (this rank's local pool, with its own share's) go behind the gathered ones;
+      // the replicated clusters' slots follow them, and the gathered pool is the round's pool from here
+      unsigned long long top = 0;
+      HC(hipMemcpyAsync(&top, P.top, 8, hipMemcpyDeviceToHost, E->st));
+      HC(hipStreamSynchronize(E->st));
+      const uint64_t base = G.cap;
+      E->A.grow_keep<uint32_t>("pool.gk", base + top + 1, base, E->st, E->st);
+      E->A.grow_keep<Fe>("pool.gv", base + top + 1, base, E->st, E->st);
+      uint32_t *gk = E->A.get<uint32_t>("pool.gk", 1);
+      Fe *gv = E->A.get<Fe>("pool.gv", 1);
+      if (top) {
+        HC(hipMemcpyAsync(gk + base, P.pk, 4 * top, hipMemcpyDeviceToDevice, E->st));
+        HC(hipMemcpyAsync(gv + base, P.pv, 32 * top, hipMemcpyDeviceToDevice, E->st));
+      }
+      launch(E->st, k_shift_owned, n_slots, (const uint32_t *)D.cid, (const uint8_t *)d_owner, W, n_slots, base, a.h_off, a.l_off);
+      P.pk = gk;
+      P.pv = gv;
+    }
     if (eo.n_clusters) {
       float ms = 0;
       unsigned long long by = 0;
@@ -1773,10 +1841,11 @@ struct LcHeap {
     uint64_t *cnt = A.get<uint64_t>("lc.cnt", m), *pos = A.get<uint64_t>("lc.pos", m);
     launch(st, k_lc_count, m, src, ids, m, cnt);
     const uint64_t tot = excl_scan_u64(E, cnt, pos, m, "lc");
-    A.grow_keep<uint64_t>("lc.off", n + m, n, st, st);
-    A.grow_keep<uint32_t>("lc.len", n + m, n, st, st);
-    A.grow_keep<uint32_t>("lc.key", top + tot, top, st, st);
-    A.grow_keep<Fe>("lc.val", top + tot, top, st, st);
+    // (a move waits for the copy stream too: a snapshot may be reading the heap there)
+    A.grow_keep<uint64_t>("lc.off", n + m, n, E->stc, st);
+    A.grow_keep<uint32_t>("lc.len", n + m, n, E->stc, st);
+    A.grow_keep<uint32_t>("lc.key", top + tot, top, E->stc, st);
+    A.grow_keep<Fe>("lc.val", top + tot, top, E->stc, st);
     launch(st, k_lc_copy, m, src, ids, m, (const uint64_t *)pos, top, n, view(A));
     n += m;
     top += tot;
@@ -2071,6 +2140,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   LcHeap lc;  // lconst (device)
   snap_join(E);
   E->snap_on = false;
+  E->lc_snap_n = 0;
   E->csr_ready = false;
   E->log_on = fl->emit_substitution_log != 0;
   E->log_from.clear();
@@ -2449,7 +2519,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     const bool shard = CM && CM->world > 1;
     launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, shard ? E->nl_lo : (uint64_t)0, shard ? E->nl_hi : n_nl, so_early, elen);
     const U3 et = excl_scan_u3(E, elen, so_eoff, n_nl, "so");
-    const uint64_t ev[3] = {et.a, et.b, et.c};
+    // single engine: the lconst rows so far (final as they enter the heap) go behind the C part
+    E->lc_snap_n = shard ? 0 : lc.n;
+    E->lc_snap_base = et.c;
+    const uint64_t lc_e = shard ? 0 : lc.top;
+    const uint64_t ev[3] = {et.a, et.b, et.c + lc_e};
     E->sh_full = false;
     if (shard) {  // every rank's share of each part gets the same capacity in the shared region
       for (int q = 0; q < 3; ++q) E->sh_cap[q] = CM->max_u64(std::max<uint64_t>(ev[q] + ev[q] / 4 + 65536, E->sh_cap[q]), st);
@@ -2480,6 +2554,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
       if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
                         (const uint64_t *)nullptr);
+      if (q == 2 && lc_e) {
+        const DRows lcv = lc.view(A);
+        launch(E->stc, k_lc_snap, lc_e, E->F, (const uint32_t *)lcv.key, (const Fe *)lcv.val, lc_e, col + et.c, val + 4 * et.c);
+      }
       void *hc = shard ? (void *)(sh_col(E, q) + CM->rank * E->sh_cap[q]) : pin_get(E, 3 + q, 4 * cap);
       void *hv = shard ? (void *)(sh_val(E, q) + 4 * CM->rank * E->sh_cap[q]) : pin_get(E, 6 + q, 32 * cap);
       E->snap_cap[q] = cap;
@@ -2629,7 +2707,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     E->stats.apply_kernel_ms += ms;
   };
   // rows that touch none of the largest clusters go through the frames while those clusters are
-  // still being eliminated (single rank: a sharded run learns the substitutions at the exchange)
+  // still being eliminated (sharded: after the exchange of the clusters other than the head, which every
+  // rank eliminates itself)
   bool nl_split = false;
   HeadOverlap overlap = [&](const uint32_t *ids, uint64_t n_head, const ElimArgs &ea) {
     hmark = A.get<uint8_t>("nl.hmark", E->S);
@@ -2663,7 +2742,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     }
     if (E->comm && E->comm->world > 1) load_order_collectives(E);
     run_linear_simplification(E, lin, fl->use_old_heuristics, eo, P, d_err, d_forb, sub_of, d_deleted,
-                              n_nl && !E->comm ? &overlap : nullptr, keys_first ? &linear_values : nullptr, relevant);
+                              n_nl ? &overlap : nullptr, keys_first ? &linear_values : nullptr, relevant);
     if (E->log_on) log_linear_round(E, eo, P);
     collect_leftovers(E, eo, P, lc);
     E->stats.rounds++;
@@ -3305,8 +3384,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint64_t *lptr = A.get<uint64_t>(std::string(nm[q]) + ".lptr", m_loc + 1);
       if (own) launch(st, k_out_late_lens, own, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
                       (const uint8_t *)so_dirty, late);
-      for (int x = 0; x < 2; ++x)
-        if (xl_n[x]) launch(st, k_row_lens, xl_n[x], xq[x], (const uint32_t *)x_ids[x], xl_n[x], late + xl_at[x]);
+      if (xl_n[0]) launch(st, k_row_lens, xl_n[0], xq[0], (const uint32_t *)x_ids[0], xl_n[0], late + xl_at[0]);
+      if (xl_n[1]) launch(st, k_lc_late_lens, xl_n[1], xq[1], (const uint32_t *)x_ids[1], xl_n[1], E->lc_snap_n, late + xl_at[1]);
       HC(hipMemsetAsync(late + m_loc, 0, 8, st));
       const uint64_t L = excl_scan_u64(E, late, lptr, m_loc + 1, "late");
       const uint64_t base = E->snap_e[q], ext = base + L;
@@ -3319,10 +3398,12 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       }
       if (own) launch(st, k_out_extent, own, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
                       (const uint8_t *)so_dirty, (const U3 *)so_eoff, q, base, (const uint64_t *)lptr, beg, end);
-      for (int x = 0; x < 2; ++x)
-        if (xl_n[x])
-          launch(st, k_out_extent, xl_n[x], xq[x], (const uint32_t *)x_ids[x], xl_n[x], (const uint32_t *)nullptr, (const uint8_t *)nullptr,
-                 (const uint8_t *)nullptr, (const U3 *)nullptr, q, base, (const uint64_t *)(lptr + xl_at[x]), beg + xl_at[x], end + xl_at[x]);
+      if (xl_n[0])
+        launch(st, k_out_extent, xl_n[0], xq[0], (const uint32_t *)x_ids[0], xl_n[0], (const uint32_t *)nullptr, (const uint8_t *)nullptr,
+               (const uint8_t *)nullptr, (const U3 *)nullptr, q, base, (const uint64_t *)(lptr + xl_at[0]), beg + xl_at[0], end + xl_at[0]);
+      if (xl_n[1])
+        launch(st, k_lc_extent, xl_n[1], xq[1], (const uint32_t *)x_ids[1], xl_n[1], E->lc_snap_n, E->lc_snap_base, q, base,
+               (const uint64_t *)(lptr + xl_at[1]), beg + xl_at[1], end + xl_at[1]);
       launch(st, k_set_u64, 1, beg + m_loc, ext);
       // the device copy of the whole layout grows past the early region when it must (the
       // early region is copied along once its gather is done)
@@ -3334,10 +3415,12 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint64_t *val = A.get<uint64_t>(xv, 4 * ext);
       if (own) launch(st, k_gather_late, own, E->F, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
                       (const uint8_t *)so_dirty, (const uint64_t *)lptr, col + base, val + 4 * base);
-      for (int x = 0; x < 2; ++x)
-        if (xl_n[x])
-          launch(st, k_gather_late, xl_n[x], E->F, xq[x], (const uint32_t *)x_ids[x], xl_n[x], (const uint32_t *)nullptr,
-                 (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + xl_at[x]), col + base, val + 4 * base);
+      if (xl_n[0])
+        launch(st, k_gather_late, xl_n[0], E->F, xq[0], (const uint32_t *)x_ids[0], xl_n[0], (const uint32_t *)nullptr,
+               (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + xl_at[0]), col + base, val + 4 * base);
+      if (xl_n[1])
+        launch(st, k_lc_gather_late, xl_n[1], E->F, xq[1], (const uint32_t *)x_ids[1], xl_n[1], E->lc_snap_n,
+               (const uint64_t *)(lptr + xl_at[1]), col + base, val + 4 * base);
     }
     if (shard) {  // a share past its capacity: the region regrows and every rank copies its whole layout
       uint64_t over = 0;

@@ -132,6 +132,52 @@ __global__ void k_out_extent(DRows R, const uint32_t *ids, uint64_t n, const uin
   }
 }
 
+// lconst rows [0, n_snap) went with the first early region (their C entries at c_base + their heap
+// offset, in heap order: fix_constraint is applied as they enter the heap, so they are final there);
+// the rest -- a later round's leftovers -- are late rows like any other
+__global__ void k_lc_late_lens(DRows R, const uint32_t *ids, uint64_t n, uint64_t n_snap, uint64_t *late) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t r = ids[i];
+    late[i] = r < n_snap ? 0 : R.len[r];
+  }
+}
+__global__ void k_lc_extent(DRows R, const uint32_t *ids, uint64_t n, uint64_t n_snap, uint64_t c_base, int q, uint64_t base,
+                            const uint64_t *lptr, uint64_t *beg, uint64_t *end) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t r = ids[i];
+    const uint64_t b = r < n_snap && q == 2 ? c_base + R.off[r] : base + lptr[i];
+    beg[i] = b;
+    end[i] = b + R.len[r];
+  }
+}
+__global__ void k_lc_gather_late(FieldP F, DRows R, const uint32_t *ids, uint64_t n, uint64_t n_snap, const uint64_t *lptr,
+                                 uint32_t *col, uint64_t *val) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const uint32_t r = ids[i];
+    if (r < n_snap) continue;
+    const uint64_t o = lptr[i], s = R.off[r];
+    for (uint32_t t = 0; t < R.len[r]; ++t) {
+      col[o + t] = R.key[s + t];
+      const Fe c = ffrom_mont(F, R.val[s + t]);
+      val[4 * (o + t) + 0] = c.l[0];
+      val[4 * (o + t) + 1] = c.l[1];
+      val[4 * (o + t) + 2] = c.l[2];
+      val[4 * (o + t) + 3] = c.l[3];
+    }
+  }
+}
+// the lconst heap's entries [0, n), canonical, behind the storage rows' C part of the early region
+__global__ void k_lc_snap(FieldP F, const uint32_t *key, const Fe *v, uint64_t n, uint32_t *col, uint64_t *val) {
+  for (uint64_t t = gtid(); t < n; t += gstride()) {
+    col[t] = key[t];
+    const Fe c = ffrom_mont(F, v[t]);
+    val[4 * t + 0] = c.l[0];
+    val[4 * t + 1] = c.l[1];
+    val[4 * t + 2] = c.l[2];
+    val[4 * t + 3] = c.l[3];
+  }
+}
+
 // the late rows, canonical, at lptr[i] of the late region
 __global__ void k_gather_late(FieldP F, DRows R, const uint32_t *ids, uint64_t n, const uint32_t *nl_of, const uint8_t *early,
                               const uint8_t *dirty, const uint64_t *lptr, uint32_t *col, uint64_t *val) {

@@ -145,22 +145,22 @@ typedef struct rs_stats {
   double elim_ms;              /* per-cluster elimination + normalisation + composition      */
   double subst_ms;             /* substitution application (non-linear rows, rounds >= 2)    */
   double final_ms;             /* compaction, rebuild_witness, output assembly               */
-  double apply_kernel_ms;      /* device time of the non-linear substitution kernel (k_nl_fill) */
+  double apply_kernel_ms;      /* device time of the non-linear frames passes (k_frames_wave<0>) */
   uint64_t apply_kernel_launches;
   uint64_t apply_bytes;        /* its algorithmic bytes (sum over launches)                  */
-  double elim_kernel_ms;       /* device time of the per-cluster elimination (k_eliminate)   */
+  double elim_kernel_ms;       /* device time of the per-cluster elimination (every kernel)  */
   uint64_t elim_kernel_launches;
   uint64_t elim_bytes;         /* its algorithmic bytes (sum over launches)                  */
-  double elim_big_ms;          /* device time of the large-cluster kernel (k_eliminate_big)  */
-  double elim_small_ms;        /* device time of the small-cluster kernel                    */
+  double elim_big_ms;          /* device time of the workgroup kernels (head + tail streams)  */
+  double elim_small_ms;        /* device time of the small-cluster kernel (k_eliminate)      */
   double nl_ms;                /* non-linear frames (count, scan, fill, split)               */
   double map_ms;               /* host copy of the non-linear signal map (rounds >= 2)       */
   double rounds_ms;            /* storage updates + bookkeeping of rounds >= 2               */
-  double big_prep_ms;          /* k_big_prep   (occurrences + uniques of the workgroup clusters) */
-  double big_main_ms;          /* k_big_main   (ordered elimination loop)                     */
-  double big_finish_ms;        /* k_big_finish (normalisation + composition)                 */
-  uint64_t big_main_bytes;     /* algorithmic bytes of k_big_main (sum over launches)        */
-  uint64_t big_finish_bytes;   /* algorithmic bytes of k_big_finish (sum over launches)      */
+  double big_prep_ms;          /* k_wide_* + k_big_prep (occurrences + uniques)              */
+  double big_main_ms;          /* the ordered elimination loops (k_big_spec<8> + k_big_main<256>) */
+  double big_finish_ms;        /* normalisation + composition (k_batch_inv_*, k_big_finish, levels) */
+  uint64_t big_main_bytes;     /* algorithmic bytes of the ordered loops (sum over launches)  */
+  uint64_t big_finish_bytes;   /* algorithmic bytes of normalisation + composition           */
   uint64_t big_launches;       /* launches of each of the three workgroup kernels            */
   uint64_t rounds;             /* linear-elimination rounds executed                         */
   uint64_t n_clusters;
@@ -173,13 +173,13 @@ typedef struct rs_stats {
    * on the second stream, the critical path) and the tail (every other workgroup cluster), each
    * with its own HIP-event time and in-kernel algorithmic bytes; the storage-row kernel of
    * rounds >= 2; the host -> host legs of rs_engine_simplify. */
-  double head_main_ms;         /* k_big_main<512> (head)                                     */
+  double head_main_ms;         /* k_big_spec<8> (head: the 48 largest clusters)              */
   uint64_t head_main_bytes;
   uint64_t head_launches;
   double tail_main_ms;         /* k_big_main<256> (tail)                                     */
   uint64_t tail_main_bytes;
   uint64_t tail_launches;
-  double round_fill_ms;        /* k_round_fill (apply_substitution_to_map, rounds >= 2)      */
+  double round_fill_ms;        /* k_frames_wave<1> + k_round_fill (apply_substitution_to_map) */
   uint64_t round_fill_bytes;
   uint64_t round_fill_launches;
   uint64_t alg_bytes;          /* B_alg of the run: every in-kernel counter +

@@ -126,18 +126,35 @@ def test_hosthost_streamed_layout(kind, rows, prime):
     inp = M.Input.synth(kind, rows, 5, prime)
     pin = M.PinnedInput(inp.c)
     fl = rsio.flags("O2")
-    o = engine().simplify(pin.c, fl)
-    got = rsio.output_arrays(o)
-    n = int(o.n_constraints)
-    for q in range(3):
-        lc, end = o.block(q)
-        assert end is not None, "a run with storage rows streams"
-        beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,))
-        e = np.ctypeslib.as_array(end, shape=(n,))
-        assert (beg[:n] <= e).all() and (e <= int(lc.nnz)).all() and int(beg[n]) == int(lc.nnz)
     ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
-    assert rsio.diff_output_arrays(got, ref) is None
+    # three calls: the first sizes the early regions, the later ones take every snapshot (the head rows'
+    # pass, each round's rewritten rows, the lconst rows) into them
+    for _ in range(3):
+        o = engine().simplify(pin.c, fl)
+        got = rsio.output_arrays(o)
+        n = int(o.n_constraints)
+        for q in range(3):
+            lc, end = o.block(q)
+            assert end is not None, "a run with storage rows streams"
+            beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,))
+            e = np.ctypeslib.as_array(end, shape=(n,))
+            assert (beg[:n] <= e).all() and (e <= int(lc.nnz)).all() and int(beg[n]) == int(lc.nnz)
+        assert rsio.diff_output_arrays(got, ref) is None
     out = engine().fetch()
     assert not out.c.a_end and not out.c.b_end and not out.c.c_end
     assert rsio.diff_output_arrays(rsio.output_arrays(out.c), ref) is None
+    pin.free()
+
+
+@pytest.mark.parametrize("level,rounds", [("O1", None), ("O2", 1), ("O2", 2)])
+def test_hosthost_streamed_levels(level, rounds):
+    """The streamed result at --O1 (every linear row joins lconst and goes with the first early region)
+    and at --O2round 1 / 2 (truncated rounds leave the linear tail late), repeated on one engine."""
+    inp = M.Input.synth(0, 500_000, 8, "bn128")
+    pin = M.PinnedInput(inp.c)
+    fl = rsio.flags(level, rounds)
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
+    for _ in range(3):
+        got = rsio.output_arrays(engine().simplify(pin.c, fl))
+        assert rsio.diff_output_arrays(got, ref) is None
     pin.free()

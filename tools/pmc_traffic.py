@@ -52,13 +52,18 @@ def main():
     ap.add_argument("--wrreq", default=None)
     ap.add_argument("--steps", type=int, default=1, help="bench steps of each pass (warmup 0)")
     ap.add_argument("--commit", default=None, help="git commit the profiled tree was at")
+    ap.add_argument("--calib", default=None, help="profiles/roundN_pmc_calib.json (tools/pmc_calib.py): bytes moved "
+                    "from the counters with the factors of the gather / emit patterns instead of FETCH_SIZE x2")
+    ap.add_argument("--bench", default="bench.py --steps K --warmup 0 --no-cpu", help="what the passes ran (for the record)")
     args = ap.parse_args()
     fe = per_dispatch(args.fetch_dir, "FETCH_SIZE")
     wr = per_dispatch(args.write_dir, "WRITE_SIZE")
     req = per_dispatch(args.wrreq, "TCC_EA0_WRREQ_sum") if args.wrreq else {}
     req64 = per_dispatch(args.wrreq, "TCC_EA0_WRREQ_64B_sum") if args.wrreq else {}
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of "
-                     "`bench.py --steps 1 --warmup 0 --no-cpu`; FETCH_SIZE x2 (gfx950), KiB -> bytes",
+    cal = json.load(open(args.calib)) if args.calib else None
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of `{args.bench}`; "
+                     "FETCH_SIZE x2 (gfx950), KiB -> bytes" + ("; calibrated: FETCH_SIZE / fetch_factor[k_runs36] + "
+                                                             "WRITE_SIZE / write_factor[k_emit36] from " + args.calib if cal else ""),
            "commit": args.commit, "steps": args.steps,
            "bytes_per_launch": {}, "bytes_per_step": {}, "launches_per_step": {}, "detail": {}}
     for name, pats in GROUPS.items():
@@ -76,10 +81,14 @@ def main():
                 w += wx * nwx / nw
         fetch = 2.0 * f * 1024.0
         write = w * 1024.0
+        if cal:  # the gather pattern's read factor, the consecutive-slot write pattern's write factor
+            fetch = f * 1024.0 / cal["fetch_factor"]["k_runs36"]
+            write = w * 1024.0 / cal["write_factor"]["k_emit36"]
         res["bytes_per_launch"][name] = int(fetch + write)
         res["bytes_per_step"][name] = int((fetch + write) * nf / args.steps)
         res["launches_per_step"][name] = nf / args.steps
-        det = {"fetch_bytes_x2": int(fetch), "write_bytes": int(write), "dispatches": [nf, nw]}
+        det = {"fetch_bytes_x2": int(2.0 * f * 1024.0), "write_bytes_raw": int(w * 1024.0), "fetch_bytes": int(fetch),
+               "write_bytes": int(write), "dispatches": [nf, nw]}
         r, _ = group_avg(req, pat)
         r64, _ = group_avg(req64, pat)
         if r is not None and r64 is not None:
