@@ -1053,10 +1053,12 @@ struct LevelLoop {
 // Kahn levels of the head's composition launched over the whole GPU before k_compose_rest takes the
 // rest per cluster in one workgroup each (level 0's items need no composition)
 constexpr uint32_t kHeadGpuLevels = 8;
-// the number of largest clusters eliminated on the second stream by the speculative loop: the next
-// size class (1,100-1,700 rows on the metric circuit) took 7-8 ms each in the tail's one-wave loop,
-// which held the first frames pass -- and so the result stream -- back until the tail was done
-constexpr uint64_t kHeadLimit = 48;
+// the number of largest clusters eliminated on the second stream by the speculative loop: the tail's
+// one-wave loop is bound by its largest clusters (~4.5 us a row), which hold the first frames pass --
+// and so the result stream -- back until the tail is done.  On the metric circuit (host -> host,
+// best of 5): 48 -> tail loop 7.7 ms, 52.0 ms; 96 -> 5.1 ms, 49.7 ms; 160 -> 5.0 ms, 49.6 ms (device
+// time 39.8 / 37.7 / 39.1 ms: the head grows with its cluster count)
+constexpr uint64_t kHeadLimit = 96;
 // The arena replay of one cluster on the host (k_cl_replay_lane's walk): rows in index order, each
 // pair's previous row found by path halving and its root's list appended to the row's.  A serial
 // union-find of dependent accesses: ~20 ns a pair in a host cache against ~0.3 us in LDS, and the
@@ -2014,7 +2016,11 @@ static void snap_join(rs_engine *E) {
   if (E->snap_thread.joinable()) E->snap_thread.join();
   E->snap_q.clear();
 }
+static void snap_start(rs_engine *E);
+// queues a job, starting the thread when none runs (a run whose first snapshot was empty takes its
+// first rows at a later one)
 static void snap_push(rs_engine *E, const rs_engine::SnapJob &j) {
+  snap_start(E);
   {
     std::lock_guard<std::mutex> lk(E->snap_m);
     E->snap_q.push_back(j);
@@ -2565,7 +2571,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       E->snap_host[2 * q + 1] = hv;
       if (ev[q]) {  // a part's copies start once its own gather is done
         HC(hipEventRecord(E->ev_snapq[q], E->stc));
-        snap_start(E);
         snap_push(E, {hc, col, 4 * ev[q], E->ev_snapq[q]});
         snap_push(E, {hv, val, 32 * ev[q], E->ev_snapq[q]});
       }

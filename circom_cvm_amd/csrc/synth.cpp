@@ -19,6 +19,8 @@
 //  kind 4  sha (config 1 stand-in): sha256 compression gadgets (XOR3, Ch, Maj, BinSum, Num2Bits).
 //  kind 5  templated (config 5 as SURVEY 8(d) words it): 64-row template instances replicated with
 //          signal offsets, wired into chains of log-normal length (see gen_templated).
+//  kind 6  templated with the 2e5 tail: kind 5 whose first chain has 9,000 instances (one ~2e5-row
+//          linear cluster), so one workload has both the replication and the tail of config 5.
 //
 // Coefficients: 60% from {1, p-1, 2^k}, 40% uniform in [1, p) (splitmix64 stream).
 #include <algorithm>
@@ -669,7 +671,9 @@ static void gen_sha(Gen &g, uint64_t R, uint32_t n_pub) {
 // signals from earlier ones (a DAG, 2-4 terms), the quadratic rows multiply defined signals (one in
 // 25 with a constant selector in A: those rows turn linear and feed round 2), the equalities
 // alias defined signals for the quadratic rows.
-static void gen_templated(Gen &g, uint64_t R, uint32_t n_pub) {
+// tail (kind 6): the first chain has 9,000 instances -- one cluster of ~2e5 linear rows, the tail
+// SURVEY 8(d) config 5 names -- and the rest follow the log-normal lengths above.
+static void gen_templated(Gen &g, uint64_t R, uint32_t n_pub, bool tail) {
   // templates, interface, locals per instance (1-4 inputs, 5-46 definitions, 47-61 aliases, 63-65
   // selectors)
   constexpr uint32_t kT = 16, kIn = 4, kOut = 4, kL = 66;
@@ -760,6 +764,7 @@ static void gen_templated(Gen &g, uint64_t R, uint32_t n_pub) {
     double z = std::sqrt(-2.0 * std::log(std::max(g.rng.uni(), 1e-300))) * std::cos(6.283185307179586 * g.rng.uni());
     uint64_t len = (uint64_t)std::llround(2.0 * std::exp(1.3 * z));
     len = std::max<uint64_t>(1, std::min<uint64_t>(len, 9000));
+    if (tail && made == 0) len = 9000;
     uint32_t prev = 0;  // base of the previous instance of the chain (0: none)
     for (uint64_t k = 0; k < len && made < R; ++k) {
       const std::vector<LRow> &T = tpl[g.rng.below(kT)];
@@ -809,7 +814,7 @@ using namespace rs;
 
 extern "C" int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id,
                         rs_input **out) {
-  if (prime_id >= 8 || kind > 5) { set_error("rs_synth: bad kind/prime"); return RS_E_INVALID; }
+  if (prime_id >= 8 || kind > 6) { set_error("rs_synth: bad kind/prime"); return RS_E_INVALID; }
   Gen g;
   g.rng.s = seed;
   memcpy(g.p, kPrimes[prime_id], 32);
@@ -821,7 +826,7 @@ extern "C" int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t pr
   else if (kind == 2) gen_chain(g, rows, n_pub);
   else if (kind == 3) gen_poseidon(g, rows, n_pub);
   else if (kind == 4) gen_sha(g, rows, n_pub);
-  else gen_templated(g, rows, n_pub);
+  else gen_templated(g, rows, n_pub, kind == 6);
   rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
   in->prime_id = prime_id;
   memcpy(in->prime, g.p, 32);

@@ -285,7 +285,8 @@ int rs_write_substitution_json(const char *path, const rs_output *out);
  * kind: 0 = mixed (metric circuit, BASELINE configs[4]), 1 = purely linear (configs[1]), 2 = chain
  * (configs[3] ECDSA stand-in: deep composition, 8 rounds), 3 = Poseidon(16) Merkle (configs[2]),
  * 4 = sha256-like bit gadgets (configs[0]), 5 = templated (64-row template instances replicated with
- * signal offsets, wired into chains; SURVEY 8(d) config 5's replication). */
+ * signal offsets, wired into chains; SURVEY 8(d) config 5's replication), 6 = templated whose first
+ * chain has 9,000 instances (one ~2e5-row linear cluster: config 5's replication and its tail). */
 int rs_synth(uint32_t kind, uint64_t rows, uint64_t seed, uint32_t prime_id, rs_input **in);
 
 /* ---- the DAG -> constraint-list flattening that produces rs_input.

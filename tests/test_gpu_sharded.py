@@ -193,18 +193,17 @@ def test_sharded_hosthost_synth_arrays(kind, rows, world):
         assert st.world == world
 
 
-def test_sharded_hosthost_bls12381_20m_world8():
-    """BASELINE configs[4] at its stated size: --prime bls12381, the 20 M-row mixed circuit, ONE circuit
-    over 8 ranks host -> host (split upload, sharded elimination with the exchange, split result
-    copy), every rank array for array equal to the single-GPU oracle.  In one process on one GPU
-    (8 engines), so the group is made for this test and closed after it."""
+def _run_20m_world8():
+    """The body of test_sharded_hosthost_bls12381_20m_world8, run in a child process (python
+    tests/test_gpu_sharded.py 20m): its 8 engines each hold the whole 20 M-row problem, which leaves no
+    room for the engines the earlier tests of this process keep."""
     import sys
     import time
     world = 8
     t0 = time.time()
 
-    def say(what):  # progress past the output capture (a quiet minute reads as a hang on the GPU box)
-        print(f"[20M world 8] {what} at {time.time() - t0:.0f} s", file=sys.__stderr__, flush=True)
+    def say(what):  # progress (a quiet minute reads as a hang on the GPU box)
+        print(f"[20M world 8] {what} at {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     inp = M.Input.synth(0, 20_000_000, 42, "bls12381")
     say("input generated")
     pin = M.PinnedInput(inp.c)
@@ -225,3 +224,23 @@ def test_sharded_hosthost_bls12381_20m_world8():
         for e in engs:
             e.close()
         pin.free()
+    say("arrays equal on every rank")
+
+
+def test_sharded_hosthost_bls12381_20m_world8():
+    """BASELINE configs[4] at its stated size: --prime bls12381, the 20 M-row mixed circuit, ONE circuit
+    over 8 ranks host -> host (split upload, sharded elimination with the exchange, split result
+    copy), every rank array for array equal to the single-GPU oracle.  In one child process on one GPU
+    (8 engines and an in-process group made for it)."""
+    import os
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "20m"], stdout=sys.__stderr__, stderr=sys.__stderr__,
+                       timeout=280, cwd=os.path.dirname(os.path.abspath(__file__)))
+    assert r.returncode == 0, f"child exited with {r.returncode}"
+
+
+if __name__ == "__main__":
+    import sys
+    if sys.argv[1:] == ["20m"]:
+        _run_20m_world8()

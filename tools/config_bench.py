@@ -20,6 +20,7 @@ CONFIGS = {  # name: (kind, rows, seed, prime)
     "mixed10M": (0, 10_000_000, 42, "bn128"),
     "bls20M": (0, 20_000_000, 42, "bls12381"),
     "templated10M": (5, 10_000_000, 42, "bn128"),
+    "templated_tail10M": (6, 10_000_000, 42, "bn128"),
 }
 
 ap = argparse.ArgumentParser()
