@@ -2035,6 +2035,7 @@ static void snap_start(rs_engine *E) {
     constexpr size_t chunk = 16ull << 20;
     if (hipSetDevice(E->device) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
     int k = 0;
+    double prof_ms = 0.0, prof_b = 0.0;
     for (;;) {
       rs_engine::SnapJob j;
       {
@@ -2047,6 +2048,7 @@ static void snap_start(rs_engine *E) {
       if (E->snap_rc) continue;
       // (an event a later snapshot records again is waited for at its newer point: still after this gather)
       if (hipEventSynchronize(j.ready) != hipSuccess) { E->snap_rc = RS_E_HIP; continue; }
+      const double tj = g_prof_env ? now_ms() : 0.0;
       for (size_t o = 0; o < j.bytes; o += chunk, ++k) {
         const size_t n = std::min(chunk, j.bytes - o);
         if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
@@ -2056,8 +2058,16 @@ static void snap_start(rs_engine *E) {
           break;
         }
       }
+      if (g_prof_env) {  // RS_PROF: the link's rate while this job copies (the job is waited for)
+        if (hipStreamSynchronize(E->stx) != hipSuccess) E->snap_rc = RS_E_HIP;
+        prof_ms += now_ms() - tj;
+        prof_b += j.bytes;
+      }
     }
     if (hipStreamSynchronize(E->stx) != hipSuccess) E->snap_rc = RS_E_HIP;
+    if (g_prof_env && prof_b)
+      fprintf(stderr, "[rs-prof] result stream: %.1f MB in %.2f ms of copying (%.1f GB/s)\n", prof_b / 1e6, prof_ms,
+              prof_b / 1e6 / prof_ms);
   });
 }
 
@@ -2841,7 +2851,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     // the earlier snapshots' gathers read the early flags / offsets this one rewrites, and its own buffers
     HC(hipStreamWaitEvent(st, E->ev_snap, 0));
     U3 *elen = A.get<U3>("so.rlen", n_st), *eoff3 = A.get<U3>("so.roff", n_st);
-    launch(st, k_snap_lens_round, n_st, pa, pb, pc, touched, turn, n_st, elen);
+    launch(st, k_snap_lens_round, n_st, pa, pb, pc, touched, turn, (const uint32_t *)st_ids, (const uint8_t *)so_early, n_st, elen);
     const U3 et = excl_scan_u3(E, elen, eoff3, n_st, "sor");
     const uint64_t e3[3] = {et.a, et.b, et.c};
     if (!(e3[0] | e3[1] | e3[2])) return;
@@ -3687,7 +3697,13 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
   o->n_labels = E->S;
   o->label_to_wire = (int32_t *)buf(9, 4 * E->S);
   HC(hipMemcpyAsync(o->label_to_wire, E->A.get<int32_t>("fin.l2w", 1), 4 * E->S, hipMemcpyDeviceToHost, E->st));
+  const double tf0 = g_prof_env ? now_ms() : 0.0;
   HC(hipStreamSynchronize(E->st));
+  if (g_prof_env && streamed) {
+    double late = 4.0 * E->S;
+    for (int q = 0; q < 3; ++q) late += 16.0 * nd + 8.0 + 36.0 * (E->out_ext[q] - E->snap_e[q]);
+    fprintf(stderr, "[rs-prof] fetch: row extents, late rows and label_to_wire %.1f MB, waited %.2f ms\n", late / 1e6, now_ms() - tf0);
+  }
   if (streamed) {
     snap_join(E);
     if (E->snap_rc) throw RsError(RS_E_HIP, "D2H of the streamed rows failed");

@@ -96,6 +96,7 @@ struct FwLds {
   uint32_t e_key[kFwE];     // plain: the signal after frame 1; constant: that signal; substituted: slot
   uint8_t e_kind[kFwE];     // bits 0-3: kind (fw_operands); 4-5: the part a fix-pass entry reads
   uint8_t e_grp[kFwE];
+  uint16_t e_pos[kFwE];     // the entry's position in its group's input row
   uint64_t e_aux[kFwE];     // substituted: pool offset of the right-hand side
   uint16_t g_e0[kFwG + 1];  // group -> first entry / term
   uint16_t g_t0[kFwG + 1];
@@ -144,7 +145,8 @@ __device__ __forceinline__ uint32_t fw_find(const uint16_t *a, uint32_t n, uint3
 }
 
 // Entry kinds (e_kind bits 0-3; bits 4-5: the part the entry reads, for kinds 3 and 4):
-//   0 plain      value = coefficient                               (input row of the group's part)
+//   0 plain      value = coefficient                               (input row of the group's part;
+//                in rounds a block of consecutive plain entries: term j = input entry e_pos + j)
 //   1 constant   value = coefficient * constant value, key 0       (frame 2)
 //   2 substitute value = coefficient * right-hand side entry j     (frame 3, pool at e_aux)
 //   3 copy       value = written output entry j                    (fix pass: the final C)
@@ -154,7 +156,11 @@ __device__ __forceinline__ uint32_t fw_epart(const FwLds &L, uint32_t e) { retur
 
 __device__ __forceinline__ uint32_t fw_term_key(const FrameWaveArgs &A, const FwLds &L, uint32_t e, uint32_t j) {
   const uint32_t kd = L.e_kind[e] & 15;
-  if (kd == 0) return L.e_key[e];
+  if (kd == 0) {
+    if (j == 0) return L.e_key[e];
+    const uint32_t g = L.e_grp[e];
+    return fw_ikey(A, fw_part(g))[L.g_in[g] + L.e_pos[e] + j];
+  }
   if (kd == 1) return 0u;
   if (kd == 2) return A.fr.pk[L.e_aux[e] + j];
   return fw_okey(A, fw_epart(L, e))[L.e_aux[e] + j];
@@ -163,7 +169,7 @@ __device__ __forceinline__ uint32_t fw_term_key(const FrameWaveArgs &A, const Fw
 __device__ __forceinline__ void fw_operands(const FrameWaveArgs &A, const FwLds &L, uint32_t e, uint32_t j, Fe &c, Fe &m) {
   const uint32_t kd = L.e_kind[e] & 15, g = L.e_grp[e];
   if (kd <= 2) {
-    c = fw_ival(A, fw_part(g))[L.g_in[g] + (e - L.g_e0[g])];
+    c = fw_ival(A, fw_part(g))[L.g_in[g] + L.e_pos[e] + (kd == 0 ? j : 0u)];
     if (kd == 1) m = A.fr.ce_val[L.e_key[e]];
     else if (kd == 2) m = A.fr.pv[L.e_aux[e] + j];
   } else {
@@ -519,7 +525,8 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
 #endif
   // ---- groups (lane = row)
   const uint32_t n0 = inb ? ln[0] : 0, n1 = inb ? ln[1] : 0, n2 = inb ? ln[2] : 0;
-  const uint32_t tot = n0 + n1 + n2, incl = fw_scan(tot, lane), ex = incl - tot, n_e = __shfl(incl, 63);
+  const uint32_t tot = n0 + n1 + n2, incl = fw_scan(tot, lane), ex = incl - tot;
+  uint32_t n_e = __shfl(incl, 63);  // entries (rounds: after the plain blocks are merged)
   if (n_e > kFwE) {
     if (lane == 0) atomicOr(A.err, 8);
     return;
@@ -581,13 +588,95 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
         rhs_terms += w[k];
       }
     }
+    uint32_t pos[kFwPE], grp[kFwPE];
 #pragma unroll
     for (uint32_t k = 0; k < kFwPE; ++k) {
       const uint32_t e = lane * kFwPE + k;
-      if (e < n_e) {
-        L.e_key[e] = ek[k];
-        L.e_kind[e] = (uint8_t)kind[k];
-        L.e_aux[e] = aux[k];
+      grp[k] = e < n_e ? L.e_grp[e] : 0u;
+      pos[k] = e < n_e ? e - L.g_e0[grp[k]] : 0u;
+    }
+    if (A.round) {
+      // Rounds: the entries the round does not substitute are most of a storage row, and the row's keys
+      // are sorted and distinct -- so each maximal block of consecutive plain entries of a group is ONE
+      // sorted run (term j = input entry e_pos + j).  The rank stage then searches one run per block
+      // and per substituted entry instead of one per entry.  A plain entry right after a plain entry of
+      // its group (pos != 0) joins that block; the kept entries are renumbered densely.
+      const uint32_t prev_kind = __shfl_up(kind[kFwPE - 1], 1);
+      uint32_t keep[kFwPE], cnt = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k) {
+        const uint32_t e = lane * kFwPE + k;
+        const uint32_t pk = k ? kind[k - 1] : prev_kind;
+        keep[k] = (e < n_e && !(kind[k] == 0 && pos[k] != 0 && pk == 0)) ? 1u : 0u;
+        cnt += keep[k];
+      }
+      const uint32_t incl = fw_scan(cnt, lane);
+      uint32_t ni[kFwPE], run = incl - cnt;
+      const uint32_t n_e2 = __shfl(incl, 63);
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k) {
+        ni[k] = run;
+        run += keep[k];
+      }
+      // scratch until fw_starts: perm = kept entry -> original index, e_t0 = original -> kept index
+      wave_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k) {
+        const uint32_t e = lane * kFwPE + k;
+        if (keep[k]) {
+          L.perm[ni[k]] = (uint16_t)e;
+          L.e_t0[e] = (uint16_t)ni[k];
+        }
+      }
+      if (lane == 63) {
+        L.perm[n_e2] = (uint16_t)n_e;
+        L.e_t0[n_e] = (uint16_t)n_e2;
+      }
+      wave_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k)  // a block's length: up to the next kept entry (a group's first is kept)
+        if (keep[k] && kind[k] == 0) w[k] = (uint32_t)L.perm[ni[k] + 1] - (lane * kFwPE + k);
+      uint32_t ge[(kFwG + 64) / 64];
+#pragma unroll
+      for (uint32_t q = 0; q < (kFwG + 64) / 64; ++q) {
+        const uint32_t g = lane + 64 * q;
+        ge[q] = g <= kFwG ? L.e_t0[L.g_e0[g]] : 0u;
+      }
+      wave_sync();
+#pragma unroll
+      for (uint32_t q = 0; q < (kFwG + 64) / 64; ++q) {
+        const uint32_t g = lane + 64 * q;
+        if (g <= kFwG) L.g_e0[g] = (uint16_t)ge[q];
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k) {
+        if (!keep[k]) continue;
+        const uint32_t d = ni[k];
+        L.e_key[d] = ek[k];
+        L.e_kind[d] = (uint8_t)kind[k];
+        L.e_aux[d] = aux[k];
+        L.e_grp[d] = (uint8_t)grp[k];
+        L.e_pos[d] = (uint16_t)pos[k];
+        L.perm[d] = (uint16_t)w[k];
+      }
+      wave_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k) {
+        const uint32_t d = lane * kFwPE + k;
+        w[k] = d < n_e2 ? (uint32_t)L.perm[d] : 0u;
+      }
+      wave_sync();
+      n_e = n_e2;
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kFwPE; ++k) {
+        const uint32_t e = lane * kFwPE + k;
+        if (e < n_e) {
+          L.e_key[e] = ek[k];
+          L.e_kind[e] = (uint8_t)kind[k];
+          L.e_aux[e] = aux[k];
+          L.e_pos[e] = (uint16_t)pos[k];
+        }
       }
     }
   }
@@ -601,7 +690,11 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
   fw_terms(A, L, lane, n_e, n_t);
   wave_sync();
   FW_CLK(2);
-  uint32_t rmax = max(n0, max(n1, n2));  // the most runs in one group of the batch
+  uint32_t rmax = 0;  // the most runs in one group of the batch
+  if (inb) {
+    const uint32_t g = 3 * lane;
+    rmax = max((uint32_t)(L.g_e0[g + 1] - L.g_e0[g]), max((uint32_t)(L.g_e0[g + 2] - L.g_e0[g + 1]), (uint32_t)(L.g_e0[g + 3] - L.g_e0[g + 2])));
+  }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d));
   if (rmax > kFwRunsRank) {

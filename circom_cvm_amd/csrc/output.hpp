@@ -65,12 +65,14 @@ __global__ void k_snap_gather(FieldP F, DRows R, const uint8_t *early, const U3 
   }
 }
 
-// A round's snapshot: the storage rows the round rewrote (touched) that stay storage rows (turn < 0)
-// -- elen[r] their part lengths by storage id (else 0); k_snap_mark_round makes them early at base +
-// their offsets (by non-linear row nl_of[r]) and clean again; k_snap_gather_st copies them.
-__global__ void k_snap_lens_round(DRows a, DRows b, DRows c, const uint8_t *touched, const int32_t *turn, uint64_t n, U3 *elen) {
+// A round's snapshot: the storage rows the round rewrote (touched), and the ones not sent yet, that stay
+// storage rows (turn < 0) -- elen[r] their part lengths by storage id (else 0); k_snap_mark_round
+// makes them early at base + their offsets (by non-linear row nl_of[r]) and clean again;
+// k_snap_gather_st copies them.  (A later round may still rewrite one: dirty again, late at the end.)
+__global__ void k_snap_lens_round(DRows a, DRows b, DRows c, const uint8_t *touched, const int32_t *turn, const uint32_t *nl_of,
+                                  const uint8_t *early, uint64_t n, U3 *elen) {
   for (uint64_t r = gtid(); r < n; r += gstride()) {
-    const bool ok = touched[r] && turn[r] < 0 && (a.len[r] | b.len[r]) != 0;
+    const bool ok = (touched[r] || !early[nl_of[r]]) && turn[r] < 0 && (a.len[r] | b.len[r]) != 0;
     elen[r] = ok ? U3{a.len[r], b.len[r], c.len[r]} : U3{0, 0, 0};
   }
 }

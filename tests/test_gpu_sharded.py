@@ -204,6 +204,12 @@ def _run_20m_world8():
 
     def say(what):  # progress (a quiet minute reads as a hang on the GPU box)
         print(f"[20M world 8] {what} at {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    def tick():
+        while True:
+            time.sleep(30)
+            say("still running")
+    threading.Thread(target=tick, daemon=True).start()
     inp = M.Input.synth(0, 20_000_000, 42, "bls12381")
     say("input generated")
     pin = M.PinnedInput(inp.c)
