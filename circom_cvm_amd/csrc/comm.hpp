@@ -46,6 +46,9 @@ struct Comm {
   virtual std::vector<uint64_t> gather_u64(uint64_t v, hipStream_t st) = 0;
   // every rank has arrived (and its work on `st` before the call is complete)
   virtual void barrier(hipStream_t st) { (void)gather_u64(0, st); }
+  // this rank's call failed: ranks waiting in a collective of an in-process group leave it with an
+  // error (RCCL ranks cannot be released this way: a failed rank there ends the job)
+  virtual void fail() {}
   // Collective: host memory every rank of the group sees at the same bytes (page-locked, registered
   // with HIP, so each rank's D2H of its own part of the result lands there directly over its own
   // PCIe link).  Slot `slot` grows only; every rank passes the same size.  nullptr if unavailable.
@@ -169,16 +172,24 @@ struct LocalGroup {
     for (Host &h : host)
       if (h.p) (void)hipHostFree(h.p);
   }
+  bool failed = false;  // a rank's call failed: every barrier throws from now on
   void barrier() {
     std::unique_lock<std::mutex> lk(m);
+    if (failed) throw RsError(RS_E_RCCL, "another rank of the in-process group failed");
     uint64_t g = gen;
     if (++arrived == world) {
       arrived = 0;
       ++gen;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      cv.wait(lk, [&] { return gen != g || failed; });
+      if (gen == g) throw RsError(RS_E_RCCL, "another rank of the in-process group failed");
     }
+  }
+  void fail() {
+    std::lock_guard<std::mutex> lk(m);
+    failed = true;
+    cv.notify_all();
   }
 };
 
@@ -247,6 +258,7 @@ struct LocalComm : Comm {
     HC(hipStreamSynchronize(st));
     g->barrier();
   }
+  void fail() override { g->fail(); }
   void *shared_host(int slot, size_t bytes, hipStream_t st) override {
     HC(hipStreamSynchronize(st));
     g->barrier();  // nobody still uses the old region

@@ -255,6 +255,8 @@ struct rs_engine {
   std::thread snap_thread;
   hipStream_t stx = nullptr;  // the early region's D2H stream
   hipStream_t str = nullptr;  // the host replay's copies (small; never behind the bulk copies)
+  hipStream_t ste = nullptr;  // the small clusters' elimination (k_eliminate), beside the tail's chain
+  hipEvent_t ev_sm[2] = {};   // its start / end
   hipEvent_t ev_chunk[2] = {};
   int snap_rc = 0;
   // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
@@ -510,6 +512,7 @@ static void load_abort(rs_engine *E) {
   if (E->stc) (void)hipStreamSynchronize(E->stc);
   snap_join(E);
   for (bool &pd : E->pending) pd = false;
+  if (E->comm) E->comm->fail();  // the other ranks leave their collectives with an error instead of waiting
 }
 
 // H2D copy whose host buffer may be released right after the call: wait for it.
@@ -1538,13 +1541,19 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       // the head's large-LDS ones have found CUs.  The small clusters first (k_eliminate, one lane
       // each), then the tail: the frames pass that follows waits for both.
       if (n_head) HC(hipStreamWaitEvent(E->st, E->evx[10], 0));
+      // the small clusters (one lane each) on their own stream: nothing of the tail's chain reads them
+      // (disjoint signals; the pool allocation is atomic), so the chain -- the first frames pass's and
+      // hence the result stream's critical path -- starts at once; the main stream joins after it
       HC(hipEventRecord(E->ev4, E->st));
+      HC(hipStreamWaitEvent(E->ste, E->ev4, 0));
+      HC(hipEventRecord(E->ev_sm[0], E->ste));
       if (n_small) {
         uint64_t blocks = (n_small + 63) / 64;
-        hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->st, a,
+        hipLaunchKernelGGL(k_eliminate, dim3((unsigned)std::min<uint64_t>(blocks, 1u << 20)), dim3(64), 0, E->ste, a,
                            (const uint32_t *)d_small, (uint64_t)n_small);
         HC(hipGetLastError());
       }
+      HC(hipEventRecord(E->ev_sm[1], E->ste));
       HC(hipEventRecord(E->evx[5], E->st));
       if (n_tail) {
         // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
@@ -1587,6 +1596,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         if (overlap) hl.run(std::min(kHeadGpuLevels, kHeadLevels), false);
       }
       HC(hipEventRecord(E->ev7, E->st));
+      HC(hipStreamWaitEvent(E->st, E->ev_sm[1], 0));  // the small clusters' substitutions too, from here on
       if (D.join_pending) {  // the main stream reads the head clusters' orders from here on
         HC(hipStreamWaitEvent(E->st, E->evx[7], 0));
         D.join_pending = false;
@@ -1683,8 +1693,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       unsigned long long by = 0;
       HC(hipEventElapsedTime(&ms, E->ev2, E->ev3));
       float msm = 0;
-      HC(hipEventElapsedTime(&msm, E->ev4, E->evx[5]));
-      E->stats.elim_big_ms += ms - msm;  // wall of the workgroup kernels (both streams)
+      HC(hipEventElapsedTime(&msm, E->ev_sm[0], E->ev_sm[1]));
+      E->stats.elim_big_ms += ms;  // wall of the workgroup kernels (both streams; the small ones run beside)
       E->stats.elim_small_ms += msm;
       unsigned long long b5[5] = {0, 0, 0, 0, 0};
       HC(hipMemcpy(b5, a.bytes, 40, hipMemcpyDeviceToHost));
@@ -1715,7 +1725,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           HC(hipEventElapsedTime(&t1, E->ev5, E->ev6));
           HC(hipEventElapsedTime(&t2, E->ev6, E->ev7));
         }
-        HC(hipEventElapsedTime(&t3, E->ev4, E->evx[5]));
+        HC(hipEventElapsedTime(&t3, E->ev_sm[0], E->ev_sm[1]));
         fprintf(stderr, "[rs-prof] tail(%llu): prep %.2f main %.2f inv+finish %.2f small %.2f", (unsigned long long)n_tail, t0, t1, t2, t3);
         if (n_head) {
           float h0 = 0, h1 = 0, h2 = 0;
@@ -2472,7 +2482,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   Fe *heap_v = E->heap_v;
   auto heap_reserve = [&](uint64_t need) {
     if (heap_top + need <= E->heap_cap && E->heap_k) return;
-    uint64_t ncap = std::max<uint64_t>(heap_top + need, E->heap_cap * 2);
+    // grows by a quarter (doubling left the 20 M-row circuit's heap at 12 GB for 6 GB of rows; eight
+    // in-process ranks on one GPU did not fit)
+    uint64_t ncap = std::max<uint64_t>(heap_top + need + (heap_top + need) / 16, E->heap_cap + E->heap_cap / 4);
     ncap = std::max<uint64_t>(ncap, 1 << 16);
     uint32_t *nk = nullptr;
     Fe *nv = nullptr;
@@ -3466,6 +3478,22 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   if (fw_err) throw RsError(RS_E_INTERNAL, "frames batch over its bounds (code " + std::to_string(fw_err) + ")");
   E->stats.final_ms = now_ms() - Tf;
   E->stats.total_ms = now_ms() - T0;
+  if (g_prof_env) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+      fprintf(stderr, "[rs-prof] device memory in use after the run: %.1f of %.1f GB (heap %.1f GB)\n", (tot - fr) / 1e9, tot / 1e9,
+              36e-9 * E->heap_cap);
+    std::vector<std::pair<size_t, std::string>> big;
+    size_t sum = 0;
+    for (auto &kv : A.bufs) {
+      big.push_back({kv.second.cap, kv.first});
+      sum += kv.second.cap;
+    }
+    std::sort(big.rbegin(), big.rend());
+    fprintf(stderr, "[rs-prof] arena %.1f GB in %zu buffers; largest:", sum / 1e9, big.size());
+    for (size_t i = 0; i < big.size() && i < 16; ++i) fprintf(stderr, " %s %.2f", big[i].second.c_str(), big[i].first / 1e9);
+    fprintf(stderr, "\n");
+  }
   E->stats.h2d_wait_ms = E->h2d_wait_ms;
   {  // B_alg: the in-kernel counters + input / output entries and rows + the label map
     const uint64_t z_in = E->ce.nnz + E->eq.nnz + E->lin.nnz + E->na.nnz + E->nb.nnz + E->nc.nnz;
@@ -3513,6 +3541,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->stx, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->str, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&E->ste, hipStreamNonBlocking));
+    for (auto &ev : E->ev_sm) HC(hipEventCreate(&ev));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));
     for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     HC(hipHostMalloc((void **)&E->h_vflag, 10 * sizeof(int), hipHostMallocDefault));
@@ -3549,6 +3579,7 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->st) (void)hipStreamSynchronize(E->st);
   if (E->st2) (void)hipStreamSynchronize(E->st2);
   if (E->stc) (void)hipStreamSynchronize(E->stc);
+  if (E->ste) (void)hipStreamSynchronize(E->ste);
   snap_join(E);
   E->comm.reset();
   for (auto &pb : E->pin)
@@ -3564,6 +3595,9 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->stc) (void)hipStreamDestroy(E->stc);
   if (E->stx) (void)hipStreamDestroy(E->stx);
   if (E->str) (void)hipStreamDestroy(E->str);
+  if (E->ste) (void)hipStreamDestroy(E->ste);
+  for (auto &ev : E->ev_sm)
+    if (ev) (void)hipEventDestroy(ev);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
   if (E->ev1) (void)hipEventDestroy(E->ev1);
   if (E->ev2) (void)hipEventDestroy(E->ev2);
