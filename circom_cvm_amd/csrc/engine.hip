@@ -1412,7 +1412,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     n_big = n_rep + nb;
     n_small = ns;
   }
-  uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 24 * (tot_nnz + n_slots)), E->pool_want);
+  // the substitution pool: 8x the cluster entries (an exhausted pool retries larger, and the size that
+  // fitted is remembered) -- the pool is the engine's largest buffer: 24x took 20.8 GB on the 20 M-row
+  // circuit, and eight in-process ranks did not fit one GPU
+  uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 8 * (tot_nnz + n_slots)), E->pool_want);
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
     Pool G{};  // sharded: every rank's exchanged entries (shard_exchange)
@@ -1664,11 +1667,17 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         fprintf(stderr, "[rs-debug] pool exhausted: cap %llu entries, top %llu, attempt %d\n",
                 (unsigned long long)want, used, attempt);
       }
-      want = std::min<uint64_t>(want * 4, (uint64_t)(fr_ * 0.8) / 36 + want / 2);
+      want = std::min<uint64_t>(want * 2, (uint64_t)(fr_ * 0.8) / 36 + want / 2);
       continue;
     }
     if (err) throw RsError(RS_E_INTERNAL, "elimination invariant violated (code " + std::to_string(err) + ")");
     E->pool_want = std::max(E->pool_want, want);  // the next run starts from a size that fitted
+    if (g_prof_env) {
+      unsigned long long used = 0;
+      HC(hipMemcpy(&used, P.top, 8, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[rs-prof] pool: %llu of %llu entries (%.2f per cluster entry)\n", used, (unsigned long long)want,
+                (double)used / (double)std::max<uint64_t>(1, tot_nnz + n_slots));
+    }
     if (W > 1 && eo.n_clusters) {
       // the head's entries (this rank's local pool, with its own share's) go behind the gathered ones;
       // the replicated clusters' slots follow them, and the gathered pool is the round's pool from here
@@ -2016,7 +2025,9 @@ static void debug_check_round(rs_engine *E, const RoundArgs &ra, uint64_t n, uin
 // ---------------------------------------------------------------- the run
 // the early region's D2H (see rs_engine::SnapJob) on its own thread, fed with jobs as snapshots are
 // taken: each job waits for its gather, then goes in 16 MB chunks, two in flight (8 / 16 / 64 MB
-// chunks measured 53.0 / 52.2 / 55.0 ms host -> host)
+// chunks measured 53.0 / 52.2 / 55.0 ms host -> host; chunks alternating over two streams -- two copy
+// engines -- 49.0 vs 49.6 ms on the metric circuit but 164.9 vs 157.6 ms templated: the run's own
+// copies wait behind both engines)
 static void snap_join(rs_engine *E) {
   {
     std::lock_guard<std::mutex> lk(E->snap_m);

@@ -24,6 +24,17 @@ def engine():
     return _ENG
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _release_engine():
+    """The module's engine goes when its tests are done (later modules -- the 20 M sharded child --
+    need the device memory)."""
+    yield
+    global _ENG
+    if _ENG is not None:
+        _ENG.close()
+        _ENG = None
+
+
 def check(sys_, level="O2", rounds=None, old=False, threads=8):
     h = rsio.InputHolder(sys_)
     fl = rsio.flags(level, rounds, old)

@@ -19,6 +19,17 @@ def engine():
     return _ENG
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _release_engine():
+    """The module's engine goes when its tests are done (later modules -- the 20 M sharded child --
+    need the device memory)."""
+    yield
+    global _ENG
+    if _ENG is not None:
+        _ENG.close()
+        _ENG = None
+
+
 @pytest.mark.parametrize("seed,prime", [(1, "bn128"), (2, "bls12381"), (3, "goldilocks"), (4, "secq256r1")])
 def test_hosthost_random_systems(seed, prime):
     p = R.PRIMES[prime]

@@ -16,6 +16,20 @@ pytestmark = pytest.mark.gpu
 _GROUPS = {}
 
 
+def release_groups():
+    """Closes the cached in-process groups' engines (their device memory)."""
+    for _, engs in _GROUPS.values():
+        for e in engs:
+            e.close()
+    _GROUPS.clear()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _release_groups():
+    yield
+    release_groups()
+
+
 def group(world):
     """W engines on device 0 joined to one in-process group (reused across tests)."""
     if world not in _GROUPS:
@@ -181,7 +195,8 @@ def test_sharded_hosthost_random_small(world):
                         raise AssertionError(f"rank {r}/{world} {lvl}/{rd}: {rsio.same_result(R.Result(ref[0], ref[1], ref[3]), got)}")
 
 
-@pytest.mark.parametrize("kind,rows,world", [(0, 300_000, 2), (0, 400_000, 4), (2, 60_000, 3), (1, 100_000, 4), (5, 200_000, 2)])
+@pytest.mark.parametrize("kind,rows,world", [(0, 300_000, 2), (0, 400_000, 4), (2, 60_000, 3), (1, 100_000, 4), (5, 200_000, 2),
+                                             (0, 2_000_000, 8)])
 def test_sharded_hosthost_synth_arrays(kind, rows, world):
     """Synthetic workloads host -> host over 2-4 ranks, array for array on every rank, three calls on
     the same engines (the shared region is reused and grows as needed)."""
@@ -193,17 +208,18 @@ def test_sharded_hosthost_synth_arrays(kind, rows, world):
         assert st.world == world
 
 
-def _run_20m_world8():
-    """The body of test_sharded_hosthost_bls12381_20m_world8, run in a child process (python
-    tests/test_gpu_sharded.py 20m): its 8 engines each hold the whole 20 M-row problem, which leaves no
-    room for the engines the earlier tests of this process keep."""
+def _run_20m_world4():
+    """The body of test_sharded_hosthost_bls12381_20m_world4, run in a child process (python
+    tests/test_gpu_sharded.py 20m): its engines each hold the whole 20 M-row problem (~51 GB of device
+    memory), which leaves no room for the engines the earlier tests of this process keep -- and eight
+    of them do not fit the card at all, so the 20 M case runs at world 4 and world 8 at 2 M."""
     import sys
     import time
-    world = 8
+    world = 4
     t0 = time.time()
 
     def say(what):  # progress (a quiet minute reads as a hang on the GPU box)
-        print(f"[20M world 8] {what} at {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+        print(f"[20M world 4] {what} at {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
 
     def tick():
         while True:
@@ -233,14 +249,15 @@ def _run_20m_world8():
     say("arrays equal on every rank")
 
 
-def test_sharded_hosthost_bls12381_20m_world8():
+def test_sharded_hosthost_bls12381_20m_world4():
     """BASELINE configs[4] at its stated size: --prime bls12381, the 20 M-row mixed circuit, ONE circuit
-    over 8 ranks host -> host (split upload, sharded elimination with the exchange, split result
+    over 4 ranks host -> host (split upload, sharded elimination with the exchange, split result
     copy), every rank array for array equal to the single-GPU oracle.  In one child process on one GPU
-    (8 engines and an in-process group made for it)."""
+    (4 engines and an in-process group made for it)."""
     import os
     import subprocess
     import sys
+    release_groups()
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "20m"], stdout=sys.__stderr__, stderr=sys.__stderr__,
                        timeout=280, cwd=os.path.dirname(os.path.abspath(__file__)))
     assert r.returncode == 0, f"child exited with {r.returncode}"
@@ -249,4 +266,4 @@ def test_sharded_hosthost_bls12381_20m_world8():
 if __name__ == "__main__":
     import sys
     if sys.argv[1:] == ["20m"]:
-        _run_20m_world8()
+        _run_20m_world4()
