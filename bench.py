@@ -89,7 +89,7 @@ def shard_seed(seed: int, rank: int) -> int:
 
 
 KERNELS = (  # (name, stats fields: ms, bytes, launches)
-    ("k_big_spec<8> (head)", "head_main_ms", "head_main_bytes", "head_launches"),
+    ("k_big_spec<12> (head)", "head_main_ms", "head_main_bytes", "head_launches"),
     # the tail's byte counter includes k_p3_fast's clusters (its PMC traffic is added likewise);
     # the time is k_big_main's
     ("k_big_main<256> (tail)", "tail_main_ms", "tail_main_bytes", "tail_launches"),

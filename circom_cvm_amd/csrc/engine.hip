@@ -1526,9 +1526,11 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));
         HC(hipEventRecord(E->evx[10], E->st2));
-        // the ordered loop: eight waves reduce rows speculatively against the LDS signal table and
-        // commit in pop order (spec_loop.hpp)
-        hipLaunchKernelGGL(k_big_spec<8>, dim3(g), dim3(512), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        // the ordered loop: twelve waves reduce rows speculatively against the LDS signal table and
+        // commit in pop order (spec_loop.hpp).  12 vs 8 waves (three per SIMD at <= 168 VGPRs, 152 B of
+        // spills): the metric circuit's largest cluster 12.9 -> 12.0 ms (the turns that wait for a row
+        // still reducing: 4.5 -> 3.0 ms), templated 26.7 -> 28.1 ms (its chains conflict at distance 1)
+        hipLaunchKernelGGL(k_big_spec<12>, dim3(g), dim3(768), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
         // one inversion per head cluster

@@ -20,7 +20,7 @@ import sys
 # (the tail's in-kernel byte counter also counts k_p3_fast, which runs just before k_big_main on the
 # same clusters' list: its traffic is added to the tail's, per launch of k_big_main)
 GROUPS = {
-    "k_big_spec<8> (head)": ("k_big_spec<",),
+    "k_big_spec<12> (head)": ("k_big_spec<",),
     "k_big_main<256> (tail)": ("k_big_main<256u>", "k_p3_fast"),
     "k_frames_wave<0> (non-linear)": ("k_frames_wave<0>",),
     "k_frames_wave<1> (rounds)": ("k_frames_wave<1>",),
