@@ -23,6 +23,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -102,7 +103,9 @@ def pmc_traffic():
     """HBM bytes per launch per kernel from the newest committed PMC summary (profiles/
     round*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE
     rocprofv3 passes of this bench)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_traffic.json")))
+    # the metric circuit's file only (round4_templated_pmc_traffic.json is the templated circuit's)
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "round*_pmc_traffic.json"))
+                   if re.fullmatch(r"round\d+_pmc_traffic\.json", os.path.basename(f)))
     if not files:
         return {}, None
     with open(files[-1]) as f:
