@@ -256,7 +256,7 @@ struct rs_engine {
   hipStream_t stx = nullptr;  // the early region's D2H stream
   hipStream_t str = nullptr;  // the host replay's copies (small; never behind the bulk copies)
   hipStream_t ste = nullptr;  // the small clusters' elimination (k_eliminate), beside the tail's chain
-  hipEvent_t ev_sm[2] = {};   // its start / end
+  hipEvent_t ev_sm[3] = {};   // its start / k_eliminate done / its work done (the tail's second group too)
   hipEvent_t ev_chunk[2] = {};
   int snap_rc = 0;
   // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
@@ -1062,6 +1062,10 @@ constexpr uint32_t kHeadGpuLevels = 8;
 // best of 5): 48 -> tail loop 7.7 ms, 52.0 ms; 96 -> 5.1 ms, 49.7 ms; 160 -> 5.0 ms, 49.6 ms (device
 // time 39.8 / 37.7 / 39.1 ms: the head grows with its cluster count)
 constexpr uint64_t kHeadLimit = 96;
+// the tail's largest clusters, eliminated on the main stream while the rest runs beside them
+// (host -> host on the metric circuit, best of 5: one group 49.6 ms; split at 256 / 1024 / 4096
+// clusters 48.6 / 48.4 / 48.7 ms; templated 159.5 vs 162.6 / 161.1 / 159.5 ms)
+constexpr uint64_t kTailSplit = 1024;
 // The arena replay of one cluster on the host (k_cl_replay_lane's walk): rows in index order, each
 // pair's previous row found by path halving and its root's list appended to the row's.  A serial
 // union-find of dependent accesses: ~20 ns a pair in a host cache against ~0.3 us in LDS, and the
@@ -1561,33 +1565,51 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipEventRecord(E->ev_sm[1], E->ste));
       HC(hipEventRecord(E->evx[5], E->st));
       if (n_tail) {
-        // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
-        // per-lane pool chunks are bounded by the grid size
-        const unsigned gb = (unsigned)std::min<uint64_t>(n_tail, 2048), gm = (unsigned)std::min<uint64_t>(n_tail, 8192);
-        const uint32_t *ids = d_big + n_head;
-        hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
-        HC(hipGetLastError());
-        // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast); the
-        // ordered loop skips the clusters it took
-        at.skip = E->A.get<uint8_t>("el.skip", n_tail);
-        HC(hipMemsetAsync(at.skip, 0, n_tail, E->st));
-        hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail);
-        HC(hipGetLastError());
-        HC(hipEventRecord(E->ev5, E->st));
-        hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, E->st, at, ids, n_tail);
-        HC(hipGetLastError());
-        HC(hipEventRecord(E->ev6, E->st));
-        {  // tail clusters flagged in cls, then one inversion per 64 slots across clusters
-          uint8_t *cls = E->A.get<uint8_t>("el.cls", eo.n_clusters);
-          HC(hipMemsetAsync(cls, 0, eo.n_clusters, E->st));
-          launch(E->st, k_mark_u8, n_tail, ids, n_tail, cls);
-          launch(E->st, k_batch_inv_flat, (n_slots + 63) / 64, at, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
+        // The tail in two groups on two streams: its kTailSplit largest clusters on the main stream
+        // (their ordered loops are the tail's latency), the rest -- most of the composition work,
+        // which fills the GPU -- beside them on the small clusters' stream, after k_eliminate.  One
+        // launch per kernel over all of them made every finish wait for the largest loops.
+        const uint64_t n_t1 = n_tail > kTailSplit + kTailSplit / 4 ? kTailSplit : n_tail, n_t2 = n_tail - n_t1;
+        auto tail_group = [&](hipStream_t s, ElimArgs g, const uint32_t *ids, uint64_t n, const char *cls_name, bool timed) {
+          // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
+          // per-lane pool chunks are bounded by the grid size
+          const unsigned gb = (unsigned)std::min<uint64_t>(n, 2048), gm = (unsigned)std::min<uint64_t>(n, 8192);
+          hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, s, g, ids, n);
+          HC(hipGetLastError());
+          // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast); the
+          // ordered loop skips the clusters it took
+          HC(hipMemsetAsync(g.skip, 0, n, s));
+          hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, s, g, ids, n);
+          HC(hipGetLastError());
+          if (timed) HC(hipEventRecord(E->ev5, s));
+          hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, s, g, ids, n);
+          HC(hipGetLastError());
+          if (timed) HC(hipEventRecord(E->ev6, s));
+          {  // the group's clusters flagged in cls, then one inversion per 64 slots across clusters
+            uint8_t *cls = E->A.get<uint8_t>(cls_name, eo.n_clusters);
+            HC(hipMemsetAsync(cls, 0, eo.n_clusters, s));
+            launch(s, k_mark_u8, n, ids, n, cls);
+            launch(s, k_batch_inv_flat, (n_slots + 63) / 64, g, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
+          }
+          // clusters of kFinWaveBelow rows and more by the workgroup, the rest one wave each (most
+          // compose chains: the level latency, not the lanes, is their cost)
+          hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, s, g, ids, n, kFinWaveBelow);
+          HC(hipGetLastError());
+        };
+        uint8_t *skip = E->A.get<uint8_t>("el.skip", n_tail);
+        at.skip = skip;
+        tail_group(E->st, at, d_big + n_head, n_t1, "el.cls", true);
+        if (n_t2) {
+          ElimArgs a2 = at;  // per-cluster side arrays indexed by the position in the launch's list
+          a2.big_touch_off += n_t1;
+          a2.big_touch_n += n_t1;
+          a2.big_alive += n_t1;
+          a2.skip = skip + n_t1;
+          if (a2.prof) a2.prof += kProfWords * n_t1;
+          tail_group(E->ste, a2, d_big + n_head + n_t1, n_t2, "el.cls2", false);
         }
-        // clusters of kFinWaveBelow rows and more by the workgroup, the rest one wave each (most compose
-        // chains: the level latency, not the lanes, is their cost)
-        hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, E->st, at, ids, n_tail, kFinWaveBelow);
-        HC(hipGetLastError());
       }
+      HC(hipEventRecord(E->ev_sm[2], E->ste));  // the main stream joins after the tail's second group
       // the head's first levels go in before the host waits for the tail's
       if (n_head) {
         hl.ah = ah;
@@ -1601,7 +1623,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         if (overlap) hl.run(std::min(kHeadGpuLevels, kHeadLevels), false);
       }
       HC(hipEventRecord(E->ev7, E->st));
-      HC(hipStreamWaitEvent(E->st, E->ev_sm[1], 0));  // the small clusters' substitutions too, from here on
+      HC(hipStreamWaitEvent(E->st, E->ev_sm[2], 0));  // the small clusters' and the tail's second group's, from here on
       if (D.join_pending) {  // the main stream reads the head clusters' orders from here on
         HC(hipStreamWaitEvent(E->st, E->evx[7], 0));
         D.join_pending = false;
