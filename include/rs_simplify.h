@@ -157,7 +157,7 @@ typedef struct rs_stats {
   double map_ms;               /* host copy of the non-linear signal map (rounds >= 2)       */
   double rounds_ms;            /* storage updates + bookkeeping of rounds >= 2               */
   double big_prep_ms;          /* k_wide_* + k_big_prep (occurrences + uniques)              */
-  double big_main_ms;          /* the ordered elimination loops (k_big_spec<8> + k_big_main<256>) */
+  double big_main_ms;          /* the ordered elimination loops (k_big_spec<12> + k_big_main<256>) */
   double big_finish_ms;        /* normalisation + composition (k_batch_inv_*, k_big_finish, levels) */
   uint64_t big_main_bytes;     /* algorithmic bytes of the ordered loops (sum over launches)  */
   uint64_t big_finish_bytes;   /* algorithmic bytes of normalisation + composition           */
@@ -173,7 +173,7 @@ typedef struct rs_stats {
    * on the second stream, the critical path) and the tail (every other workgroup cluster), each
    * with its own HIP-event time and in-kernel algorithmic bytes; the storage-row kernel of
    * rounds >= 2; the host -> host legs of rs_engine_simplify. */
-  double head_main_ms;         /* k_big_spec<8> (head: the 48 largest clusters)              */
+  double head_main_ms;         /* k_big_spec<12> (head: the 96 largest clusters)             */
   uint64_t head_main_bytes;
   uint64_t head_launches;
   double tail_main_ms;         /* k_big_main<256> (tail)                                     */
