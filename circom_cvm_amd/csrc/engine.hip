@@ -2048,10 +2048,11 @@ static void debug_check_round(rs_engine *E, const RoundArgs &ra, uint64_t n, uin
 
 // ---------------------------------------------------------------- the run
 // the early region's D2H (see rs_engine::SnapJob) on its own thread, fed with jobs as snapshots are
-// taken: each job waits for its gather, then goes in 16 MB chunks, two in flight (8 / 16 / 64 MB
-// chunks measured 53.0 / 52.2 / 55.0 ms host -> host; chunks alternating over two streams -- two copy
-// engines -- 49.0 vs 49.6 ms on the metric circuit but 164.9 vs 157.6 ms templated: the run's own
-// copies wait behind both engines)
+// taken: each job waits for its gather, then goes in 32 MB chunks, two in flight (16 / 32 / 64 MB,
+// best of 7, two rounds each: metric circuit 48.0-48.4 / 47.8 / 47.6-48.0 ms host -> host, templated
+// 159.8-160.3 / 155.5-156.0 / 158.4 ms; chunks alternating over two streams -- two copy engines --
+// 49.0 vs 49.6 ms on the metric circuit but 164.9 vs 157.6 ms templated: the run's own copies wait
+// behind both engines)
 static void snap_join(rs_engine *E) {
   {
     std::lock_guard<std::mutex> lk(E->snap_m);
@@ -2077,7 +2078,7 @@ static void snap_start(rs_engine *E) {
   E->snap_rc = 0;
   E->snap_closed = false;
   E->snap_thread = std::thread([E]() {
-    constexpr size_t chunk = 16ull << 20;
+    constexpr size_t chunk = 32ull << 20;
     if (hipSetDevice(E->device) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
     int k = 0;
     double prof_ms = 0.0, prof_b = 0.0;
