@@ -138,6 +138,7 @@ SYMBOLS = [
     ("rs_group_destroy", None, [C.c_void_p]),
     ("rs_simplify_multi", C.c_int, [C.POINTER(RsInput), C.POINTER(RsFlags), C.c_int, C.POINTER(C.c_int),
                                     C.POINTER(C.POINTER(RsOutput))]),
+    ("rs_engine_inject_fault", C.c_int, [C.c_void_p, C.c_int]),
     ("rs_read_r1cs_o0", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(RsInput))]),
     ("rs_input_free", None, [C.POINTER(RsInput)]),
     ("rs_write_r1cs", C.c_int, [C.c_char_p, C.POINTER(RsInput), C.POINTER(RsOutput)]),
@@ -265,6 +266,10 @@ class Engine:
         out = C.POINTER(RsOutput)()
         check(lib().rs_engine_simplify(self._h, C.byref(inp), C.byref(flags), C.byref(out)))
         return out.contents
+
+    def inject_fault(self, where: int = 1):
+        """rs_engine_inject_fault: the next run / simplify on this engine fails at `where` (tests)."""
+        check(lib().rs_engine_inject_fault(self._h, where))
 
     def write_r1cs(self, path: str, o0_r1cs: str | None = None) -> float:
         """rs_engine_write_r1cs: the last result as a .r1cs file (device-built constraint section).

@@ -21,7 +21,9 @@
 
 #include <condition_variable>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <set>
 #include <vector>
 
 namespace rs {
@@ -49,6 +51,11 @@ struct Comm {
   // this rank's call failed: ranks waiting in a collective of an in-process group leave it with an
   // error (RCCL ranks cannot be released this way: a failed rank there ends the job)
   virtual void fail() {}
+  // Every entry point that may run collectives brackets itself with begin_call / end_call (every
+  // rank makes the same sequence of calls).  A failure belongs to the call it happened in: once
+  // every rank has left that call, the group is usable again (in-process groups; no-ops for RCCL).
+  virtual void begin_call() {}
+  virtual void end_call() {}
   // Collective: host memory every rank of the group sees at the same bytes (page-locked, registered
   // with HIP, so each rank's D2H of its own part of the result lands there directly over its own
   // PCIe link).  Slot `slot` grows only; every rank passes the same size.  nullptr if unavailable.
@@ -159,8 +166,6 @@ struct LocalGroup {
   int world;
   std::mutex m;
   std::condition_variable cv;
-  uint64_t gen = 0;
-  int arrived = 0;
   std::vector<std::vector<uint8_t>> slot;
   struct Host {
     void *p = nullptr;
@@ -172,29 +177,50 @@ struct LocalGroup {
     for (Host &h : host)
       if (h.p) (void)hipHostFree(h.p);
   }
-  bool failed = false;  // a rank's call failed: every barrier throws from now on
-  void barrier() {
+  // Barriers are counted per call (calls are numbered by each rank's begin_call; every rank makes the
+  // same sequence), so ranks one call apart never share a barrier's count.  A failed call releases
+  // its waiters with an error; its state is dropped once every rank has ended it, and the ranks'
+  // next calls run normally (a persistent group survives an input every rank rejects).
+  struct Bar {
+    int arrived = 0;
+    uint64_t gen = 0;
+  };
+  std::map<uint64_t, Bar> bars;
+  std::set<uint64_t> failed_calls;
+  std::map<uint64_t, int> ended;
+  void barrier(uint64_t call) {
     std::unique_lock<std::mutex> lk(m);
-    if (failed) throw RsError(RS_E_RCCL, "another rank of the in-process group failed");
-    uint64_t g = gen;
-    if (++arrived == world) {
-      arrived = 0;
-      ++gen;
+    if (failed_calls.count(call)) throw RsError(RS_E_RCCL, "another rank of the in-process group failed");
+    Bar &b = bars[call];
+    const uint64_t g = b.gen;
+    if (++b.arrived == world) {
+      b.arrived = 0;
+      ++b.gen;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g || failed; });
-      if (gen == g) throw RsError(RS_E_RCCL, "another rank of the in-process group failed");
+      cv.wait(lk, [&] { return b.gen != g || failed_calls.count(call) != 0; });
+      if (b.gen == g) throw RsError(RS_E_RCCL, "another rank of the in-process group failed");
     }
   }
-  void fail() {
+  void fail(uint64_t call) {
     std::lock_guard<std::mutex> lk(m);
-    failed = true;
+    failed_calls.insert(call);
     cv.notify_all();
+  }
+  void end(uint64_t call) {
+    std::lock_guard<std::mutex> lk(m);
+    if (++ended[call] == world) {  // nobody is inside this call any more
+      ended.erase(call);
+      bars.erase(call);
+      failed_calls.erase(call);
+    }
   }
 };
 
 struct LocalComm : Comm {
   LocalGroup *g;
+  uint64_t call = 0;     // this rank's current call number (begin_call)
+  bool in_call = false;
   LocalComm(LocalGroup *grp, int r) : g(grp) {
     rank = r;
     world = grp->world;
@@ -210,7 +236,7 @@ struct LocalComm : Comm {
   void allgatherv(const void *send, void *recv, const std::vector<uint64_t> &counts, hipStream_t st) override {
     HC(hipStreamSynchronize(st));  // the send buffer is complete
     g->dsend[rank] = send;
-    g->barrier();
+    g->barrier(call);
     uint64_t off = 0;
     for (int q = 0; q < world; ++q) {
       const bool in_place = g->dsend[q] == (const void *)((uint8_t *)recv + off);  // this rank's own share, already there
@@ -218,12 +244,12 @@ struct LocalComm : Comm {
       off += counts[q];
     }
     HC(hipStreamSynchronize(st));
-    g->barrier();  // the send buffers may be reused only after every rank has read them
+    g->barrier(call);  // the send buffers may be reused only after every rank has read them
   }
   void allreduce_sum(void *buf, uint64_t n, int elem_bytes, hipStream_t st) override {
     if (!n) return;
     post(buf, n * elem_bytes, st);
-    g->barrier();
+    g->barrier(call);
     std::vector<uint8_t> acc(g->slot[0]);
     for (int q = 1; q < world; ++q) {
       if (elem_bytes == 8) {
@@ -238,15 +264,15 @@ struct LocalComm : Comm {
     }
     HC(hipMemcpyAsync(buf, acc.data(), n * elem_bytes, hipMemcpyHostToDevice, st));
     HC(hipStreamSynchronize(st));
-    g->barrier();
+    g->barrier(call);
   }
   std::vector<uint64_t> gather_u64(uint64_t v, hipStream_t) override {
     g->slot[rank].resize(8);
     memcpy(g->slot[rank].data(), &v, 8);
-    g->barrier();
+    g->barrier(call);
     std::vector<uint64_t> r(world);
     for (int q = 0; q < world; ++q) memcpy(&r[q], g->slot[q].data(), 8);
-    g->barrier();
+    g->barrier(call);
     return r;
   }
   uint64_t max_u64(uint64_t v, hipStream_t st) override {
@@ -256,12 +282,21 @@ struct LocalComm : Comm {
   }
   void barrier(hipStream_t st) override {
     HC(hipStreamSynchronize(st));
-    g->barrier();
+    g->barrier(call);
   }
-  void fail() override { g->fail(); }
+  void fail() override { g->fail(call); }
+  void begin_call() override {
+    ++call;
+    in_call = true;
+  }
+  void end_call() override {
+    if (!in_call) return;
+    in_call = false;
+    g->end(call);
+  }
   void *shared_host(int slot, size_t bytes, hipStream_t st) override {
     HC(hipStreamSynchronize(st));
-    g->barrier();  // nobody still uses the old region
+    g->barrier(call);  // nobody still uses the old region
     LocalGroup::Host &h = g->host[slot];
     if (rank == 0 && h.cap < bytes) {
       const size_t cap = std::max(bytes, h.cap + h.cap / 4);
@@ -271,7 +306,7 @@ struct LocalComm : Comm {
       if (hipHostMalloc(&h.p, cap, hipHostMallocDefault) == hipSuccess) h.cap = cap;
       else h.p = nullptr;
     }
-    g->barrier();
+    g->barrier(call);
     return h.cap >= bytes ? h.p : nullptr;
   }
 };

@@ -85,13 +85,26 @@ struct Arena {
   // one hash probe per lookup
   std::unordered_map<std::string, B> bufs{512};
   uint64_t gen = 0;  // bumped whenever a buffer moves (raw pointers taken before are then stale)
+  // hipFree waits for the whole device: while `defer` is set (the sharded exchange, which runs beside
+  // the head's elimination) a moved buffer's old block is kept until flush() instead
+  bool defer = false;
+  std::vector<void *> graveyard;
+  void release(void *p) {
+    if (!p) return;
+    if (defer) graveyard.push_back(p);
+    else HC(hipFree(p));
+  }
+  void flush() {
+    for (void *p : graveyard) (void)hipFree(p);
+    graveyard.clear();
+  }
   template <class T>
   T *get(const std::string &name, size_t n) {
     size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
     B &b = bufs[name];
     if (b.cap < bytes) {
       ++gen;
-      if (b.p) HC(hipFree(b.p));
+      release(b.p);
       size_t cap = std::max(bytes, b.cap + b.cap / 4);
       HC(hipMalloc(&b.p, cap));
       b.cap = cap;
@@ -113,7 +126,7 @@ struct Arena {
       HC(hipStreamSynchronize(ps));
       if (keep) HC(hipMemcpyAsync(p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
       HC(hipStreamSynchronize(st));
-      HC(hipFree(b.p));
+      release(b.p);
     }
     b.p = p;
     b.cap = cap;
@@ -123,6 +136,7 @@ struct Arena {
     return it == bufs.end() ? 0 : it->second.cap;
   }
   ~Arena() {
+    flush();
     for (auto &kv : bufs)
       if (kv.second.p) (void)hipFree(kv.second.p);
   }
@@ -168,6 +182,7 @@ struct rs_engine {
   Arena A;
   bool loaded = false;
   bool have_result = false;
+  int fault_at = 0;  // rs_engine_inject_fault: 1 = throw at the start of the first elimination round
   FieldP F;
   uint64_t prime[4];
   uint32_t prime_id = 0;
@@ -1011,7 +1026,6 @@ struct DevClusters {
   // the end); only the head -- ordered after the replay on that stream -- reads them until the join
   bool join_pending = false;
 };
-// the number of largest clusters eliminated on the second stream (RS_HEAD overrides)
 // Split composition (k_big_finish with ElimArgs.split, then one k_compose_level launch per Kahn
 // level of every cluster at once over the whole GPU, k_big_emit at the end).  Level L reads count
 // L%3, appends to (L+1)%3 and zeroes (L+2)%3 -- the one level L-1 read and level L+1 appends to --
@@ -1320,6 +1334,7 @@ static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D
   Arena &A = E->A;
   hipStream_t st = E->st;
   const double t0 = now_ms();
+  A.defer = true;  // the head is still running on st2: no device-wide hipFree while its buffers grow
   const uint64_t n_slots = D.n_slots, n_cl = a.n_clusters;
   uint64_t *sf = A.get<uint64_t>("x.sf", n_slots), *sp = A.get<uint64_t>("x.sp", n_slots);
   uint64_t *se = A.get<uint64_t>("x.se", n_slots), *sep = A.get<uint64_t>("x.sep", n_slots);
@@ -1362,6 +1377,7 @@ static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D
     os += ns[q]; ol += nl[q]; oe += ne[q];
   }
   HC(hipStreamSynchronize(st));
+  A.defer = false;
   G.pk = gk;
   G.pv = gv;
   G.top = nullptr;
@@ -1382,6 +1398,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
                                       const std::function<void()> *before_elim = nullptr,
                                       const uint8_t *need = nullptr) {
   double t0 = now_ms();
+  if (E->fault_at == 1) {
+    E->fault_at = 0;
+    throw RsError(RS_E_INTERNAL, "injected fault (rs_engine_inject_fault)");
+  }
   DevClusters D = gpu_clusters(E, view, old_heur, d_forb, eo);
   // keys-first rows: their values now (main stream; every elimination kernel is ordered after it)
   if (before_elim) (*before_elim)();
@@ -1861,6 +1881,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     eo.n_left = sums[1];
     E->stats.n_substitutions += eo.n_sub;
     E->stats.elim_ms += now_ms() - t1;
+    E->A.defer = false;
+    E->A.flush();  // every stream that could read an old block was synchronised above
     return;
   }
   throw RsError(RS_E_OOM_DEVICE, "substitution pool exhausted");
@@ -2176,6 +2198,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   hipStream_t st = E->st;
   E->stats = rs_stats{};
   E->stats.world = E->comm ? (uint64_t)E->comm->world : 1;
+  E->A.defer = false;  // an exchange a failed run left mid-way
   double T0 = now_ms();
   bool apply_linear = !fl->flag_s;
   uint64_t no_rounds = fl->no_rounds;
@@ -2592,7 +2615,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (shard) {  // every rank's share of each part gets the same capacity in the shared region
       for (int q = 0; q < 3; ++q) E->sh_cap[q] = CM->max_u64(std::max<uint64_t>(ev[q] + ev[q] / 4 + 65536, E->sh_cap[q]), st);
       E->sh_ent = CM->shared_host(0, sh_ent_bytes(E), st);
-      if (!E->sh_ent) throw RsError(RS_E_RCCL, "no shared host memory for the sharded result");
+      if (!E->sh_ent) {  // every rank alike (shared_host agrees): no stream; each rank fetches the whole result
+        if (g_prof_env) fprintf(stderr, "[rs-prof] no shared host memory: unstreamed per-rank result\n");
+        E->stream_out = false;
+        return;
+      }
     }
     // the gather reads copies of the row views: the second pass and later rounds re-point rows
     const DRows *src[3] = {&sa, &sb, &sc};
@@ -3492,6 +3519,8 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         snap_join(E);  // the early copies into the old region are done (they are redone below)
         for (int q = 0; q < 3; ++q) E->sh_cap[q] = CMf->max_u64(E->out_ext[q] + E->out_ext[q] / 4 + 65536, st);
         E->sh_ent = CMf->shared_host(0, sh_ent_bytes(E), st);
+        // (the first snapshot's shared_host already fell back when the host had no room; a regrow
+        // that fails here is an error every rank reports alike)
         if (!E->sh_ent) throw RsError(RS_E_RCCL, "no shared host memory for the sharded result");
         E->sh_full = true;
       }
@@ -3542,6 +3571,24 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   E->have_result = true;
 }
 
+}  // namespace rs
+
+namespace rs {
+// One entry point's bracket around its collectives (Comm::begin_call / end_call): a call that does not
+// end in RS_OK marks the call failed, which releases the ranks of an in-process group waiting in its
+// collectives (rs_engine_run's failures left them waiting); the group itself stays usable.
+struct CallScope {
+  rs_engine *E;
+  bool ok = false;
+  explicit CallScope(rs_engine *e) : E(e) {
+    if (E->comm) E->comm->begin_call();
+  }
+  ~CallScope() {
+    if (!E->comm) return;
+    if (!ok) E->comm->fail();
+    E->comm->end_call();
+  }
+};
 }  // namespace rs
 
 // ==================================================================== C API
@@ -3658,10 +3705,12 @@ void rs_engine_destroy(rs_engine *E) {
 }
 
 int rs_engine_load(rs_engine *E, const rs_input *in) {
+  CallScope cs(E);
   try {
     HC(hipSetDevice(E->device));
     load_enqueue(E, in, false);
     load_wait_all(E);
+    cs.ok = true;
     return RS_OK;
   } catch (const RsError &e) {
     load_abort(E);
@@ -3677,10 +3726,12 @@ int rs_engine_load(rs_engine *E, const rs_input *in) {
 }
 
 int rs_engine_run(rs_engine *E, const rs_flags *fl) {
+  CallScope cs(E);
   try {
     if (!E->loaded) { set_error("engine has no input"); return RS_E_INVALID; }
     HC(hipSetDevice(E->device));
     engine_run(E, fl);
+    cs.ok = true;
     return RS_OK;
   } catch (const RsError &e) {
     set_error(e.what());
@@ -3913,6 +3964,7 @@ int rs_engine_fetch(rs_engine *E, rs_output **out) {
 }
 
 int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, const rs_output **out) {
+  CallScope cs(E);
   try {
     const double t0 = now_ms();
     HC(hipSetDevice(E->device));
@@ -3934,6 +3986,7 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
     E->stats.d2h_ms = t2 - t1;
     E->stats.host_total_ms = t2 - t0;
     *out = &E->view;
+    cs.ok = true;
     return RS_OK;
   } catch (const RsError &e) {
     load_abort(E);
@@ -4138,6 +4191,12 @@ int rs_engine_join_rccl(rs_engine *E, int world, int rank, const uint8_t id[RS_C
     set_error(e.what());
     return RS_E_INTERNAL;
   }
+}
+
+int rs_engine_inject_fault(rs_engine *E, int where) {
+  if (!E || where < 0 || where > 1) { set_error("rs_engine_inject_fault: bad argument"); return RS_E_INVALID; }
+  E->fault_at = where;
+  return RS_OK;
 }
 
 rs_group *rs_group_create(int world) {

@@ -258,6 +258,14 @@ int rs_engine_join_group(rs_engine *eng, rs_group *g, int rank);
 void rs_group_destroy(rs_group *g);
 int rs_simplify_multi(const rs_input *in, const rs_flags *fl, int n_devices, const int *devices, rs_output **out);
 
+/* Fault injection (tests; SURVEY 5 "failure detection / fault injection"): the engine's next
+ * rs_engine_run / rs_engine_simplify fails with RS_E_INTERNAL at `where` (1: the start of the first
+ * linear elimination round, after the run's first collectives; 0: cancel).  A failure belongs to the
+ * call it happens in: the other ranks of an in-process group leave that call with RS_E_RCCL, and the
+ * group runs the ranks' next calls normally.  RCCL ranks are not released (a failed rank there ends
+ * the job). */
+int rs_engine_inject_fault(rs_engine *eng, int where);
+
 /* --O0 .r1cs -> rs_input (host arrays owned by the library; free with rs_input_free).
  * Classifies rows exactly like dag/src/map_to_constraint_list.rs:12-44.  The signals of the
  * custom-gate applications (section 5, dag/src/r1cs_porting.rs:74-107) join `forbidden`, as

@@ -208,6 +208,101 @@ def test_sharded_hosthost_synth_arrays(kind, rows, world):
         assert st.world == world
 
 
+def _run_expect_fail(engs, inp, fl, mode):
+    """Every rank runs `mode` ('simplify' or 'load+run') on its own input; returns the per-rank
+    exception (None on success).  A hang fails the test."""
+    world = len(engs)
+    errs = [None] * world
+
+    def work(r):
+        try:
+            if mode == "simplify":
+                engs[r].simplify(inp[r], fl[r])
+            else:
+                engs[r].load(inp[r])
+                engs[r].run(fl[r])
+        except Exception as ex:  # noqa: BLE001 -- returned
+            errs[r] = ex
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+        assert not t.is_alive(), "a rank hung after another rank's failure"
+    return errs
+
+
+def _fresh_group(world):
+    g = M.Group(world)
+    engs = [M.Engine(0) for _ in range(world)]
+    for r, e in enumerate(engs):
+        e.join_group(g, r)
+    return g, engs
+
+
+def test_group_survives_rejected_input():
+    """a failure is scoped to the call it happened in.  An input every rank rejects (a key
+    past max_signal, caught by the device checks) fails the call on every rank; the same persistent
+    in-process group then runs a valid input host -> host and load + run, equal to the oracle."""
+    world = 2
+    g, engs = _fresh_group(world)
+    try:
+        p = R.PRIMES["bn128"]
+        good = rsio.InputHolder(rsio.gen_system(91, p, n_sig=80, n_rows=120))
+        bad = rsio.InputHolder(rsio.gen_system(91, p, n_sig=80, n_rows=120))
+        bad.blocks[2].col[0] = bad.inp.max_signal + 7  # the first linear row's first key: out of range
+        fl = rsio.flags("O2")
+        for mode in ("simplify", "load+run"):
+            errs = _run_expect_fail(engs, [bad.inp] * world, [fl] * world, mode)
+            assert all(isinstance(e, M.RsError) for e in errs), errs
+        ref, _, _ = rsio.oracle_run(good.inp, fl)
+        for _ in range(2):
+            for r, (got, _st) in enumerate(sharded_simplify(good.inp, fl, world, engs=engs, arrays=False)):
+                assert got == ref, f"rank {r} after the rejected input"
+        outs = [None] * world
+
+        def work(r):
+            engs[r].load(good.inp)
+            engs[r].run(fl)
+            outs[r] = rsio.output_to_py(engs[r].fetch().c)
+        th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+            assert not t.is_alive()
+        assert all(o == ref for o in outs)
+    finally:
+        for e in engs:
+            e.close()
+
+
+def test_one_rank_fails_others_released():
+    """when ONE rank's run fails mid-way (an injected fault at the start of its first
+    elimination round, after the run's first collectives), the other ranks of the in-process group
+    leave their collectives with RS_E_RCCL instead of waiting forever -- for load + run and for host ->
+    host -- and the same group then runs valid calls equal to the oracle."""
+    world = 3
+    g, engs = _fresh_group(world)
+    try:
+        p = R.PRIMES["bn128"]
+        good = rsio.InputHolder(rsio.gen_system(92, p, n_sig=300, n_rows=250, big_cluster=700))
+        fl = rsio.flags("O2")
+        ref, _, _ = rsio.oracle_run(good.inp, fl)
+        for mode in ("load+run", "simplify"):
+            engs[2].inject_fault(1)
+            errs = _run_expect_fail(engs, [good.inp] * world, [fl] * world, mode)
+            assert isinstance(errs[2], M.RsError) and errs[2].code == -5, errs  # RS_E_INTERNAL: the fault
+            for r in range(2):
+                assert isinstance(errs[r], M.RsError) and errs[r].code == -4, errs  # RS_E_RCCL: released
+            for r, (got, _st) in enumerate(sharded_simplify(good.inp, fl, world, engs=engs, arrays=False)):
+                assert got == ref, f"rank {r} after the fault ({mode})"
+    finally:
+        for e in engs:
+            e.close()
+
+
 def _run_20m_world4():
     """The body of test_sharded_hosthost_bls12381_20m_world4, run in a child process (python
     tests/test_gpu_sharded.py 20m): its engines each hold the whole 20 M-row problem (~51 GB of device

@@ -2,7 +2,7 @@
 # A/B of kernel times under environment knobs (GPU box, repo root): for each "TAG:ENV=V,ENV=V" argument,
 # rocprofv3 --kernel-trace --stats of tools/config_bench.py on CONFIGS (default mixed10M), then
 # tools/kstats.py prints the per-step time of the main kernels side by side.
-# usage: CONFIGS="mixed10M" REPS=4 bash tools/ab_kernels.sh base: sort:RS_COMPOSE=sort
+# usage: CONFIGS="mixed10M" REPS=4 bash tools/ab_kernels.sh base: prof:RS_PROF=1
 set -e
 OUT=gpurun_out/ab
 mkdir -p $OUT
