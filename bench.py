@@ -49,6 +49,7 @@ def cpu_baseline(M, inp, threads: int, j1_rows: int, seed: int, prime: str):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import rsio
     arrays, ms = rsio.oracle_arrays(inp.c, rsio.flags("O2"), threads=threads)
+    alg = rsio.oracle_last_alg()  # B_alg of the same run (the roofline path's numerator)
     res = {"value": round(inp.rows() / (ms / 1000.0), 1), "unit": "constraints/s", "cores": threads,
            "kind": "port", "affinity_cpus": len(os.sched_getaffinity(0)),
            "sample": f"the full rank-0 workload ({inp.rows()} rows), oracle/refcpu.cpp simplification() "
@@ -60,7 +61,7 @@ def cpu_baseline(M, inp, threads: int, j1_rows: int, seed: int, prime: str):
                      "sample": f"synth_mixed rows={smp.rows()} seed={seed} {prime} --O2 on 1 thread: "
                                f"{ms1 / 1000.0:.2f} s"}
         smp.free()
-    return res, arrays
+    return res, arrays, alg
 
 
 def reduce_over_ranks(dist, dt: float, n_rows: int, device):
@@ -418,8 +419,21 @@ def main():
             line["weak_shards"] = weak
         if not args.no_cpu:
             threads = args.cpu_threads or cpu_threads()
-            cb, ref = cpu_baseline(M, inp, threads, args.cpu_j1_rows, args.seed, args.prime)
+            cb, ref, alg = cpu_baseline(M, inp, threads, args.cpu_j1_rows, args.seed, args.prime)
             line["cpu_baseline"] = cb
+            # the whole-path roofline from the oracle's B_alg (implementation-independent: counted over
+            # the canonical execution's logical operations, oracle/refcpu.cpp header); the device's own
+            # in-kernel total stays beside it
+            p = line["roofline"]["path"]
+            p["alg_bytes_device_per_step"] = p.pop("alg_bytes_per_step")
+            p["achieved_device"] = p.pop("achieved")
+            p.pop("frac", None)
+            p["alg_bytes_refcpu"] = alg["B_alg"]
+            p["alg_terms_refcpu"] = {k: v for k, v in alg.items() if k != "B_alg"}
+            ach = alg["B_alg"] / (ms_step / 1000.0) / 1e9
+            p["achieved"] = round(ach, 2)
+            p["frac"] = round(ach / HBM_PEAK_GBS, 5)
+            p["device_over_refcpu"] = round(p["alg_bytes_device_per_step"] / max(alg["B_alg"], 1), 3)
             import rsio
             diff = rsio.diff_output_arrays(got, ref)
             line["bit_exact"] = diff is None

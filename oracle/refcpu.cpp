@@ -27,6 +27,23 @@
 //
 // Parallel structure mirrors the reference: a pool of n_threads over eq clusters of size > 1
 // and over linear clusters (constraint_simplification.rs:212, :293); everything else serial.
+//
+// Algorithmic bytes (the roofline numerator; refcpu_last_alg): counted over the LOGICAL
+// operations of this canonical execution, so they do not depend on how an implementation moves the
+// data.  With w = 4 + field bytes per (signal, coefficient) entry:
+//   B_alg = w * (Z_in + Z_out + subs + app + rowupd + merges) + 8 * (R_in + R_out) + 8 * max_signal
+//   Z_in / Z_out   entries of the input blocks / of the result;  R_in / R_out their rows
+//   subs           entries of every substitution written: eq and constant substitutions, the holders
+//                  (clear_signal_not_normalized), their normalised copies (normalize_substitutions)
+//   app            for every application of a substitution to a row or to another substitution
+//                  (fast_encoded_constraint_substitution, apply_substitution_to_map, the lconst
+//                  passes, create_nonoverlapping_substitutions): the entries of its right-hand side
+//   rowupd         per row rewritten by one substitution pass (the eq + constant frames of a linear
+//                  row; the three frames + fix of a non-linear row; one round's substitutions of a
+//                  storage row or an lconst row; one composition step of a substitution; the ordered
+//                  loop's reduction of a popped row into its holder or leftover): entries before +
+//                  entries after
+//   merges         per conflict merge of treat_constraint_3/4: |work| + |conflicting RHS| + |new work|
 
 #include "refcpu_field.h"
 #include "../include/rs_simplify.h"
@@ -77,7 +94,16 @@ static const uint64_t kPrimes[8][4] = {
     {0xffffffffffffffffULL, 0x00000000ffffffffULL, 0x0000000000000000ULL, 0xffffffff00000001ULL},
     {0x0a11800000000001ULL, 0x59aa76fed0000001ULL, 0x60b44d1e5c37b001ULL, 0x12ab655e9a2ca556ULL}};
 
+// the B_alg terms (entries, except the row counts); summed per cluster, so parallel workers never share one
+struct Alg {
+  uint64_t z_in = 0, z_out = 0, subs = 0, app = 0, rowupd = 0, merges = 0, r_in = 0, r_out = 0;
+  void add(const Alg &o) {
+    z_in += o.z_in; z_out += o.z_out; subs += o.subs; app += o.app;
+    rowupd += o.rowupd; merges += o.merges; r_in += o.r_in; r_out += o.r_out;
+  }
+};
 struct Ctx {
+  Alg alg;
   Field F;
   uint64_t max_signal = 0;
   std::vector<uint8_t> forbidden;
@@ -352,6 +378,7 @@ static void merge_conflict(const Field &F, const Fe &coef, const Map &L, const F
 struct Simplified {
   std::vector<Map> lconst;  // leftover linear constraints (C part)
   std::vector<Sub> subs;    // ascending from
+  Alg alg;                  // this cluster's B_alg terms
 };
 
 static void normalize_and_compose(Ctx &X, Holder &H, const std::vector<uint32_t> *order,
@@ -371,8 +398,10 @@ static void normalize_and_compose(Ctx &X, Holder &H, const std::vector<uint32_t>
     invs[i - 1] = F.mul(pre[i - 1], inv);
     inv = F.mul(inv, H.coef[perm[i - 1]]);
   }
-  for (size_t i = 0; i < m; ++i)
+  for (size_t i = 0; i < m; ++i) {
     for (Term &t : H.to[perm[i]]) t.v = F.mul(t.v, invs[i]);
+    res.alg.subs += H.to[perm[i]].size();  // the normalised copy
+  }
   // create_nonoverlapping_substitutions(_4) (simplification_utils.rs:451-479)
   std::vector<uint32_t> seq;
   if (order) seq.assign(order->rbegin(), order->rend());  // newest first
@@ -384,7 +413,13 @@ static void normalize_and_compose(Ctx &X, Holder &H, const std::vector<uint32_t>
     apply.clear();
     for (const Term &t : to)
       if (X.noov_idx[t.k] >= 0) apply.push_back(t.k);
-    for (uint32_t k : apply) raw_substitution(F, to, k, H.to[X.noov_idx[k]]);
+    for (uint32_t k : apply) {
+      const Map &rk = H.to[X.noov_idx[k]];
+      const uint64_t before = to.size();
+      raw_substitution(F, to, k, rk);
+      res.alg.app += rk.size();
+      res.alg.rowupd += before + to.size();
+    }
     X.noov_idx[s] = hi;
   }
   for (size_t i = 0; i < m; ++i) {
@@ -405,12 +440,14 @@ static void process_3(Ctx &X, std::vector<Map> &cons, Simplified &res) {
     work.swap(cons.back());
     cons.pop_back();
     RC_TRACE_ROW(work.size());
+    const uint64_t popped = work.size();
+    uint64_t written = 0;
     for (;;) {
       if (work.empty()) break;
       int64_t out = -1;
       for (size_t i = work.size(); i-- > 0;)
         if (!X.forbidden[work[i].k]) { out = work[i].k; break; }
-      if (out < 0) { RC_TRACE_LEFT(work.size()); res.lconst.push_back(work); break; }
+      if (out < 0) { RC_TRACE_LEFT(work.size()); written = work.size(); res.lconst.push_back(work); break; }
       clear_nn(F, work, (uint32_t)out, coef, to);
       int32_t hi = X.holder_idx[out];
       if (hi >= 0) RC_TRACE_MERGE((uint32_t)out, work.size(), hi, H.to[hi].size());
@@ -420,10 +457,15 @@ static void process_3(Ctx &X, std::vector<Map> &cons, Simplified &res) {
         H.sig.push_back((uint32_t)out);
         H.coef.push_back(coef);
         H.to.push_back(to);
+        written = to.size();
+        res.alg.subs += to.size();
         break;
       }
+      const uint64_t w0 = work.size();
       merge_conflict(F, coef, to, H.coef[hi], H.to[hi], work);
+      res.alg.merges += w0 + H.to[hi].size() + work.size();
     }
+    res.alg.rowupd += popped + written;
   }
   RC_TRACE_END();
   normalize_and_compose(X, H, nullptr, res);
@@ -469,6 +511,8 @@ static void process_4(Ctx &X, std::vector<Map> &vec, Simplified &res) {
     remove_constraint(actual);
     clear_nn(F, actual, u.first, coef, to);
     RC_TRACE_INSERT(u.first, H.sig.size(), to.size());
+    res.alg.rowupd += actual.size() + to.size();
+    res.alg.subs += to.size();
     insert(u.first, coef, to);
   }
   while (!vec.empty()) {
@@ -476,6 +520,8 @@ static void process_4(Ctx &X, std::vector<Map> &vec, Simplified &res) {
     vec.pop_back();
     remove_constraint(work);
     RC_TRACE_ROW(work.size());
+    const uint64_t popped = work.size();
+    uint64_t written = 0;
     for (;;) {
       if (work.empty()) break;
       // take_signal_4 (simplification_utils.rs:379-411), HashMap order := ascending
@@ -489,13 +535,22 @@ static void process_4(Ctx &X, std::vector<Map> &vec, Simplified &res) {
         if (occ_ret < 0 || n < occ_ret) { ret = t.k; occ_ret = n; }
         else if (n == occ_ret && ret < (int64_t)t.k) ret = t.k;
       }
-      if (ret < 0) { RC_TRACE_LEFT(work.size()); res.lconst.push_back(work); break; }
+      if (ret < 0) { RC_TRACE_LEFT(work.size()); written = work.size(); res.lconst.push_back(work); break; }
       clear_nn(F, work, (uint32_t)ret, coef, to);
       int32_t hi = X.holder_idx[ret];
-      if (hi < 0) { RC_TRACE_INSERT((uint32_t)ret, H.sig.size(), to.size()); insert((uint32_t)ret, coef, to); break; }
+      if (hi < 0) {
+        RC_TRACE_INSERT((uint32_t)ret, H.sig.size(), to.size());
+        written = to.size();
+        res.alg.subs += to.size();
+        insert((uint32_t)ret, coef, to);
+        break;
+      }
       RC_TRACE_MERGE((uint32_t)ret, work.size(), hi, H.to[hi].size());
+      const uint64_t w0 = work.size();
       merge_conflict(F, coef, to, H.coef[hi], H.to[hi], work);
+      res.alg.merges += w0 + H.to[hi].size() + work.size();
     }
+    res.alg.rowupd += popped + written;
   }
   RC_TRACE_END();
   for (uint32_t s : touched) X.occ[s] = -1;
@@ -525,6 +580,7 @@ static void linear_simplification(Ctx &X, const std::vector<Con> &linear, bool o
     results[i] = full_simplification(X, std::move(rows), old_heur);
   });
   for (auto &r : results) {
+    X.alg.add(r.alg);
     for (auto &m : r.lconst) { Con c; c.c = std::move(m); cons.push_back(std::move(c)); }
     for (auto &s : r.subs) subs.push_back(std::move(s));
   }
@@ -532,15 +588,20 @@ static void linear_simplification(Ctx &X, const std::vector<Con> &linear, bool o
 
 // fast_encoded_constraint_substitution (simplification_utils.rs:496-507)
 static bool fast_encoded(const Field &F, Con &c, const std::vector<int32_t> &idx,
-                         const std::vector<Sub> &subs, std::vector<uint32_t> &sig) {
+                         const std::vector<Sub> &subs, std::vector<uint32_t> &sig, uint64_t *app = nullptr) {
   take_signals(c, sig);
   bool applied = false;
   for (uint32_t s : sig) {
     int32_t i = idx[s];
-    if (i >= 0) { apply_substitution(F, c, s, subs[i].to); applied = true; }
+    if (i >= 0) {
+      apply_substitution(F, c, s, subs[i].to);
+      applied = true;
+      if (app) *app += subs[i].to.size();
+    }
   }
   return applied;
 }
+static inline uint64_t con_size(const Con &c) { return c.a.size() + c.b.size() + c.c.size(); }
 
 // ------------------------------------------------------------------ simplification (:442-730)
 struct Input {
@@ -605,10 +666,19 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
   }
   std::vector<int32_t> eq_idx(S, -1);
   for (size_t i = 0; i < eq_subs.size(); ++i) eq_idx[eq_subs[i].from] = (int32_t)i;
-  for (Con &c : in.linear)
-    if (fast_encoded(F, c, eq_idx, eq_subs, sig)) fix_constraint(F, c);
-  for (Con &c : in.cons_eq)
-    if (fast_encoded(F, c, eq_idx, eq_subs, sig)) fix_constraint(F, c);
+  for (const Sub &sb : eq_subs) X.alg.subs += sb.to.size();
+  // B_alg: a linear row's eq + constant frames are one update (its size before them, after both)
+  std::vector<uint32_t> lin0(in.linear.size());
+  std::vector<uint8_t> lin_touched(in.linear.size(), 0);
+  for (size_t i = 0; i < in.linear.size(); ++i) lin0[i] = (uint32_t)con_size(in.linear[i]);
+  for (size_t i = 0; i < in.linear.size(); ++i) {
+    Con &c = in.linear[i];
+    if (fast_encoded(F, c, eq_idx, eq_subs, sig, &X.alg.app)) { fix_constraint(F, c); lin_touched[i] = 1; }
+  }
+  for (Con &c : in.cons_eq) {
+    const uint64_t before = con_size(c);
+    if (fast_encoded(F, c, eq_idx, eq_subs, sig, &X.alg.app)) { fix_constraint(F, c); X.alg.rowupd += before + con_size(c); }
+  }
   for (const Sub &s : eq_subs) deleted[s.from] = 1;
   std::vector<int32_t> single_idx(S, -1);  // remove_not_relevant
   for (size_t i = 0; i < eq_subs.size(); ++i)
@@ -632,12 +702,16 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
     Fe inv = F.inv(F.neg(k));
     for (Term &t : rest) t.v = F.mul(t.v, inv);
     remove_zero(rest);
+    X.alg.subs += rest.size();
     c_subs.push_back(Sub{s, std::move(rest)});
   }
   std::vector<int32_t> c_idx(S, -1);
   for (size_t i = 0; i < c_subs.size(); ++i) c_idx[c_subs[i].from] = (int32_t)i;  // last wins
-  for (Con &c : in.linear)
-    if (fast_encoded(F, c, c_idx, c_subs, sig)) fix_constraint(F, c);
+  for (size_t i = 0; i < in.linear.size(); ++i) {
+    Con &c = in.linear[i];
+    if (fast_encoded(F, c, c_idx, c_subs, sig, &X.alg.app)) { fix_constraint(F, c); lin_touched[i] = 1; }
+    if (lin_touched[i]) X.alg.rowupd += lin0[i] + con_size(c);
+  }
   for (const Sub &s : c_subs) deleted[s.from] = 1;
 
   relevant = relevant_set(&single_idx, &eq_subs, &c_idx);
@@ -656,19 +730,23 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
     }
     for (size_t i = 0; i < l_subs.size(); ++i) l_idx[l_subs[i].from] = (int32_t)i;
     for (auto &c : cons) lconst.push_back(std::move(c));
-    for (Con &c : lconst)
-      if (fast_encoded(F, c, l_idx, l_subs, sig)) fix_constraint(F, c);
+    for (Con &c : lconst) {
+      const uint64_t before = con_size(c);
+      if (fast_encoded(F, c, l_idx, l_subs, sig, &X.alg.app)) { fix_constraint(F, c); X.alg.rowupd += before + con_size(c); }
+    }
   } else {
     for (auto &c : in.linear) lconst.push_back(std::move(c));
   }
 
   // ---- obtain_and_simplify_non_linear (non_linear_utils.rs:6-31)
   std::vector<Con> storage, linear;
-  for (Con &c : in.nonlin) {
-    fast_encoded(F, c, single_idx, eq_subs, sig);
-    fast_encoded(F, c, c_idx, c_subs, sig);
-    fast_encoded(F, c, l_idx, l_subs, sig);
+  for (Con &c : in.nonlin) {  // B_alg: the three frames and the fix are one update of the row
+    const uint64_t before = con_size(c);
+    fast_encoded(F, c, single_idx, eq_subs, sig, &X.alg.app);
+    fast_encoded(F, c, c_idx, c_subs, sig, &X.alg.app);
+    fast_encoded(F, c, l_idx, l_subs, sig, &X.alg.app);
     fix_constraint(F, c);
+    X.alg.rowupd += before + con_size(c);
     if (is_linear(c)) linear.push_back(std::move(c));
     else storage.push_back(std::move(c));
   }
@@ -681,6 +759,7 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
     for (uint32_t s : sig) nl_map[s].push_back((uint32_t)id);
   }
   std::vector<int32_t> r_idx(S, -1);
+  std::vector<uint8_t> round_seen(storage.size(), 0);
   while (apply_round) {
     std::vector<Sub> subs;
     std::vector<Con> constants;
@@ -691,6 +770,8 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
     // for constraint in lconst { for sub in subs { apply } fix }  (:629-634)
     for (size_t i = 0; i < subs.size(); ++i) r_idx[subs[i].from] = (int32_t)i;
     for (Con &c : lconst) {
+      const uint64_t before = con_size(c);
+      bool touched = false;
       if (!subs.empty()) {
         init_map(c.a);
         init_map(c.b);
@@ -700,23 +781,32 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
         for (uint32_t s : sig)
           if (r_idx[s] >= 0) which.push_back(r_idx[s]);
         std::sort(which.begin(), which.end());
-        for (int32_t w : which) apply_substitution(F, c, subs[w].from, subs[w].to);
+        for (int32_t w : which) { apply_substitution(F, c, subs[w].from, subs[w].to); X.alg.app += subs[w].to.size(); }
+        touched = !which.empty();
       }
       fix_constraint(F, c);
+      if (touched) X.alg.rowupd += before + con_size(c);
     }
     for (const Sub &s : subs) r_idx[s.from] = -1;
     // apply_substitution_to_map (:345-396)
     std::vector<uint32_t> linear_id;
+    std::vector<std::pair<uint32_t, uint64_t>> first_touch;  // B_alg: a storage row's round is one update
     for (const Sub &sub : subs) {
       if (nl_map[sub.from].empty()) continue;
       std::vector<uint32_t> c_ids = nl_map[sub.from];
       for (uint32_t cid : c_ids) {
         Con &c = storage[cid];
+        if (!round_seen[cid]) { round_seen[cid] = 1; first_touch.push_back({cid, con_size(c)}); }
+        X.alg.app += sub.to.size();
         apply_substitution(F, c, sub.from, sub.to);
         fix_constraint(F, c);
         if (is_linear(c)) linear_id.push_back(cid);
         for (const Term &t : sub.to) nl_map[t.k].push_back(cid);
       }
+    }
+    for (const auto &ft : first_touch) {
+      X.alg.rowupd += ft.second + con_size(storage[ft.first]);
+      round_seen[ft.first] = 0;
     }
     linear.clear();
     for (uint32_t cid : linear_id) {
@@ -741,6 +831,8 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
   }
   for (Con &c : storage)
     if (!is_empty(c)) out.constraints.push_back(std::move(c));
+  for (const Con &c : out.constraints) X.alg.z_out += con_size(c);
+  X.alg.r_out = out.constraints.size();
   // rebuild_witness (:101-124): the kept signals, ranked
   out.label_to_wire.assign(S, -1);
   int64_t w = 0;
@@ -761,6 +853,7 @@ static void simplification(Ctx &X, Input &in, uint32_t flag_s, uint64_t no_round
 using namespace refcpu;
 
 static thread_local std::string g_err;
+static thread_local uint64_t g_alg[11];  // the last refcpu_simplify's B_alg and its terms (refcpu_last_alg)
 
 static bool load_block(const Ctx &X, const rs_lc &b, std::vector<Con> &rows, int part,
                        bool need_rows) {
@@ -809,6 +902,10 @@ extern "C" {
 
 const char *refcpu_last_error(void) { return g_err.c_str(); }
 
+// The last refcpu_simplify's algorithmic bytes (this thread): out[0] = B_alg, out[1..10] = Z_in, Z_out,
+// subs, app, rowupd, merges (entries), R_in, R_out, max_signal, w (bytes per entry).
+void refcpu_last_alg(uint64_t out[11]) { memcpy(out, g_alg, sizeof g_alg); }
+
 // Runs the canonical restatement on a host rs_input.  *ms = wall time of simplification()
 // alone (input already converted to the oracle's in-memory form), n_threads = pool size.
 int refcpu_simplify(const rs_input *in, const rs_flags *fl, int n_threads, rs_output **out,
@@ -841,9 +938,20 @@ int refcpu_simplify(const rs_input *in, const rs_flags *fl, int n_threads, rs_ou
               load_block(X, in->nl_c, I.nonlin, 2, false);
     if (!ok) { g_err = "invalid input block"; return RS_E_INVALID; }
     Output O;
+    for (const rs_lc *b : {&in->cons_eq, &in->eq, &in->linear, &in->nl_a, &in->nl_b, &in->nl_c}) X.alg.z_in += b->nnz;
+    X.alg.r_in = in->cons_eq.n_rows + in->eq.n_rows + in->linear.n_rows + in->nl_a.n_rows;
     auto t0 = std::chrono::steady_clock::now();
     simplification(X, I, fl->flag_s, fl->no_rounds, fl->use_old_heuristics != 0, O);
     auto t1 = std::chrono::steady_clock::now();
+    {  // refcpu_last_alg: w = 4 + the field's r1cs element size (r1cs_porting.rs:6-10)
+      int bits = 256;
+      while (bits > 1 && !((p[(bits - 1) / 64] >> ((bits - 1) % 64)) & 1)) --bits;
+      const uint64_t fb = bits % 64 == 0 ? bits / 8 : (bits / 64 + 1) * 8, w = 4 + fb;
+      const Alg &a = X.alg;
+      g_alg[0] = w * (a.z_in + a.z_out + a.subs + a.app + a.rowupd + a.merges) + 8 * (a.r_in + a.r_out) + 8 * X.max_signal;
+      g_alg[1] = a.z_in; g_alg[2] = a.z_out; g_alg[3] = a.subs; g_alg[4] = a.app; g_alg[5] = a.rowupd;
+      g_alg[6] = a.merges; g_alg[7] = a.r_in; g_alg[8] = a.r_out; g_alg[9] = X.max_signal; g_alg[10] = w;
+    }
     if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (rounds_out) *rounds_out = O.rounds;
     rs_output *o = (rs_output *)calloc(1, sizeof(rs_output));

@@ -197,6 +197,8 @@ def oracle_lib():
                                         C.POINTER(C.c_uint64)]
         lib.refcpu_simplify.restype = C.c_int
         lib.refcpu_output_free.argtypes = [C.POINTER(RsOutput)]
+        lib.refcpu_last_alg.argtypes = [C.c_uint64 * 11]
+        lib.refcpu_last_alg.restype = None
         lib.refcpu_last_error.restype = C.c_char_p
         lib.refcpu_field_op.argtypes = [C.c_uint64 * 4, C.c_int, C.c_uint64 * 4, C.c_uint64 * 4,
                                         C.c_uint64 * 4]
@@ -318,6 +320,17 @@ def diff_output_arrays(x, y) -> str | None:
             if not np.array_equal(x[nm][i], y[nm][i]):
                 return f"{nm}.{part} differs"
     return None
+
+
+ALG_TERMS = ("B_alg", "z_in", "z_out", "subs", "app", "rowupd", "merges", "r_in", "r_out", "max_signal", "w")
+
+
+def oracle_last_alg() -> dict:
+    """The algorithmic bytes of this thread's last oracle run (refcpu_last_alg: SURVEY 8(d)'s B_alg over
+    the canonical execution's logical operations) and its terms."""
+    a = (C.c_uint64 * 11)()
+    oracle_lib().refcpu_last_alg(a)
+    return dict(zip(ALG_TERMS, (int(x) for x in a)))
 
 
 def oracle_arrays(inp: RsInput, fl: RsFlags, threads=1):

@@ -263,3 +263,44 @@ def test_map_lists_across_rounds(tmp_path):
         for rounds, signals in ((8, 40), (5, 200), (12, 25)):
             out = subprocess.run([exe, str(seed), str(rounds), str(signals)], capture_output=True, text=True)
             assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout
+
+
+def test_refcpu_alg_bytes():
+    """SURVEY 8(d)'s B_alg as the oracle counts it (refcpu_last_alg; the roofline path's numerator in
+    bench.py): deterministic across thread counts, the formula over its terms, Z_in = the input's
+    entries, Z_out / R_out = the result's, and on the docs circuit (basic.circom at --O2) the value
+    counted by hand from the reference's steps."""
+    R = rsio.R
+    for seed, p in ((3, 257), (11, R.PRIMES["bn128"]), (12, R.PRIMES["goldilocks"])):
+        sys_ = rsio.gen_system(seed, p, n_sig=300, n_rows=250, big_cluster=700)
+        h = rsio.InputHolder(sys_)
+        fl = rsio.flags("O2")
+        res = []
+        for threads in (1, 4):
+            arrays, _ = rsio.oracle_arrays(h.inp, fl, threads)
+            res.append(rsio.oracle_last_alg())
+        a = res[0]
+        assert res[0] == res[1]
+        assert a["B_alg"] == a["w"] * (a["z_in"] + a["z_out"] + a["subs"] + a["app"] + a["rowupd"] + a["merges"]) + \
+            8 * (a["r_in"] + a["r_out"] + a["max_signal"])
+        assert a["z_in"] == sum(b.lc.nnz for b in h.blocks)
+        assert a["r_out"] == arrays["n_constraints"]
+        assert a["z_out"] == sum(len(arrays[x][1]) for x in ("a", "b", "c"))
+        assert a["w"] == (12 if p < 2 ** 64 else 36) and a["merges"] > 0  # 4 + r1cs_porting.rs:6-10 field size
+    # basic.circom (constraints-json.md:57-96), counted by hand.  Input: eq rows {2: 1, 5: -1},
+    # {1: -1, 4: 1}; the linear row {0: 1, 2: 2, 3: 1, 6: -1}; the non-linear row [5: -1] * [6: 1] =
+    # [4: -1] -- 11 entries, 4 rows.  eq_simplification: 5 := 2 and 4 := 1 (1 forbidden), 1 entry each;
+    # the eq frame renames nothing in the linear row.  Its cluster (1 row, process_3) pops it: pivot 6
+    # (the largest takeable key), a holder of {0, 2, 3} (row update 4 + 3 entries) and its normalised
+    # copy.  The non-linear row reads the two eq substitutions (both relevant) and the one of 6 (3
+    # entries) and grows from 3 to 5 entries (A {2}, B {0, 2, 3}, C {1}) -- the result (:95-96).
+    p = R.PRIMES["bn128"]
+    m = p - 1
+    rows = [R.Con({}, {}, {2: 1, 5: m}), R.Con({}, {}, {0: 1, 2: 2, 3: 1, 6: m}),
+            R.Con({}, {}, {1: m, 4: 1}), R.Con({5: m}, {6: 1}, {4: m})]
+    h = rsio.InputHolder(R.System(p, 7, 1, 0, 2, {0, 1}, rows))
+    arrays, _ = rsio.oracle_arrays(h.inp, rsio.flags("O2"), 1)
+    a = rsio.oracle_last_alg()
+    assert (a["z_in"], a["r_in"], a["r_out"], a["z_out"]) == (11, 4, 1, 5)
+    assert (a["subs"], a["app"], a["rowupd"], a["merges"]) == (2 + 3 + 3, 1 + 1 + 3, (4 + 3) + (3 + 5), 0), a
+    assert a["B_alg"] == 36 * (11 + 5 + 8 + 5 + 15) + 8 * (4 + 1 + 7)
