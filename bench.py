@@ -97,6 +97,14 @@ KERNELS = (  # (name, stats fields: ms, bytes, launches)
     ("k_big_main<256> (tail)", "tail_main_ms", "tail_main_bytes", "tail_launches"),
     ("k_frames_wave<0> (non-linear)", "apply_kernel_ms", "apply_bytes", "apply_kernel_launches"),
     ("k_frames_wave<1> (rounds)", "round_fill_ms", "round_fill_bytes", "round_fill_launches"),
+    # ABI 8: the rest of the elimination and the clustering (HIP events on their own streams)
+    ("k_batch_inv_flat + k_big_finish<4> (tail normalisation + composition)", "tail_fin_ms", "tail_fin_bytes",
+     "tail_fin_launches"),
+    ("k_batch_inv_tree .. k_big_emit (head normalisation + composition)", "head_fin_ms", "head_fin_bytes",
+     "head_fin_launches"),
+    ("k_eliminate (clusters under 32 rows)", "small_ms", "small_bytes", "small_launches"),
+    ("build_clusters (k_cl_*, pair sort, arena replays)", "cluster_dev_ms", "cluster_bytes", "cluster_launches"),
+    ("k_gi_* (giant clusters' component loops)", "giant_ms", "giant_bytes", "giant_launches"),
 )
 
 
@@ -172,20 +180,21 @@ def flatten_bench(seed: int, prime: str, mids: int = 12000, leaves: int = 20, re
     want = {"cons_eq": 4 * n_leaf, "eq": 10 * n_leaf + leaves * mids, "linear": 14 * n_leaf + 2,
             "nl": 12 * n_leaf}
     times, ok = [], True
+    eng = M.Engine(0)
     for _ in range(reps):
         t0 = time.perf_counter()
-        inp = dag.flatten(0)
+        c = eng.flatten_dag(dag)
         times.append(time.perf_counter() - t0)
-        c = inp.c
         got = {"cons_eq": c.cons_eq.n_rows, "eq": c.eq.n_rows, "linear": c.linear.n_rows, "nl": c.nl_a.n_rows}
         ok &= got == want and c.max_signal == 1 + 3 + mids * (L_MID + leaves * L_LEAF)
-        inp.free()
+    eng.close()
     n = sum(want.values())
     best = min(times)
     return {"ms": round(best * 1e3, 2), "constraints": n, "instances": 1 + mids * (1 + leaves),
             "value": round(n / best, 1), "unit": "constraints/s", "counts_ok": bool(ok),
-            "what": "rs_flatten_dag host DAG -> host rs_input (templates up, every instance's rows classified "
-                    "and offset on the device, blocks back over PCIe), best of %d" % reps}
+            "what": "rs_engine_flatten_dag host DAG -> host rs_input in the engine's page-locked buffers "
+                    "(templates up, every instance's rows classified and offset on the device, blocks back "
+                    "over PCIe at link speed), best of %d" % reps}
 
 
 def _prime_value(name: str) -> int:
@@ -392,7 +401,7 @@ def main():
                          "launches_per_step": dom["launches_per_step"],
                          "path": {"alg_bytes_per_step": int(tot["alg_bytes"] / K), "T_simplify_ms": round(ms_step, 3),
                                   "achieved": round(path_ach, 2), "frac": round(path_ach / HBM_PEAK_GBS, 5)},
-                         "kernels": {k: kline(k) for k in acc}},
+                         "kernels": {k: kline(k) for k in acc if acc[k][2]}},
             "phases_ms": {"device_run": round(tot["total_ms"] / K, 3), "h2d_wait": round(tot["h2d_wait_ms"] / K, 3),
                           "d2h": round(tot["d2h_ms"] / K, 3), "host_total": round(tot["host_total_ms"] / K, 3)},
             "last_step": {k: round(getattr(last, k), 2) for k in

@@ -46,34 +46,61 @@ class RsOutput(C.Structure):
                 ("n_labels", C.c_uint64), ("label_to_wire", C.POINTER(C.c_int32)),
                 ("n_wires", C.c_uint64), ("no_private_inputs_witness", C.c_uint64),
                 ("n_log", C.c_uint64), ("log_from", C.POINTER(C.c_uint32)), ("log_to", RsLc),
-                ("a_end", C.POINTER(C.c_uint64)), ("b_end", C.POINTER(C.c_uint64)), ("c_end", C.POINTER(C.c_uint64))]
+                ("a_len", C.POINTER(C.c_uint32)), ("b_len", C.POINTER(C.c_uint32)), ("c_len", C.POINTER(C.c_uint32)),
+                ("a_jump", C.POINTER(C.c_uint64)), ("b_jump", C.POINTER(C.c_uint64)), ("c_jump", C.POINTER(C.c_uint64)),
+                ("a_njump", C.c_uint64), ("b_njump", C.c_uint64), ("c_njump", C.c_uint64)]
 
     def block(self, q: int):
-        """(rs_lc, its row ends or None) of part q = 0/1/2 (a/b/c)."""
+        """(rs_lc, its ABI 8 row layout (len, jump, n_jump) or None for CSR) of part q = 0/1/2 (a/b/c)."""
         lc = (self.a, self.b, self.c)[q]
-        end = (self.a_end, self.b_end, self.c_end)[q]
-        return lc, (end if end else None)
+        ln = (self.a_len, self.b_len, self.c_len)[q]
+        if not ln:
+            return lc, None
+        return lc, (ln, (self.a_jump, self.b_jump, self.c_jump)[q], int((self.a_njump, self.b_njump, self.c_njump)[q]))
 
 
-def block_csr(lc: "RsLc", end=None):
+ROW_JUMP = 0x80000000
+
+
+def row_starts(lens: np.ndarray, jumps: np.ndarray) -> np.ndarray:
+    """The storage start of every row of ABI 8's streamed layout (rs_rows_next, include/rs_simplify.h):
+    a row starts where the previous one ended unless RS_ROW_JUMP is set, then at the next jump."""
+    n = lens.shape[0]
+    j = (lens & ROW_JUMP) != 0
+    ln = (lens & ~np.uint32(ROW_JUMP)).astype(np.int64)
+    if int(j.sum()) != jumps.shape[0]:
+        raise ValueError("row layout: %d jumping rows, %d jump offsets" % (int(j.sum()), jumps.shape[0]))
+    seg = np.cumsum(j) - 1  # the jump each row's run starts from (-1: the run from offset 0)
+    last = np.maximum.accumulate(np.where(j, np.arange(n), -1)) if n else np.zeros(0, np.int64)
+    ex = np.zeros(n + 1, np.int64)
+    np.cumsum(ln, out=ex[1:])
+    base = np.where(seg >= 0, jumps.astype(np.int64)[np.maximum(seg, 0)] if jumps.size else 0, 0)
+    return base + ex[:-1] - np.where(last >= 0, ex[np.maximum(last, 0)], 0)
+
+
+def block_csr(lc: "RsLc", layout=None):
     """Copies of one result block as compact CSR numpy arrays (ptr u64[n+1], col u32, val u64[4 nnz]):
-    a block with row ends (ABI 7, rs_engine_simplify's streamed layout) is compacted row by row."""
+    a block in ABI 8's streamed layout (row lengths + jumps) is compacted row by row."""
     n = int(lc.n_rows)
     if n == 0:
         return np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint64)
-    beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,)).copy()
     ext = int(lc.nnz)
     col = np.ctypeslib.as_array(lc.col, shape=(max(ext, 1),))
     val = np.ctypeslib.as_array(lc.val, shape=(max(ext, 1) * 4,))
-    if end is None:
+    if layout is None:
+        beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,)).copy()
         nnz = int(beg[n])
         return beg, col[:nnz].copy(), val[:4 * nnz].copy()
-    e = np.ctypeslib.as_array(end, shape=(n,)).astype(np.int64)
-    b = beg[:n].astype(np.int64)
-    lens = e - b
+    lp, jp, nj = layout
+    lens = np.ctypeslib.as_array(lp, shape=(n,))
+    jumps = np.ctypeslib.as_array(jp, shape=(nj,)) if nj else np.zeros(0, np.uint64)
+    b = row_starts(lens, jumps)
+    ln = (lens & ~np.uint32(ROW_JUMP)).astype(np.int64)
+    if n and int((b + ln).max()) > ext:
+        raise ValueError("row layout reaches past the block's entries")
     ptr = np.zeros(n + 1, np.uint64)
-    np.cumsum(lens, out=ptr[1:])
-    idx = np.repeat(b - ptr[:-1].astype(np.int64), lens) + np.arange(int(ptr[n]), dtype=np.int64)
+    np.cumsum(ln, out=ptr[1:])
+    idx = np.repeat(b - ptr[:-1].astype(np.int64), ln) + np.arange(int(ptr[n]), dtype=np.int64)
     v4 = val[: 4 * ext].reshape(-1, 4)
     return ptr, col[idx].copy(), v4[idx].reshape(-1).copy()
 
@@ -95,7 +122,8 @@ class RsStats(C.Structure):
                 ("tail_main_ms", C.c_double), ("tail_main_bytes", C.c_uint64), ("tail_launches", C.c_uint64),
                 ("round_fill_ms", C.c_double), ("round_fill_bytes", C.c_uint64),
                 ("round_fill_launches", C.c_uint64), ("alg_bytes", C.c_uint64), ("h2d_wait_ms", C.c_double),
-                ("d2h_ms", C.c_double), ("host_total_ms", C.c_double), ("write_ms", C.c_double)]
+                ("d2h_ms", C.c_double), ("host_total_ms", C.c_double), ("write_ms", C.c_double),
+                ("tail_fin_ms", C.c_double), ("tail_fin_bytes", C.c_uint64), ("tail_fin_launches", C.c_uint64), ("head_fin_ms", C.c_double), ("head_fin_bytes", C.c_uint64), ("head_fin_launches", C.c_uint64), ("small_ms", C.c_double), ("small_bytes", C.c_uint64), ("small_launches", C.c_uint64), ("prep_ms", C.c_double), ("prep_launches", C.c_uint64), ("cluster_dev_ms", C.c_double), ("cluster_bytes", C.c_uint64), ("cluster_launches", C.c_uint64), ("giant_ms", C.c_double), ("giant_bytes", C.c_uint64), ("giant_launches", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -148,6 +176,7 @@ SYMBOLS = [
     ("rs_write_substitution_json", C.c_int, [C.c_char_p, C.POINTER(RsOutput)]),
     ("rs_synth", C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.POINTER(RsInput))]),
     ("rs_flatten_dag", C.c_int, [C.c_int, C.POINTER(RsDag), C.POINTER(C.POINTER(RsInput))]),
+    ("rs_engine_flatten_dag", C.c_int, [C.c_void_p, C.POINTER(RsDag), C.POINTER(C.POINTER(RsInput))]),
 ]
 
 _LIB = None
@@ -267,6 +296,13 @@ class Engine:
         check(lib().rs_engine_simplify(self._h, C.byref(inp), C.byref(flags), C.byref(out)))
         return out.contents
 
+    def flatten_dag(self, dag) -> RsInput:
+        """rs_engine_flatten_dag: `dag` (circom_cvm_amd.Dag) flattened into this engine's page-locked
+        buffers; the returned struct views them until the next flatten_dag on this engine."""
+        p = C.POINTER(RsInput)()
+        check(lib().rs_engine_flatten_dag(self._h, C.byref(dag.c), C.byref(p)))
+        return p.contents
+
     def inject_fault(self, where: int = 1):
         """rs_engine_inject_fault: the next run / simplify on this engine fails at `where` (tests)."""
         check(lib().rs_engine_inject_fault(self._h, where))
@@ -297,7 +333,9 @@ class Output:
 
     @property
     def c(self) -> RsOutput:
-        return self.ptr.contents
+        s = self.ptr.contents
+        s._owner = self  # the struct keeps its owner (and so the library's buffers) alive
+        return s
 
     def free(self):
         if self.ptr:
@@ -319,7 +357,9 @@ class Input:
 
     @property
     def c(self) -> RsInput:
-        return self.ptr.contents
+        s = self.ptr.contents
+        s._owner = self
+        return s
 
     @staticmethod
     def read_r1cs(path: str) -> "Input":

@@ -11,7 +11,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librs_simplify.so")
 CLI = os.path.join(PKG, "circom-simplify")
 SOURCES = ["engine.hip", "r1cs_io.cpp", "synth.cpp", "host_common.cpp"]
-HEADERS = ["field.hpp", "kernels.hpp", "frames_wave.hpp", "spec_loop.hpp", "output.hpp", "flatten.hpp", "cluster.hpp", "writer.hpp", "comm.hpp", "host_common.hpp", os.path.join("..", "..", "include", "rs_simplify.h")]
+HEADERS = ["field.hpp", "kernels.hpp", "frames_wave.hpp", "spec_loop.hpp", "giant_loop.hpp", "output.hpp", "flatten.hpp", "cluster.hpp", "writer.hpp", "comm.hpp", "host_common.hpp", os.path.join("..", "..", "include", "rs_simplify.h")]
 
 
 def _stale(target, deps):

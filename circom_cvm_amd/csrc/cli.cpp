@@ -63,9 +63,14 @@ int main(int argc, char **argv) {
   }
   // constraint_writers/src/log_writer.rs:24-47
   uint64_t nl = 0, l = 0;
+  rs_rows ia, ib;
+  rs_rows_begin(o, 0, &ia);
+  rs_rows_begin(o, 1, &ib);
   for (uint64_t r = 0; r < o->n_constraints; ++r) {
-    bool lin = o->a.ptr[r] == rs_row_end(&o->a, o->a_end, r) && o->b.ptr[r] == rs_row_end(&o->b, o->b_end, r);
-    (lin ? l : nl)++;
+    uint64_t ba, la, bb, lb;
+    rs_rows_next(&ia, r, &ba, &la);
+    rs_rows_next(&ib, r, &bb, &lb);
+    ((la | lb) == 0 ? l : nl)++;
   }
   printf("non-linear constraints: %llu\n", (unsigned long long)nl);
   printf("linear constraints: %llu\n", (unsigned long long)l);

@@ -31,6 +31,7 @@
 #include "kernels.hpp"
 #include "frames_wave.hpp"
 #include "spec_loop.hpp"
+#include "giant_loop.hpp"
 #include "cluster.hpp"
 #include "writer.hpp"
 #include "maplists.hpp"
@@ -229,8 +230,10 @@ struct rs_engine {
     void *p = nullptr;
     size_t cap = 0;
   };
-  Pin pin[20];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers;
-                // a/b/c row ends (streamed result); [16..17] the host replay's staging
+  Pin pin[40];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers;
+                // a/b/c row ends (streamed result); [16..17] the host replay's staging; [20..38]
+                // rs_engine_flatten_dag's result (19 arrays)
+  rs_input flat_view{};  // rs_engine_flatten_dag's result (views pin[20..38])
   rs_output view{};
   // streamed result (output.hpp; rs_engine_simplify): the storage rows final after round 1 go to
   // pin[3..8] on the copy stream during the later rounds (ev_snap: their D2H is done)
@@ -271,6 +274,13 @@ struct rs_engine {
   hipStream_t stx = nullptr;  // the early region's D2H stream
   hipStream_t str = nullptr;  // the host replay's copies (small; never behind the bulk copies)
   hipStream_t ste = nullptr;  // the small clusters' elimination (k_eliminate), beside the tail's chain
+  hipStream_t stg = nullptr;  // the giant clusters' component loops (giant_loop.hpp), beside the head's
+  hipEvent_t evg[2] = {};     // giant path: fork after the head's preparation / join before its inversion
+  // per-kernel timing (rs_stats ABI 8): the tail groups' [prep, after prep + p3_fast, after the loop,
+  // after the inversion, after the finish]; build_clusters' device span; the giant path's span
+  hipEvent_t evt[2][5] = {};
+  hipEvent_t evc[2] = {};
+  hipEvent_t evgt[3] = {};
   hipEvent_t ev_sm[3] = {};   // its start / k_eliminate done / its work done (the tail's second group too)
   hipEvent_t ev_chunk[2] = {};
   int snap_rc = 0;
@@ -281,6 +291,7 @@ struct rs_engine {
   // heap as the run left them; nothing between the run and ensure_csr may move them (fin_gen = the
   // arena generation then; ensure_csr refuses a stale view instead of gathering from freed memory).
   DRows fin_parts[3] = {}, fin_xq[2][3] = {};  // storage rows; extras: leftover linear rows, lconst
+  uint64_t out_njump[3] = {0, 0, 0};  // ABI 8: rows of the streamed layout that jump, per part
   const uint32_t *fin_keep_ids = nullptr, *fin_x_ids[2] = {nullptr, nullptr};
   uint64_t fin_keep = 0, fin_xn[2] = {0, 0}, fin_gen = 0;
 };
@@ -607,12 +618,21 @@ __global__ void k_append_marks(const uint32_t *usig, const uint64_t *uoff, const
 
 template <class K, class V>
 static void sort_pairs(rs_engine *E, const K *kin, K *kout, const V *vin, V *vout, uint64_t n, int end_bit,
-                       const char *tag) {
+                       const char *tag, hipStream_t s = nullptr) {
+  if (!n) return;
+  if (!s) s = E->st;
+  size_t tb = 0;
+  HC(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, s));
+  void *tmp = E->A.get<uint8_t>(std::string("sort.tmp.") + tag, tb);
+  HC(rocprim::radix_sort_pairs(tmp, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, s));
+}
+// device-only exclusive scan of u32 on stream s (no read-back; tmp sized on first use)
+static void dev_scan_u32(rs_engine *E, const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s, const char *tag) {
   if (!n) return;
   size_t tb = 0;
-  HC(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, E->st));
-  void *tmp = E->A.get<uint8_t>(std::string("sort.tmp.") + tag, tb);
-  HC(rocprim::radix_sort_pairs(tmp, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, E->st));
+  HC(rocprim::exclusive_scan(nullptr, tb, in, out, (uint32_t)0, (size_t)n, rocprim::plus<uint32_t>(), s));
+  void *tmp = E->A.get<uint8_t>(std::string("dscan.tmp.") + tag, tb);
+  HC(rocprim::exclusive_scan(tmp, tb, in, out, (uint32_t)0, (size_t)n, rocprim::plus<uint32_t>(), s));
 }
 
 template <class K>
@@ -1025,6 +1045,11 @@ struct DevClusters {
   // the largest clusters' row orders are still being replayed on the second stream (evx[7] marks
   // the end); only the head -- ordered after the replay on that stream -- reads them until the join
   bool join_pending = false;
+  // host copy of the sorted size keys of the kHeadLimit largest clusters (k_cl_sizekey: size in the
+  // high word, inverted; the cluster index in the low word)
+  std::vector<uint64_t> top_keys;
+  bool timed = false;  // evc[0..1] bracket the clustering kernels
+  uint64_t alg = 0;    // their algorithmic bytes
 };
 // Split composition (k_big_finish with ElimArgs.split, then one k_compose_level launch per Kahn
 // level of every cluster at once over the whole GPU, k_big_emit at the end).  Level L reads count
@@ -1120,6 +1145,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   D.cl_off = A.get<uint64_t>("el.cl", 1);
   HC(hipMemsetAsync(D.cl_off, 0, 8, st));
   if (n == 0) return D;
+  HC(hipEventRecord(E->evc[0], st));
   uint64_t *npairs = A.get<uint64_t>("cl.np", n);
   unsigned long long *stat = A.get<unsigned long long>("cl.stat", 8);
   HC(hipMemsetAsync(stat, 0, 64, st));
@@ -1132,6 +1158,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   D.tot_nnz = hs[0];
   const uint64_t n_act = hs[1];
   if (n_act == 0) return D;
+  D.timed = true;
   int sbits = 1;
   while (sbits < 32 && (1ull << sbits) <= E->S) ++sbits;
   uint32_t *uf = A.get<uint32_t>("cl.uf", n);
@@ -1176,10 +1203,13 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   launch_capped(st, k_cl_sizekey, n_cl, 1024, (const uint64_t *)D.cl_off, n_cl, (const uint32_t *)srow, (const uint32_t *)V.len, sk, si, cnt);
   sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
   unsigned long long hc[5];
-  uint64_t first = 0;
+  // the size keys of the largest clusters (the head's; the giant path reads their row counts)
+  const uint64_t n_top = std::min<uint64_t>(n_cl, kHeadLimit);
+  D.top_keys.assign(n_top, 0);
   HC(hipMemcpyAsync(hc, cnt, 40, hipMemcpyDeviceToHost, st));
-  HC(hipMemcpyAsync(&first, sk2, 8, hipMemcpyDeviceToHost, st));
+  HC(hipMemcpyAsync(D.top_keys.data(), sk2, 8 * n_top, hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
+  const uint64_t first = n_top ? D.top_keys[0] : 0;
   // replay of the arena merges -> row order inside every cluster
   D.perm = A.get<uint32_t>("el.perm", n_act);
   uint32_t *c2c = A.get<uint32_t>("cl.c2c", n_act), *tail = A.get<uint32_t>("cl.tail", n_act);
@@ -1298,6 +1328,11 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   D.cid = cid;
   eo.n_clusters = n_cl;
   eo.n_slots = n_act;
+  HC(hipEventRecord(E->evc[1], st));
+  // its algorithmic bytes: the rows' keys read twice (count, fill), each (signal, row) pair written,
+  // sorted (one read and one write) and linked (read, prev written), ~8 words per row over the
+  // union-find / root / key / order passes, the replay stream written and read
+  D.alg = 8 * D.tot_nnz + 52 * P + 32 * n + 8 * Q;
   E->stats.n_clusters += n_cl;
   E->stats.max_cluster = std::max<uint64_t>(E->stats.max_cluster, (0xffffffffull - (first >> 32)) & 0x7fffffffull);
   return D;
@@ -1384,6 +1419,114 @@ static void shard_exchange(rs_engine *E, const ElimArgs &a, const DevClusters &D
   G.cap = te;  // entries in use
   E->stats.exchange_ms += now_ms() - t0;
   E->stats.exchange_bytes += sizeof(XRec) * (ts + tl) + 36 * te + 24 * CM.world;
+}
+
+// ---- the giant path (giant_loop.hpp): head clusters of kGiantRows rows or more
+// Buffers for a giant cluster of n rows (allocated before any launch of the round: a growing arena
+// buffer is freed with hipFree, which waits for the whole device).
+static GiantArgs giant_buffers(rs_engine *E, uint64_t n) {
+  Arena &A = E->A;
+  GiantArgs G{};
+  G.n = n;
+  G.uf = A.get<uint32_t>("gi.uf", E->S);
+  G.gst = A.get<uint64_t>("gi.gst", E->S);
+  G.rkey = A.get<uint64_t>("gi.rkey", n);
+  G.rkey2 = A.get<uint64_t>("gi.rkey2", n);
+  G.rval = A.get<uint32_t>("gi.rval", n);
+  G.rval2 = A.get<uint32_t>("gi.rval2", n);
+  G.comp_of = A.get<uint32_t>("gi.comp_of", n);
+  G.c_start = A.get<uint32_t>("gi.c_start", n);
+  G.c_size = A.get<uint32_t>("gi.c_size", n);
+  G.ckey = A.get<uint64_t>("gi.ckey", n);
+  G.ckey2 = A.get<uint64_t>("gi.ckey2", n);
+  G.cidx = A.get<uint32_t>("gi.cidx", n);
+  G.cidx2 = A.get<uint32_t>("gi.cidx2", n);
+  G.c_nsub = A.get<uint32_t>("gi.c_nsub", n);
+  G.c_nleft = A.get<uint32_t>("gi.c_nleft", n);
+  G.c_dsub = A.get<uint32_t>("gi.c_dsub", n);
+  G.scal = A.get<uint32_t>("gi.scal", 8);
+  G.t_sig = A.get<uint32_t>("gi.t_sig", n);
+  G.t_coef = A.get<Fe>("gi.t_coef", n);
+  G.t_off = A.get<uint64_t>("gi.t_off", n);
+  G.t_len = A.get<uint32_t>("gi.t_len", n);
+  G.lmark = A.get<uint32_t>("gi.lmark", n);
+  G.lscan = A.get<uint32_t>("gi.lscan", n);
+  G.tl_off = A.get<uint64_t>("gi.tl_off", n);
+  G.tl_len = A.get<uint32_t>("gi.tl_len", n);
+  if (g_prof_env) {
+    G.c_merges = A.get<uint32_t>("gi.c_merges", n);
+    G.c_clk = A.get<uint64_t>("gi.c_clk", n);
+    G.sec = A.get<unsigned long long>("gi.sec", 8);
+  }
+  size_t tb = 0;  // the sorts' and scans' temporaries at their final size
+  HC(rocprim::radix_sort_pairs(nullptr, tb, G.rkey, G.rkey2, G.rval, G.rval2, (size_t)n, 0, 64, E->stg));
+  (void)A.get<uint8_t>("sort.tmp.gi", tb);
+  tb = 0;
+  HC(rocprim::exclusive_scan(nullptr, tb, G.c_nsub, G.c_dsub, (uint32_t)0, (size_t)n, rocprim::plus<uint32_t>(), E->stg));
+  (void)A.get<uint8_t>("dscan.tmp.gi", tb);
+  return G;
+}
+// The giant path of head cluster c (position ci in the head list) on E->stg: components, the
+// component loops, the results back into the cluster's slots (n_sub / n_left set at the end).
+static void giant_launch(rs_engine *E, const ElimArgs &a, GiantArgs G, uint64_t c, uint64_t ci) {
+  hipStream_t s = E->stg;
+  G.ci = ci;
+  const uint64_t n = G.n;
+  const unsigned gb = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_gi_state, dim3(gb), dim3(256), 0, s, a, G, c);
+  hipLaunchKernelGGL(k_gi_union, dim3(gb), dim3(256), 0, s, a, G, c);
+  hipLaunchKernelGGL(k_gi_rowkey, dim3(gb), dim3(256), 0, s, a, G, c);
+  HC(hipGetLastError());
+  sort_pairs(E, (const uint64_t *)G.rkey, G.rkey2, (const uint32_t *)G.rval, G.rval2, n, 64, "gi", s);
+  hipLaunchKernelGGL(k_gi_segment, dim3(1), dim3(1024), 0, s, a, G);
+  HC(hipGetLastError());
+  sort_pairs(E, (const uint64_t *)G.ckey, G.ckey2, (const uint32_t *)G.cidx, G.cidx2, n, 64, "gi", s);
+  if (g_prof_env) {
+    HC(hipMemsetAsync(G.sec, 0, 64, s));
+    HC(hipStreamSynchronize(s));
+  }
+  const double tl0 = g_prof_env ? now_ms() : 0.0;
+  hipLaunchKernelGGL(k_gi_loop<kGiNW>, dim3((unsigned)std::min<uint64_t>(n, 512)), dim3(kGiT), 0, s, a, G, c);
+  HC(hipGetLastError());
+  if (g_prof_env) {  // the components' loops: count, the largest by time, merges per microsecond
+    HC(hipStreamSynchronize(s));
+    const double tl1 = now_ms();
+    uint32_t nc = 0;
+    HC(hipMemcpy(&nc, G.scal, 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> sz(nc), mg(nc);
+    std::vector<uint64_t> ck(nc);
+    if (nc) {
+      HC(hipMemcpy(sz.data(), G.c_size, 4 * nc, hipMemcpyDeviceToHost));
+      HC(hipMemcpy(mg.data(), G.c_merges, 4 * nc, hipMemcpyDeviceToHost));
+      HC(hipMemcpy(ck.data(), G.c_clk, 8 * nc, hipMemcpyDeviceToHost));
+    }
+    std::vector<uint32_t> ord(nc);
+    for (uint32_t i = 0; i < nc; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return ck[x] > ck[y]; });
+    uint64_t tm = 0, tc = 0;
+    for (uint32_t i = 0; i < nc; ++i) { tm += mg[i]; tc += ck[i]; }
+    fprintf(stderr, "[rs-prof] giant %llu rows: %u components, %llu merges, loop %.1f ms (sum of component times %.1f ms)\n",
+            (unsigned long long)n, nc, (unsigned long long)tm, tl1 - tl0, tc / 1e5);
+    for (uint32_t i = 0; i < nc && i < 8; ++i)
+      fprintf(stderr, "[rs-prof]   component rows %u merges %u: %.1f ms (%.2f us/merge)\n", sz[ord[i]], mg[ord[i]], ck[ord[i]] / 1e5,
+              mg[ord[i]] ? ck[ord[i]] / 1e2 / mg[ord[i]] : 0.0);
+    unsigned long long sec[8];
+    HC(hipMemcpy(sec, G.sec, 64, hipMemcpyDeviceToHost));
+    const double tot = (double)(sec[0] + sec[1] + sec[2] + sec[3] + sec[4] + sec[5] + sec[6] + sec[7]);
+    fprintf(stderr, "[rs-prof]   loop sections (clocks per merge; share): pivot %.0f %.2f | holder header %.0f %.2f | rhs %.0f %.2f | "
+            "search+product %.0f %.2f | scan %.0f %.2f | scatter %.0f %.2f | row start %.0f %.2f | other %.0f %.2f\n",
+            sec[0] / (double)std::max<uint64_t>(tm, 1), sec[0] / tot, sec[1] / (double)std::max<uint64_t>(tm, 1), sec[1] / tot,
+            sec[2] / (double)std::max<uint64_t>(tm, 1), sec[2] / tot, sec[3] / (double)std::max<uint64_t>(tm, 1), sec[3] / tot,
+            sec[4] / (double)std::max<uint64_t>(tm, 1), sec[4] / tot, sec[5] / (double)std::max<uint64_t>(tm, 1), sec[5] / tot,
+            sec[6] / (double)std::max<uint64_t>(tm, 1), sec[6] / tot, sec[7] / (double)std::max<uint64_t>(tm, 1), sec[7] / tot);
+  }
+  dev_scan_u32(E, G.c_nsub, G.c_dsub, n, s, "gi");
+  hipLaunchKernelGGL(k_gi_gather, dim3(gb), dim3(256), 0, s, a, G, c);
+  HC(hipGetLastError());
+  dev_scan_u32(E, G.lmark, G.lscan, n, s, "gi");
+  hipLaunchKernelGGL(k_gi_scatter, dim3(gb), dim3(256), 0, s, a, G, c);
+  hipLaunchKernelGGL(k_gi_fin, dim3(1), dim3(64), 0, s, a, G, c);
+  HC(hipGetLastError());
 }
 
 // Runs linear_simplification (:275-325) for the rows of `view`; on return the per-slot arrays in
@@ -1481,9 +1624,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     // compositions sort unless the sort cannot take them (merging the short ones too was 45 % slower
     // on the metric circuit's tail, equal on templated)
     a.compose_sort = 1;
-    // in-kernel algorithmic-byte counters: [0] k_eliminate / composition emits, [1] / [2] the head's
-    // k_big_main / normalisation + composition, [3] / [4] the tail's
-    a.bytes = E->A.get<unsigned long long>("el.bytes", 5);
+    // in-kernel algorithmic-byte counters: [0] k_eliminate, [1] / [2] the head's ordered loop /
+    // inversion + normalisation + composition + emit, [3] / [4] the tail's, [7] the giant path
+    a.bytes = E->A.get<unsigned long long>("el.bytes", 8);
     a.big_touch_off = E->A.get<uint64_t>("el.bt_off", std::max<uint64_t>(n_big, 1));
     a.big_touch_n = E->A.get<uint32_t>("el.bt_n", std::max<uint64_t>(n_big, 1));
     a.big_alive = E->A.get<uint32_t>("el.alive", std::max<uint64_t>(n_big, 1));
@@ -1494,7 +1637,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     if (a.prof) HC(hipMemsetAsync(a.prof, 0, 8 * kProfWords * n_big, E->st));
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
-    HC(hipMemsetAsync(a.bytes, 0, 40, E->st));
+    HC(hipMemsetAsync(a.bytes, 0, 64, E->st));
     // The largest clusters' prep -> main -> finish chain runs on a second stream: the elimination
     // time is the critical path of the largest cluster, and everything else overlaps it.
     const uint64_t n_head = std::min<uint64_t>(n_big, kHeadLimit), n_tail = n_big - n_head;
@@ -1509,6 +1652,22 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     at.big_alive += n_head;
     if (at.prof) at.prof += kProfWords * n_head;
     at.split = 0;
+    // the head's giant clusters (rows >= kGiantRows, from the size keys the clustering read back): the
+    // component loops of giant_loop.hpp on their own stream; k_big_spec skips them
+    std::vector<uint64_t> giants;  // head positions
+    for (uint64_t i = 0; i < n_head && i < D.top_keys.size(); ++i)
+      if (((0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull) >= kGiantRows) giants.push_back(i);
+    uint64_t giant_rows = 0;
+    for (uint64_t i : giants) giant_rows = std::max<uint64_t>(giant_rows, (0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull);
+    GiantArgs GA{};
+    ElimArgs aspec = a;  // the speculative loop's arguments: the giants flagged in skip
+    if (!giants.empty()) {
+      GA = giant_buffers(E, giant_rows);
+      uint8_t *gskip = E->A.get<uint8_t>("gi.skip", n_head);
+      HC(hipMemsetAsync(gskip, 0, n_head, E->st));
+      for (uint64_t i : giants) HC(hipMemsetAsync(gskip + i, 1, 1, E->st));
+      aspec.skip = gskip;
+    }
     ElimArgs ah = a;  // the head: split composition (k_big_finish -> k_compose_level per level -> k_big_emit)
     uint64_t *cf_next = nullptr;
     if (n_head) {
@@ -1529,6 +1688,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     // GPU like the head's was slower on the metric circuit, 15 vs 6.6 ms)
     constexpr uint32_t kHeadLevels = 36;
     LevelLoop hl;
+    int n_tgroups = 0;  // tail groups launched (their evt events are recorded)
     if (eo.n_clusters) {
       HC(hipEventRecord(E->ev2, E->st));
       if (n_head) {
@@ -1550,13 +1710,28 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[2], E->st2));
         HC(hipEventRecord(E->evx[10], E->st2));
+        if (!giants.empty()) {  // beside the speculative loop, joined before the head's inversion
+          HC(hipStreamWaitEvent(E->stg, E->evx[10], 0));
+          HC(hipEventRecord(E->evgt[0], E->stg));
+          ElimArgs ag = a;
+          ag.bytes_main = a.bytes + 7;
+          for (uint64_t i : giants) {
+            GiantArgs G = GA;
+            G.n = (0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull;
+            giant_launch(E, ag, G, D.top_keys[i] & 0xffffffffull, i);
+          }
+          HC(hipEventRecord(E->evgt[1], E->stg));
+          HC(hipEventRecord(E->evg[1], E->stg));
+        }
         // the ordered loop: twelve waves reduce rows speculatively against the LDS signal table and
         // commit in pop order (spec_loop.hpp).  12 vs 8 waves (three per SIMD at <= 168 VGPRs, 152 B of
         // spills): the metric circuit's largest cluster 12.9 -> 12.0 ms (the turns that wait for a row
         // still reducing: 4.5 -> 3.0 ms), templated 26.7 -> 28.1 ms (its chains conflict at distance 1)
-        hipLaunchKernelGGL(k_big_spec<12>, dim3(g), dim3(768), 0, E->st2, a, (const uint32_t *)d_big, n_head);
+        hipLaunchKernelGGL(k_big_spec<12>, dim3(g), dim3(768), 0, E->st2, aspec, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
         HC(hipEventRecord(E->evx[3], E->st2));
+        if (!giants.empty()) HC(hipStreamWaitEvent(E->st2, E->evg[1], 0));
+        HC(hipEventRecord(E->evgt[2], E->st2));  // the head's composition chain starts (after the giants)
         // one inversion per head cluster
         hipLaunchKernelGGL(k_batch_inv_tree, dim3(g), dim3(256), 0, E->st2, a, (const uint32_t *)d_big, n_head);
         HC(hipGetLastError());
@@ -1584,16 +1759,21 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       }
       HC(hipEventRecord(E->ev_sm[1], E->ste));
       HC(hipEventRecord(E->evx[5], E->st));
+      n_tgroups = 0;
       if (n_tail) {
         // The tail in two groups on two streams: its kTailSplit largest clusters on the main stream
         // (their ordered loops are the tail's latency), the rest -- most of the composition work,
         // which fills the GPU -- beside them on the small clusters' stream, after k_eliminate.  One
         // launch per kernel over all of them made every finish wait for the largest loops.
         const uint64_t n_t1 = n_tail > kTailSplit + kTailSplit / 4 ? kTailSplit : n_tail, n_t2 = n_tail - n_t1;
-        auto tail_group = [&](hipStream_t s, ElimArgs g, const uint32_t *ids, uint64_t n, const char *cls_name, bool timed) {
+        n_tgroups = n_t2 ? 2 : 1;
+        auto tail_group = [&](hipStream_t s, ElimArgs g, const uint32_t *ids, uint64_t n, const char *cls_name, int grp) {
+          const bool timed = grp == 0;
+          hipEvent_t *ev = E->evt[grp];
           // grids: a few workgroups per CU, grid-stride over the clusters (largest first); the
           // per-lane pool chunks are bounded by the grid size
           const unsigned gb = (unsigned)std::min<uint64_t>(n, 2048), gm = (unsigned)std::min<uint64_t>(n, 8192);
+          HC(hipEventRecord(ev[0], s));
           hipLaunchKernelGGL(k_big_prep, dim3(gb), dim3(256), 0, s, g, ids, n);
           HC(hipGetLastError());
           // process_3 clusters whose rows' pivots are all distinct: every row at once (k_p3_fast); the
@@ -1602,23 +1782,27 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           hipLaunchKernelGGL(k_p3_fast, dim3(gb), dim3(256), 0, s, g, ids, n);
           HC(hipGetLastError());
           if (timed) HC(hipEventRecord(E->ev5, s));
+          HC(hipEventRecord(ev[1], s));
           hipLaunchKernelGGL(k_big_main<256>, dim3(gm), dim3(64), 0, s, g, ids, n);
           HC(hipGetLastError());
           if (timed) HC(hipEventRecord(E->ev6, s));
+          HC(hipEventRecord(ev[2], s));
           {  // the group's clusters flagged in cls, then one inversion per 64 slots across clusters
             uint8_t *cls = E->A.get<uint8_t>(cls_name, eo.n_clusters);
             HC(hipMemsetAsync(cls, 0, eo.n_clusters, s));
             launch(s, k_mark_u8, n, ids, n, cls);
             launch(s, k_batch_inv_flat, (n_slots + 63) / 64, g, (const uint32_t *)d_cid, (const uint8_t *)cls, n_slots);
           }
+          HC(hipEventRecord(ev[3], s));
           // clusters of kFinWaveBelow rows and more by the workgroup, the rest one wave each (most
           // compose chains: the level latency, not the lanes, is their cost)
           hipLaunchKernelGGL(k_big_finish<4>, dim3(gb), dim3(256), 0, s, g, ids, n, kFinWaveBelow);
           HC(hipGetLastError());
+          HC(hipEventRecord(ev[4], s));
         };
         uint8_t *skip = E->A.get<uint8_t>("el.skip", n_tail);
         at.skip = skip;
-        tail_group(E->st, at, d_big + n_head, n_t1, "el.cls", true);
+        tail_group(E->st, at, d_big + n_head, n_t1, "el.cls", 0);
         if (n_t2) {
           ElimArgs a2 = at;  // per-cluster side arrays indexed by the position in the launch's list
           a2.big_touch_off += n_t1;
@@ -1626,7 +1810,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
           a2.big_alive += n_t1;
           a2.skip = skip + n_t1;
           if (a2.prof) a2.prof += kProfWords * n_t1;
-          tail_group(E->ste, a2, d_big + n_head + n_t1, n_t2, "el.cls2", false);
+          tail_group(E->ste, a2, d_big + n_head + n_t1, n_t2, "el.cls2", 1);
         }
       }
       HC(hipEventRecord(E->ev_sm[2], E->ste));  // the main stream joins after the tail's second group
@@ -1749,16 +1933,37 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       HC(hipEventElapsedTime(&msm, E->ev_sm[0], E->ev_sm[1]));
       E->stats.elim_big_ms += ms;  // wall of the workgroup kernels (both streams; the small ones run beside)
       E->stats.elim_small_ms += msm;
-      unsigned long long b5[5] = {0, 0, 0, 0, 0};
-      HC(hipMemcpy(b5, a.bytes, 40, hipMemcpyDeviceToHost));
+      unsigned long long b5[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      HC(hipMemcpy(b5, a.bytes, 64, hipMemcpyDeviceToHost));
       by = b5[0];
       E->stats.elim_kernel_ms += ms;
       E->stats.elim_kernel_launches++;
       E->stats.elim_bytes += by;
-      E->stats.big_main_bytes += b5[1] + b5[3];
+      E->stats.big_main_bytes += b5[1] + b5[3] + b5[7];
       E->stats.big_finish_bytes += b5[2] + b5[4];
       E->stats.head_main_bytes += b5[1];
       E->stats.tail_main_bytes += b5[3];
+      E->stats.tail_fin_bytes += b5[4];
+      E->stats.head_fin_bytes += b5[2];
+      E->stats.small_bytes += b5[0];
+      E->stats.giant_bytes += b5[7];
+      if (D.timed) {
+        float mc = 0;
+        HC(hipEventElapsedTime(&mc, E->evc[0], E->evc[1]));
+        E->stats.cluster_dev_ms += mc;
+        E->stats.cluster_bytes += D.alg;
+        E->stats.cluster_launches++;
+      }
+      if (n_small) {
+        E->stats.small_ms += msm;
+        E->stats.small_launches++;
+      }
+      if (!giants.empty()) {
+        float mg = 0;
+        HC(hipEventElapsedTime(&mg, E->evgt[0], E->evgt[1]));
+        E->stats.giant_ms += mg;
+        E->stats.giant_launches++;
+      }
       if (n_tail) {
         float m0 = 0, m1 = 0, m2 = 0;
         HC(hipEventElapsedTime(&m0, E->evx[5], E->ev5));
@@ -1768,8 +1973,18 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.big_main_ms += m1;
         E->stats.big_finish_ms += m2;
         E->stats.big_launches++;
-        E->stats.tail_main_ms += m1;
-        E->stats.tail_launches++;
+        for (int g = 0; g < n_tgroups; ++g) {  // each group on its own stream: kernel times add up
+          float p0 = 0, p1 = 0, p2 = 0;
+          HC(hipEventElapsedTime(&p0, E->evt[g][0], E->evt[g][1]));
+          HC(hipEventElapsedTime(&p1, E->evt[g][1], E->evt[g][2]));
+          HC(hipEventElapsedTime(&p2, E->evt[g][2], E->evt[g][4]));
+          E->stats.prep_ms += p0;
+          E->stats.tail_main_ms += p1;
+          E->stats.tail_fin_ms += p2;
+        }
+        E->stats.prep_launches += n_tgroups;
+        E->stats.tail_launches += n_tgroups;
+        E->stats.tail_fin_launches += n_tgroups;
       }
       if (g_prof_env) {
         float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
@@ -1800,6 +2015,10 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.big_launches++;
         E->stats.head_main_ms += m1;
         E->stats.head_launches++;
+        float mf = 0;
+        HC(hipEventElapsedTime(&mf, E->evgt[2], E->evx[4]));
+        E->stats.head_fin_ms += mf;
+        E->stats.head_fin_launches++;
       }
     }
     if (a.prof) {
@@ -3424,6 +3643,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     x_at[0] = n_keep;
     x_at[1] = n_keep + n_x[0];
     const uint64_t n_out = n_keep + n_x[0] + n_x[1];
+    if (n_keep > n_st || n_x[0] > lv.n || n_x[1] > lcv.n) throw RsError(RS_E_INTERNAL, "final assembly: row counts out of range");
     E->out_n_dev = n_out;
     const DRows *parts[3] = {&ta_, &tb_, &tc_};
     const char *nm[3] = {"out.a", "out.b", "out.c"};
@@ -3482,10 +3702,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       E->out_ext[q] = ext;
       uint64_t *beg = A.get<uint64_t>(std::string(nm[q]) + ".beg", m_loc + 1);
       uint64_t *end = A.get<uint64_t>(std::string(nm[q]) + ".end", m_loc + 1);
-      if (shard) {  // fetch_result_shared's rebased copies (allocated here: nothing may move after the run)
-        (void)A.get<uint64_t>(std::string(nm[q]) + ".begx", m_loc);
-        (void)A.get<uint64_t>(std::string(nm[q]) + ".endx", m_loc);
-      }
+
       if (own) launch(st, k_out_extent, own, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
                       (const uint8_t *)so_dirty, (const U3 *)so_eoff, q, base, (const uint64_t *)lptr, beg, end);
       if (xl_n[0])
@@ -3495,6 +3712,20 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         launch(st, k_lc_extent, xl_n[1], xq[1], (const uint32_t *)x_ids[1], xl_n[1], E->lc_snap_n, E->lc_snap_base, q, base,
                (const uint64_t *)(lptr + xl_at[1]), beg + xl_at[1], end + xl_at[1]);
       launch(st, k_set_u64, 1, beg + m_loc, ext);
+      {  // ABI 8: per row its length (+ RS_ROW_JUMP) and the jump table -- what crosses the link
+        uint32_t *len32 = A.get<uint32_t>(std::string(nm[q]) + ".len32", m_loc + 1);
+        uint64_t *jf = A.get<uint64_t>(std::string(nm[q]) + ".jf", m_loc + 1);
+        uint64_t *jpos = A.get<uint64_t>(std::string(nm[q]) + ".jpos", m_loc + 1);
+        uint64_t nj = 0;
+        if (m_loc) {
+          launch(st, k_out_jumps, m_loc, (const uint64_t *)beg, (const uint64_t *)end, m_loc, shard ? 1 : 0, len32, jf);
+          nj = excl_scan_u64(E, jf, jpos, m_loc, "jump");
+        }
+        uint64_t *jtab = A.get<uint64_t>(std::string(nm[q]) + ".jtab", nj + 1);
+        if (nj) launch(st, k_out_jtab, m_loc, (const uint64_t *)beg, (const uint64_t *)jf, (const uint64_t *)jpos, m_loc, (uint64_t)0, jtab);
+        E->out_njump[q] = nj;
+        if (shard) (void)A.get<uint64_t>(std::string(nm[q]) + ".jtabx", nj + 1);  // fetch_result_shared's rebased copy
+      }
       // the device copy of the whole layout grows past the early region when it must (the
       // early region is copied along once its gather is done)
       const std::string xc = std::string(nm[q]) + ".xcol", xv = std::string(nm[q]) + ".xval";
@@ -3566,7 +3797,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     const uint64_t z_out = E->out_nnz[0] + E->out_nnz[1] + E->out_nnz[2], r_out = E->out_n_dev;
     const rs_stats &s = E->stats;
     E->stats.alg_bytes = s.elim_bytes + s.big_main_bytes + s.big_finish_bytes + s.apply_bytes + s.round_fill_bytes +
-                         36 * (z_in + z_out) + 8 * (r_in + r_out) + 8 * S;
+                         s.cluster_bytes + 36 * (z_in + z_out) + 8 * (r_in + r_out) + 8 * S;
   }
   E->have_result = true;
 }
@@ -3625,6 +3856,12 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipStreamCreateWithFlags(&E->stx, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->str, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->ste, hipStreamNonBlocking));
+    HC(hipStreamCreateWithFlags(&E->stg, hipStreamNonBlocking));
+    for (auto &ev : E->evg) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (auto &g : E->evt)
+      for (auto &ev : g) HC(hipEventCreate(&ev));
+    for (auto &ev : E->evc) HC(hipEventCreate(&ev));
+    for (auto &ev : E->evgt) HC(hipEventCreate(&ev));
     for (auto &ev : E->ev_sm) HC(hipEventCreate(&ev));
     for (auto &ev : E->evx) HC(hipEventCreate(&ev));
     for (auto &ev : E->ev_grp) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -3663,6 +3900,7 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->st2) (void)hipStreamSynchronize(E->st2);
   if (E->stc) (void)hipStreamSynchronize(E->stc);
   if (E->ste) (void)hipStreamSynchronize(E->ste);
+  if (E->stg) (void)hipStreamSynchronize(E->stg);
   snap_join(E);
   E->comm.reset();
   for (auto &pb : E->pin)
@@ -3679,6 +3917,16 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->stx) (void)hipStreamDestroy(E->stx);
   if (E->str) (void)hipStreamDestroy(E->str);
   if (E->ste) (void)hipStreamDestroy(E->ste);
+  if (E->stg) (void)hipStreamDestroy(E->stg);
+  for (auto &ev : E->evg)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto &g : E->evt)
+    for (auto &ev : g)
+      if (ev) (void)hipEventDestroy(ev);
+  for (auto &ev : E->evc)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto &ev : E->evgt)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : E->ev_sm)
     if (ev) (void)hipEventDestroy(ev);
   if (E->ev0) (void)hipEventDestroy(E->ev0);
@@ -3776,7 +4024,9 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
   o->n_constraints = nd;
   const char *nm[3] = {"out.a", "out.b", "out.c"};
   rs_lc *dst[3] = {&o->a, &o->b, &o->c};
-  uint64_t **ends[3] = {&o->a_end, &o->b_end, &o->c_end};
+  uint32_t **lens[3] = {&o->a_len, &o->b_len, &o->c_len};
+  uint64_t **jumps[3] = {&o->a_jump, &o->b_jump, &o->c_jump};
+  uint64_t *njs[3] = {&o->a_njump, &o->b_njump, &o->c_njump};
   if (!streamed) ensure_csr(E);
   for (int q = 0; q < 3; ++q) {
     rs_lc &L = *dst[q];
@@ -3788,7 +4038,9 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
       L.ptr = (uint64_t *)buf(q, 8 * (nd + 1));
       L.col = (uint32_t *)buf(3 + q, 4 * (tot ? tot : 1));
       L.val = (uint64_t *)buf(6 + q, 32 * (tot ? tot : 1));
-      *ends[q] = nullptr;
+      *lens[q] = nullptr;
+      *jumps[q] = nullptr;
+      *njs[q] = 0;
       if (nd) HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(n + ".ptr", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
       else L.ptr[0] = 0;
       if (tot) {
@@ -3797,18 +4049,16 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
       }
       continue;
     }
-    const uint64_t early = E->snap_e[q], ext = E->out_ext[q];
+    const uint64_t early = E->snap_e[q], ext = E->out_ext[q], nj = E->out_njump[q];
     L.nnz = ext;
-    L.ptr = (uint64_t *)pin_get(E, q, 8 * (nd + 1));
-    *ends[q] = (uint64_t *)pin_get(E, 13 + q, 8 * (nd + 1));
+    L.ptr = nullptr;  // ABI 8: lengths + jumps (rs_rows_next)
+    *lens[q] = (uint32_t *)pin_get(E, 13 + q, 4 * (nd ? nd : 1));
+    *jumps[q] = (uint64_t *)pin_get(E, q, 8 * (nj ? nj : 1));
+    *njs[q] = nj;
     L.col = (uint32_t *)pin_grow_keep(E, 3 + q, 4 * (ext ? ext : 1), 4 * early);
     L.val = (uint64_t *)pin_grow_keep(E, 6 + q, 32 * (ext ? ext : 1), 32 * early);
-    if (nd) {
-      HC(hipMemcpyAsync(L.ptr, E->A.get<uint64_t>(n + ".beg", 1), 8 * (nd + 1), hipMemcpyDeviceToHost, E->st));
-      HC(hipMemcpyAsync(*ends[q], E->A.get<uint64_t>(n + ".end", 1), 8 * nd, hipMemcpyDeviceToHost, E->st));
-    } else {
-      L.ptr[0] = ext;
-    }
+    if (nd) HC(hipMemcpyAsync(*lens[q], E->A.get<uint32_t>(n + ".len32", 1), 4 * nd, hipMemcpyDeviceToHost, E->st));
+    if (nj) HC(hipMemcpyAsync(*jumps[q], E->A.get<uint64_t>(n + ".jtab", 1), 8 * nj, hipMemcpyDeviceToHost, E->st));
     if (ext > early) {
       HC(hipMemcpyAsync(L.col + early, E->A.get<uint32_t>(n + ".xcol", 1) + early, 4 * (ext - early), hipMemcpyDeviceToHost, E->st));
       HC(hipMemcpyAsync(L.val + 4 * early, E->A.get<uint64_t>(n + ".xval", 1) + 4 * early, 32 * (ext - early),
@@ -3822,7 +4072,7 @@ static void fetch_result(rs_engine *E, rs_output *o, const std::function<void *(
   HC(hipStreamSynchronize(E->st));
   if (g_prof_env && streamed) {
     double late = 4.0 * E->S;
-    for (int q = 0; q < 3; ++q) late += 16.0 * nd + 8.0 + 36.0 * (E->out_ext[q] - E->snap_e[q]);
+    for (int q = 0; q < 3; ++q) late += 4.0 * nd + 8.0 * E->out_njump[q] + 36.0 * (E->out_ext[q] - E->snap_e[q]);
     fprintf(stderr, "[rs-prof] fetch: row extents, late rows and label_to_wire %.1f MB, waited %.2f ms\n", late / 1e6, now_ms() - tf0);
   }
   if (streamed) {
@@ -3871,32 +4121,42 @@ static void fetch_result_shared(rs_engine *E, rs_output *o, bool own_log) {
   const uint64_t k_lo = E->sh_klo, own = E->sh_khi - E->sh_klo, n_keep = E->fin_keep;
   const bool with_x = r == W - 1;
   const uint64_t m_loc = own + (with_x ? nd - n_keep : 0);
-  // rows region: ptr, end of a, b, c, then label_to_wire
-  const uint64_t rows_bytes = 3 * 8 * (2 * nd + 1) + 4 * S;
+  // rows region (ABI 8): the row lengths of a, b, c (u32, nd each), the jump tables of a, b, c (every
+  // rank's, in rank order -- the ranks' rows are consecutive in storage order, each rank's first row
+  // jumps to its base), then label_to_wire
+  uint64_t nj_tot[3], nj_before[3];
+  for (int q = 0; q < 3; ++q) {
+    const std::vector<uint64_t> g = CM.gather_u64(E->out_njump[q], st);
+    nj_tot[q] = nj_before[q] = 0;
+    for (uint64_t x = 0; x < W; ++x) {
+      if (x < r) nj_before[q] += g[x];
+      nj_tot[q] += g[x];
+    }
+  }
+  const uint64_t len_bytes = (12 * nd + 7) / 8 * 8, jump_bytes = 8 * (nj_tot[0] + nj_tot[1] + nj_tot[2]);
+  const uint64_t rows_bytes = len_bytes + jump_bytes + 4 * S;
   uint8_t *rb = (uint8_t *)CM.shared_host(1, rows_bytes, st);
   if (!rb) throw RsError(RS_E_RCCL, "no shared host memory for the sharded result");
   const char *nm[3] = {"out.a", "out.b", "out.c"};
   rs_lc *dst[3] = {&o->a, &o->b, &o->c};
-  uint64_t **ends[3] = {&o->a_end, &o->b_end, &o->c_end};
+  uint32_t **lens[3] = {&o->a_len, &o->b_len, &o->c_len};
+  uint64_t **jumps[3] = {&o->a_jump, &o->b_jump, &o->c_jump};
+  uint64_t *njs[3] = {&o->a_njump, &o->b_njump, &o->c_njump};
   o->n_constraints = nd;
+  uint64_t *jbase = (uint64_t *)(rb + len_bytes);
   for (int q = 0; q < 3; ++q) {
-    uint64_t *ptr = (uint64_t *)(rb + 8 * (2 * nd + 1) * q), *end = ptr + nd + 1;
+    uint32_t *len = (uint32_t *)(rb + 4 * nd * q);
+    uint64_t *jtab = jbase + (q > 0 ? nj_tot[0] : 0) + (q > 1 ? nj_tot[1] : 0);
     const std::string n(nm[q]);
-    const uint64_t rbase = r * E->sh_cap[q], early = E->snap_e[q], ext = E->out_ext[q];
-    if (m_loc) {  // this rank's extents, moved to its base, to their global rows
-      uint64_t *bx = A.get<uint64_t>(n + ".begx", 1), *ex = A.get<uint64_t>(n + ".endx", 1);  // sized by the run
-      launch(st, k_add_u64, m_loc, (const uint64_t *)A.get<uint64_t>(n + ".beg", 1), m_loc, rbase, bx);
-      launch(st, k_add_u64, m_loc, (const uint64_t *)A.get<uint64_t>(n + ".end", 1), m_loc, rbase, ex);
-      if (own) {
-        HC(hipMemcpyAsync(ptr + k_lo, bx, 8 * own, hipMemcpyDeviceToHost, st));
-        HC(hipMemcpyAsync(end + k_lo, ex, 8 * own, hipMemcpyDeviceToHost, st));
-      }
-      if (m_loc > own) {
-        HC(hipMemcpyAsync(ptr + n_keep, bx + own, 8 * (m_loc - own), hipMemcpyDeviceToHost, st));
-        HC(hipMemcpyAsync(end + n_keep, ex + own, 8 * (m_loc - own), hipMemcpyDeviceToHost, st));
-      }
+    const uint64_t rbase = r * E->sh_cap[q], early = E->snap_e[q], ext = E->out_ext[q], nj = E->out_njump[q];
+    if (own) HC(hipMemcpyAsync(len + k_lo, A.get<uint32_t>(n + ".len32", 1), 4 * own, hipMemcpyDeviceToHost, st));
+    if (m_loc > own)
+      HC(hipMemcpyAsync(len + n_keep, A.get<uint32_t>(n + ".len32", 1) + own, 4 * (m_loc - own), hipMemcpyDeviceToHost, st));
+    if (nj) {  // this rank's jumps, moved to its base
+      uint64_t *jx = A.get<uint64_t>(n + ".jtabx", 1);  // sized by the run
+      launch(st, k_add_u64, nj, (const uint64_t *)A.get<uint64_t>(n + ".jtab", 1), nj, rbase, jx);
+      HC(hipMemcpyAsync(jtab + nj_before[q], jx, 8 * nj, hipMemcpyDeviceToHost, st));
     }
-    if (with_x) ptr[nd] = W * E->sh_cap[q];
     const uint64_t from = E->sh_full ? 0 : early;  // the early entries are on their way (snap thread)
     if (ext > from) {
       HC(hipMemcpyAsync(sh_col(E, q) + rbase + from, A.get<uint32_t>(n + ".xcol", 1) + from, 4 * (ext - from), hipMemcpyDeviceToHost, st));
@@ -3906,12 +4166,14 @@ static void fetch_result_shared(rs_engine *E, rs_output *o, bool own_log) {
     rs_lc &L = *dst[q];
     L.n_rows = nd;
     L.nnz = W * E->sh_cap[q];
-    L.ptr = ptr;
+    L.ptr = nullptr;
     L.col = sh_col(E, q);
     L.val = sh_val(E, q);
-    *ends[q] = end;
+    *lens[q] = len;
+    *jumps[q] = jtab;
+    *njs[q] = nj_tot[q];
   }
-  int32_t *l2w = (int32_t *)(rb + 3 * 8 * (2 * nd + 1));
+  int32_t *l2w = (int32_t *)(rb + len_bytes + jump_bytes);
   const uint64_t s0 = S * r / W, s1 = S * (r + 1) / W;
   if (s1 > s0) HC(hipMemcpyAsync(l2w + s0, A.get<int32_t>("fin.l2w", 1) + s0, 4 * (s1 - s0), hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
@@ -4153,9 +4415,12 @@ void rs_output_free(rs_output *o) {
   free(o->label_to_wire);
   free(o->log_from);
   free_lc(o->log_to);
-  free(o->a_end);
-  free(o->b_end);
-  free(o->c_end);
+  free(o->a_len);
+  free(o->b_len);
+  free(o->c_len);
+  free(o->a_jump);
+  free(o->b_jump);
+  free(o->c_jump);
   free(o);
 }
 
@@ -4268,9 +4533,16 @@ int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in) {
   rs_engine *E = nullptr;
   int rc = rs_engine_create(device, &E);
   if (rc) return rc;
+  rs_input *o = (rs_input *)calloc(1, sizeof(rs_input));
   try {
     HC(hipSetDevice(E->device));
-    *in = flatten_dag(E, dag);
+    flatten_dag(E, dag, o, [](int, size_t bytes) {  // malloc'ed like rs_read_r1cs_o0's (rs_input_free)
+      void *p = malloc(bytes ? bytes : 1);
+      if (!p) throw std::bad_alloc();
+      return p;
+    });
+    *in = o;
+    o = nullptr;
     rc = RS_OK;
   } catch (const RsError &e) {
     set_error(e.what());
@@ -4279,8 +4551,28 @@ int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in) {
     set_error(e.what());
     rc = RS_E_INTERNAL;
   }
+  if (o) rs_input_free(o);  // a failed call: the arrays made so far (calloc'ed struct: NULL elsewhere)
   rs_engine_destroy(E);
   return rc;
+}
+
+int rs_engine_flatten_dag(rs_engine *E, const rs_dag *dag, const rs_input **in) {
+  if (!E || !dag || !in) { set_error("rs_engine_flatten_dag: null argument"); return RS_E_INVALID; }
+  *in = nullptr;
+  try {
+    HC(hipSetDevice(E->device));
+    snap_join(E);  // no D2H of an earlier result still reads the engine's buffers
+    E->flat_view = rs_input{};
+    flatten_dag(E, dag, &E->flat_view, [E](int slot, size_t bytes) { return pin_get(E, 20 + slot, bytes); });
+    *in = &E->flat_view;
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
 }
 
 int rs_simplify(const rs_input *in, const rs_flags *fl, rs_output **out) {

@@ -166,7 +166,10 @@ static T *fl_up(rs_engine *E, const std::string &name, const T *h, uint64_t n) {
   return d;
 }
 
-static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
+// buf(slot, bytes): the destination of each output array -- slots 3q, 3q + 1, 3q + 2 for block q's ptr,
+// col, val (cons_eq, eq, linear, nl_a, nl_b, nl_c), 18 for forbidden (malloc for rs_flatten_dag, the
+// engine's page-locked buffers for rs_engine_flatten_dag, whose D2H then runs at link speed)
+static void flatten_dag(rs_engine *E, const rs_dag *D, rs_input *in, const std::function<void *(int, size_t)> &buf) {
   hipStream_t st = E->st;
   uint64_t p[4];
   if (D->prime_id == RS_PRIME_CUSTOM) memcpy(p, D->prime, 32);
@@ -383,8 +386,7 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
   HC(hipMemcpyAsync(&err, A.err, 4, hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));
   if (err) throw RsError(RS_E_INTERNAL, "rs_flatten_dag: instance expansion out of range");
-  // ---- the rs_input (malloc'ed like rs_read_r1cs_o0's, freed by rs_input_free)
-  rs_input *in = (rs_input *)calloc(1, sizeof(rs_input));
+  // ---- the rs_input
   in->prime_id = D->prime_id;
   memcpy(in->prime, p, 32);
   in->max_signal = tot.v[12] + 1;  // the witness list: signal 0 and every instance's locals
@@ -396,9 +398,9 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
     rs_lc &o = *outs[q];
     o.n_rows = rows[q];
     o.nnz = nnz[q];
-    o.ptr = (uint64_t *)malloc(8 * (rows[q] + 1));
-    o.col = (uint32_t *)malloc(4 * std::max<uint64_t>(nnz[q], 1));
-    o.val = (uint64_t *)malloc(32 * std::max<uint64_t>(nnz[q], 1));
+    o.ptr = (uint64_t *)buf(3 * q, 8 * (rows[q] + 1));
+    o.col = (uint32_t *)buf(3 * q + 1, 4 * std::max<uint64_t>(nnz[q], 1));
+    o.val = (uint64_t *)buf(3 * q + 2, 32 * std::max<uint64_t>(nnz[q], 1));
     HC(hipMemcpyAsync(o.ptr, A.optr[q], 8 * (rows[q] + 1), hipMemcpyDeviceToHost, st));
     if (nnz[q]) {
       HC(hipMemcpyAsync(o.col, A.okey[q], 4 * nnz[q], hipMemcpyDeviceToHost, st));
@@ -412,7 +414,6 @@ static rs_input *flatten_dag(rs_engine *E, const rs_dag *D) {
   std::sort(forb.begin(), forb.end());
   forb.erase(std::unique(forb.begin(), forb.end()), forb.end());
   in->n_forbidden = forb.size();
-  in->forbidden = (uint32_t *)malloc(4 * std::max<size_t>(forb.size(), 1));
+  in->forbidden = (uint32_t *)buf(18, 4 * std::max<size_t>(forb.size(), 1));
   if (!forb.empty()) memcpy(in->forbidden, forb.data(), 4 * forb.size());
-  return in;
 }

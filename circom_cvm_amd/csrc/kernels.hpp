@@ -1920,6 +1920,7 @@ __global__ __launch_bounds__(256) void k_batch_inv_tree(ElimArgs A, const uint32
     const uint64_t b = A.cl_off[c];
     const uint32_t m = A.n_sub[c];
     if (m == 0) continue;
+    if (t == 0) atomicAdd(A.bytes_fin, 96ull * m);  // per pivot: its coefficient, the prefix written and read back
     const uint32_t per = (m + 255) / 256, c0 = min(m, t * per), c1 = min(m, c0 + per);
     Fe acc = F.one;  // the chunk's running product, kept in ftmp
     for (uint32_t i = c0; i < c1; ++i) {
@@ -1981,6 +1982,7 @@ __device__ __forceinline__ bool d_inv_slot(const ElimArgs &A, const uint32_t *ci
 }
 __global__ void k_batch_inv_flat(ElimArgs A, const uint32_t *cid, const uint8_t *cls, uint64_t n_slots) {
   const FieldP &F = A.F;
+  unsigned long long by = 0;  // per pivot: its coefficient, the prefix written and read back
   for (uint64_t t = gtid(); t * 64 < n_slots; t += gstride()) {
     const uint64_t s0 = t * 64, s1 = min<uint64_t>(n_slots, s0 + 64);
     Fe acc = F.one;
@@ -1990,6 +1992,7 @@ __global__ void k_batch_inv_flat(ElimArgs A, const uint32_t *cid, const uint8_t 
       acc = fmul(F, acc, A.h_coef[sl]);
       A.ftmp[sl] = acc;  // prefix product up to sl
       last = sl;
+      by += 96;
     }
     if (last == RS_NONE) continue;
     Fe inv = finv(F, acc);
@@ -2003,6 +2006,7 @@ __global__ void k_batch_inv_flat(ElimArgs A, const uint32_t *cid, const uint8_t 
     }
     A.ftmp[cur] = inv;
   }
+  wave_atomic_add(A.bytes_fin, by);
 }
 
 // Lane-serial composition of slot `sl` (raw_substitution key by key, ascending): the fallback for
@@ -2679,8 +2683,7 @@ __global__ __launch_bounds__(64 * NW, 3) void k_big_finish(ElimArgs A, const uin
     d_finish_cluster<64 * NW>(A, al, ci, ids[ci], tid, s_team[0], bufs, 0, by_el, by_fin);
   for (uint64_t ci = split + (uint64_t)blockIdx.x * NW + wv; ci < n_ids; ci += (uint64_t)gridDim.x * NW)
     d_finish_cluster<64>(A, al, ci, ids[ci], tid & 63, s_team[wv], bufs, wv, by_el, by_fin);
-  wave_atomic_add(A.bytes, by_el);
-  wave_atomic_add(A.bytes_fin, by_fin);
+  wave_atomic_add(A.bytes_fin, by_el + by_fin);  // the emit's reads count with the finish (A.bytes: k_eliminate)
 }
 
 // One Kahn level of the split composition, over every head cluster at once and the whole GPU: each
@@ -2875,7 +2878,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_emit(ElimArgs A, const uint32_t
     by_el += 36ull * (rows_e + 3 * subs_e) + 8ull * (tid == 0 ? n : 0);
     if (tid == 0 && A.prof) A.prof[kProfWords * ci + 1] = m;
   }
-  wave_atomic_add(A.bytes, by_el);
+  wave_atomic_add(A.bytes_fin, by_el);
 }
 
 // ---------------------------------------------------------------- substitution frames

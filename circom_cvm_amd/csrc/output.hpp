@@ -1,4 +1,4 @@
-// output.hpp -- row extents of the result and the streamed D2H of rs_engine_simplify (ABI 7).
+// output.hpp -- row extents of the result and the streamed D2H of rs_engine_simplify (ABI 8 layout).
 //
 // The result is the storage rows in storage order, then the linear rows the rounds left, then the
 // host-side lconst rows (constraint_simplification.rs:648-729).  A storage row is final once round
@@ -223,5 +223,23 @@ __global__ void k_keep_range(const uint32_t *keep, uint64_t n_keep, const uint32
 }
 __global__ void k_add_u64(const uint64_t *in, uint64_t n, uint64_t add, uint64_t *out) {
   for (uint64_t i = gtid(); i < n; i += gstride()) out[i] = in[i] + add;
+}
+
+// ABI 8's row layout from the extents [beg, end) of rows [0, m): len[i] = the row's entries, bit 31
+// (RS_ROW_JUMP) when it does not start where row i - 1 ended (row 0: unless it starts at 0; always
+// when first_jump -- a rank's first row in the shared layout); jf[i] = that bit, for the jump table
+// (a row's keys are distinct signals below max_signal < 2^31, so its length never reaches bit 31)
+__global__ void k_out_jumps(const uint64_t *beg, const uint64_t *end, uint64_t m, int first_jump, uint32_t *len, uint64_t *jf) {
+  for (uint64_t i = gtid(); i < m; i += gstride()) {
+    const uint64_t b = beg[i], l = end[i] - b;
+    const bool j = i == 0 ? (first_jump || b != 0) : b != end[i - 1];
+    len[i] = (uint32_t)l | (j ? RS_ROW_JUMP : 0u);
+    jf[i] = j ? 1 : 0;
+  }
+}
+// the jump table: the starts of the rows that jump, in row order (+ add: a rank's base in the shared layout)
+__global__ void k_out_jtab(const uint64_t *beg, const uint64_t *jf, const uint64_t *jpos, uint64_t m, uint64_t add, uint64_t *jtab) {
+  for (uint64_t i = gtid(); i < m; i += gstride())
+    if (jf[i]) jtab[jpos[i]] = beg[i] + add;
 }
 

@@ -205,9 +205,9 @@ static std::string dec_string(const uint64_t *v) {
 
 // hashmap_as_json (json_porting.rs:16-26) + JsonValue::to_string: {"k":"v",...}, keys ascending
 // (as numbers), `ids` mapped through `l2w` when given (apply_correspondence).
-static bool map_json(std::string &o, const rs_lc &L, const uint64_t *end, uint64_t r, const int32_t *l2w, uint64_t n_labels) {
+static bool map_json(std::string &o, const rs_lc &L, uint64_t beg, uint64_t len, const int32_t *l2w, uint64_t n_labels) {
   std::vector<std::pair<uint64_t, uint64_t>> ord;  // (key, entry)
-  for (uint64_t e = L.ptr[r]; e < rs_row_end(&L, end, r); ++e) {
+  for (uint64_t e = beg; e < beg + len; ++e) {
     uint64_t k = L.col[e];
     if (l2w) {
       int64_t w = k < n_labels ? l2w[k] : -1;
@@ -377,7 +377,8 @@ static int write_r1cs(const char *path, const rs_input *in, const rs_output *out
   };
   std::vector<std::pair<uint64_t, uint64_t>> ord;  // (order key, entry)
   const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
-  const uint64_t *ends[3] = {out->a_end, out->b_end, out->c_end};
+  rs_rows it[3];
+  for (int q = 0; q < 3; ++q) rs_rows_begin(out, q, &it[q]);
   const bool with_gates = gates && (gates->have[4] || gates->have[5]);
   fwrite(with_gates ? "r1cs\x01\x00\x00\x00\x05\x00\x00\x00" : "r1cs\x01\x00\x00\x00\x03\x00\x00\x00", 1, 12, f);
   // constraints section (r1cs_porting.rs:20-35) -- written first, size back-patched
@@ -392,7 +393,9 @@ static int write_r1cs(const char *path, const rs_input *in, const rs_output *out
     for (int q = 0; q < 3; ++q) {
       const rs_lc &b = *parts[q];
       ord.clear();
-      for (uint64_t e = b.ptr[r]; e < rs_row_end(&b, ends[q], r); ++e) {
+      uint64_t rb, rl;
+      rs_rows_next(&it[q], r, &rb, &rl);
+      for (uint64_t e = rb; e < rb + rl; ++e) {
         uint32_t k = b.col[e];
         uint32_t w;
         if (k == 0) w = 0;
@@ -405,13 +408,13 @@ static int write_r1cs(const char *path, const rs_input *in, const rs_output *out
           }
           w = (uint32_t)ww;
         }
-        ord.push_back({le_order_key(w), ((uint64_t)w << 32) | (e - b.ptr[r])});
+        ord.push_back({le_order_key(w), ((uint64_t)w << 32) | (e - rb)});
       }
       std::sort(ord.begin(), ord.end());
       put32(body, (uint32_t)ord.size());
       for (auto &x : ord) {
         put32(body, (uint32_t)(x.second >> 32));
-        uint64_t e = b.ptr[r] + (x.second & 0xffffffffu);
+        uint64_t e = rb + (x.second & 0xffffffffu);
         const uint8_t *v = (const uint8_t *)(b.val + 4 * e);
         body.insert(body.end(), v, v + fs);
       }
@@ -484,12 +487,15 @@ int rs_write_constraints_json(const char *path, const rs_output *out) {
   fputs("{\n\"constraints\": [", f);
   std::string line;
   const rs_lc *parts[3] = {&out->a, &out->b, &out->c};
-  const uint64_t *ends[3] = {out->a_end, out->b_end, out->c_end};
+  rs_rows it[3];
+  for (int q = 0; q < 3; ++q) rs_rows_begin(out, q, &it[q]);
   for (uint64_t r = 0; r < out->n_constraints; ++r) {
     line.assign(r ? ",\n[" : "\n[");
     for (int q = 0; q < 3; ++q) {
       if (q) line += ',';
-      if (!map_json(line, *parts[q], ends[q], r, out->label_to_wire, out->n_labels)) {
+      uint64_t rb, rl;
+      rs_rows_next(&it[q], r, &rb, &rl);
+      if (!map_json(line, *parts[q], rb, rl, out->label_to_wire, out->n_labels)) {
         fclose(f);
         set_error("constraint mentions a removed signal (apply_correspondence panics)");
         return RS_E_INTERNAL;
@@ -515,7 +521,7 @@ int rs_write_substitution_json(const char *path, const rs_output *out) {
     line.assign(i ? ",\n\"" : "\n\"");
     line += std::to_string(out->log_from[i]);
     line += "\" : ";
-    map_json(line, out->log_to, nullptr, i, nullptr, 0);
+    map_json(line, out->log_to, out->log_to.ptr[i], out->log_to.ptr[i + 1] - out->log_to.ptr[i], nullptr, 0);
     fwrite(line.data(), 1, line.size(), f);
   }
   fputs("\n}", f);

@@ -575,6 +575,7 @@ __global__ __launch_bounds__(64 * NW) void k_big_spec(ElimArgs A, const uint32_t
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = 64 * NW;
   const bool prof = A.prof != nullptr;
   for (uint64_t ci = blockIdx.x; ci < n_ids; ci += gridDim.x) {
+    if (A.skip && A.skip[ci]) continue;  // a giant cluster: giant_loop.hpp's component loops take it
     const uint64_t c = ids[ci];
     const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
     const bool p4 = d_is_p4(A, (uint32_t)(e - b));

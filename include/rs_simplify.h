@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 7
+#define RS_ABI_VERSION 8
 
 enum rs_status {
   RS_OK = 0,
@@ -125,17 +125,48 @@ typedef struct rs_output {
   uint64_t n_log;
   uint32_t *log_from;
   rs_lc log_to;
-  /* ABI 7: row extents of a / b / c.  NULL: the block is CSR (row i = [ptr[i], ptr[i+1])), as
-   * rs_simplify / rs_engine_fetch return it.  Non-NULL (rs_engine_simplify's streamed result):
-   * row i = [ptr[i], end[i]) of col / val.  Rows stay in storage order but need not be contiguous:
-   * the storage rows that were final after the first round went to the host while the later rounds
-   * ran, the rest follow them, so col / val may hold entries no row refers to.  nnz is then the
-   * extent of col / val (= ptr[n_rows]), not the sum of the row lengths. */
-  uint64_t *a_end, *b_end, *c_end;
+  /* ABI 8: the row layout of a / b / c.  NULL: the block is CSR (row i = [ptr[i], ptr[i+1])), as
+   * rs_simplify / rs_engine_fetch return it.  Non-NULL (rs_engine_simplify's streamed result): ptr is
+   * NULL and rows are walked in storage order: row i holds {a,b,c}_len[i] & ~RS_ROW_JUMP entries of
+   * col / val, starting where row i - 1's ended -- or, when bit 31 (RS_ROW_JUMP) is set, at the next
+   * offset of {a,b,c}_jump (row 0 starts at 0 unless it jumps).  The storage rows that were final
+   * after the first round went to the host while the later rounds ran and the rest follow them, so
+   * col / val may hold entries no row refers to; nnz is the extent of col / val.  rs_rows_begin /
+   * rs_rows_next below walk either layout.  (ABI 7 sent a u64 start and a u64 end per row and part:
+   * 48 bytes a row on the PCIe link against 12 + a few jumps.) */
+  uint32_t *a_len, *b_len, *c_len;
+  uint64_t *a_jump, *b_jump, *c_jump;
+  uint64_t a_njump, b_njump, c_njump;
 } rs_output;
 
-/* End of row r of a result block: end[r] when the block has row ends (ABI 7), else ptr[r + 1]. */
-static inline uint64_t rs_row_end(const rs_lc *L, const uint64_t *end, uint64_t r) { return end ? end[r] : L->ptr[r + 1]; }
+#define RS_ROW_JUMP 0x80000000u
+/* The rows of result block q (0 a, 1 b, 2 c) in order, for either layout: rs_rows_begin, then
+ * rs_rows_next(&it, r, &beg, &len) for r = 0, 1, 2, ... (a CSR block also allows any order). */
+typedef struct rs_rows {
+  const rs_lc *L;
+  const uint32_t *len;
+  const uint64_t *jump;
+  uint64_t pos, j;
+} rs_rows;
+static inline void rs_rows_begin(const rs_output *o, int q, rs_rows *it) {
+  it->L = q == 0 ? &o->a : (q == 1 ? &o->b : &o->c);
+  it->len = q == 0 ? o->a_len : (q == 1 ? o->b_len : o->c_len);
+  it->jump = q == 0 ? o->a_jump : (q == 1 ? o->b_jump : o->c_jump);
+  it->pos = 0;
+  it->j = 0;
+}
+static inline void rs_rows_next(rs_rows *it, uint64_t r, uint64_t *beg, uint64_t *len) {
+  if (!it->len) {
+    *beg = it->L->ptr[r];
+    *len = it->L->ptr[r + 1] - it->L->ptr[r];
+    return;
+  }
+  const uint32_t x = it->len[r];
+  if (x & RS_ROW_JUMP) it->pos = it->jump[it->j++];
+  *beg = it->pos;
+  *len = x & ~RS_ROW_JUMP;
+  it->pos += *len;
+}
 
 /* Phase timings of the last rs_engine_run (milliseconds, HIP events + host clock). */
 typedef struct rs_stats {
@@ -188,6 +219,25 @@ typedef struct rs_stats {
   double d2h_ms;               /* D2H of the result into the engine's pinned buffers        */
   double host_total_ms;        /* rs_engine_simplify: host input -> host output             */
   double write_ms;             /* ABI 5: the last rs_engine_write_r1cs (device image + file)  */
+  /* ABI 8: the rest of the elimination's kernels, each with its HIP-event time (on the stream it runs
+   * on) and in-kernel algorithmic bytes, so the per-kernel rooflines cover the GPU time */
+  double tail_fin_ms;          /* k_batch_inv_flat + k_big_finish<4>: the tail's normalisation + composition (both groups) */
+  uint64_t tail_fin_bytes;
+  uint64_t tail_fin_launches;
+  double head_fin_ms;          /* the head's k_batch_inv_tree, k_normalize, k_big_finish<8>, Kahn levels, k_big_emit */
+  uint64_t head_fin_bytes;
+  uint64_t head_fin_launches;
+  double small_ms;             /* k_eliminate (clusters under 32 rows, one lane each)               */
+  uint64_t small_bytes;
+  uint64_t small_launches;
+  double prep_ms;              /* the tail's k_big_prep + k_p3_fast (both groups)                    */
+  uint64_t prep_launches;
+  double cluster_dev_ms;       /* build_clusters on the device (pair sort, union-find, arena replays) */
+  uint64_t cluster_bytes;      /* its keys read, (signal, row) pairs written, sorted and linked, per-row arrays */
+  uint64_t cluster_launches;
+  double giant_ms;             /* the giant path (giant_loop.hpp): component loops of the largest clusters */
+  uint64_t giant_bytes;
+  uint64_t giant_launches;
 } rs_stats;
 
 typedef struct rs_engine rs_engine;
@@ -328,6 +378,11 @@ typedef struct rs_dag {
  * malformed CSR blocks (ptr[0] != 0, decreasing pointers, ptr[T] != nnz) and a graph whose offset
  * signal ids (instance offset + node-local id) or signal count reach 2^31. */
 int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in);
+/* The same on a persistent engine (its device buffers stay allocated across calls), into page-locked
+ * buffers the engine owns, so the blocks' D2H runs at PCIe speed and the result feeds
+ * rs_engine_simplify's H2D at full speed too.  *in views those buffers: valid until the next
+ * rs_engine_flatten_dag on `eng` or rs_engine_destroy (do not rs_input_free it). */
+int rs_engine_flatten_dag(rs_engine *eng, const rs_dag *dag, const rs_input **in);
 
 #ifdef __cplusplus
 }

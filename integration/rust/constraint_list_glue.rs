@@ -149,12 +149,12 @@ pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, Signal
         panic!("rs_simplify failed ({}): {}", rc, msg);
     }
     let o = unsafe { &*out };
-    // row r = [ptr[r], end[r]) when the block carries row ends (ABI 7), else [ptr[r], ptr[r + 1])
-    let map_of = |lc: &ffi::rs_lc, end: *mut u64, r: usize| -> HashMap<usize, BigInt> {
+    // rows in order through ffi::RowCursor (CSR here; ABI 8's streamed layout walks the same way)
+    let map_of = |cur: &mut ffi::RowCursor, r: usize| -> HashMap<usize, BigInt> {
         let mut m = HashMap::new();
-        let lo = unsafe { *lc.ptr.add(r) as usize };
-        let hi = unsafe { if end.is_null() { *lc.ptr.add(r + 1) as usize } else { *end.add(r) as usize } };
-        for e in lo..hi {
+        let lc = cur.lc();
+        let (lo, n) = cur.next(r);
+        for e in lo..lo + n {
             let k = unsafe { *lc.col.add(e) } as usize;
             let limbs: Vec<u64> = (0..4).map(|i| unsafe { *lc.val.add(4 * e + i) }).collect();
             m.insert(k, from_limbs(&limbs)); // canonical, non-negative
@@ -162,9 +162,10 @@ pub fn simplification_mi355x(smp: &mut Simplifier) -> (ConstraintStorage, Signal
         m
     };
     let mut storage = ConstraintStorage::new();
+    let (mut ca, mut cb, mut cc) = (ffi::RowCursor::new(o, 0), ffi::RowCursor::new(o, 1), ffi::RowCursor::new(o, 2));
     for r in 0..o.n_constraints as usize {
         // Constraint::new is private (algebra.rs:1012): the shim adds `pub fn new_unchecked(a, b, c)`
-        storage.add_constraint(C::new_unchecked(map_of(&o.a, o.a_end, r), map_of(&o.b, o.b_end, r), map_of(&o.c, o.c_end, r)));
+        storage.add_constraint(C::new_unchecked(map_of(&mut ca, r), map_of(&mut cb, r), map_of(&mut cc, r)));
     }
     let mut signal_map = SignalMap::with_capacity(o.n_wires as usize);
     for s in 0..o.n_labels as usize {

@@ -1,10 +1,10 @@
-//! Raw bindings of `include/rs_simplify.h` (ABI 7), one item per C declaration, same order and
+//! Raw bindings of `include/rs_simplify.h` (ABI 8), one item per C declaration, same order and
 //! layout.  The safe wrapper a caller uses is `constraint_list_glue.rs` (the body that replaces
 //! `constraint_list::constraint_simplification::simplification`, constraint_simplification.rs:442).
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const RS_ABI_VERSION: c_int = 7;
+pub const RS_ABI_VERSION: c_int = 8;
 pub const RS_COMM_ID_BYTES: usize = 128;
 
 pub const RS_OK: c_int = 0;
@@ -65,9 +65,59 @@ pub struct rs_output {
     pub n_log: u64,
     pub log_from: *mut u32,
     pub log_to: rs_lc,
-    pub a_end: *mut u64,
-    pub b_end: *mut u64,
-    pub c_end: *mut u64,
+    /// ABI 8 row layout (null: CSR through `ptr`): row lengths, bit 31 = RS_ROW_JUMP
+    pub a_len: *mut u32,
+    pub b_len: *mut u32,
+    pub c_len: *mut u32,
+    pub a_jump: *mut u64,
+    pub b_jump: *mut u64,
+    pub c_jump: *mut u64,
+    pub a_njump: u64,
+    pub b_njump: u64,
+    pub c_njump: u64,
+}
+
+pub const RS_ROW_JUMP: u32 = 0x8000_0000;
+
+/// rs_rows_begin / rs_rows_next (include/rs_simplify.h): the rows of block q (0 a, 1 b, 2 c) in
+/// order, for either layout; `next(r)` must be called for r = 0, 1, 2, ... and returns (start, len).
+pub struct RowCursor<'a> {
+    lc: &'a rs_lc,
+    len: *const u32,
+    jump: *const u64,
+    pos: u64,
+    j: usize,
+}
+
+impl<'a> RowCursor<'a> {
+    pub fn new(o: &'a rs_output, q: usize) -> Self {
+        let (lc, len, jump) = match q {
+            0 => (&o.a, o.a_len, o.a_jump),
+            1 => (&o.b, o.b_len, o.b_jump),
+            _ => (&o.c, o.c_len, o.c_jump),
+        };
+        RowCursor { lc, len, jump, pos: 0, j: 0 }
+    }
+    pub fn lc(&self) -> &'a rs_lc {
+        self.lc
+    }
+    pub fn next(&mut self, r: usize) -> (usize, usize) {
+        unsafe {
+            if self.len.is_null() {
+                let lo = *self.lc.ptr.add(r);
+                return (lo as usize, (*self.lc.ptr.add(r + 1) - lo) as usize);
+            }
+            let x = *self.len.add(r);
+            if x & RS_ROW_JUMP != 0 {
+                self.pos = *self.jump.add(self.j);
+                self.j += 1;
+            }
+            let l = (x & !RS_ROW_JUMP) as u64;
+            let b = self.pos;
+            self.pos += l;
+            (b as usize, l as usize)
+        }
+    }
 }
 
 /// the component DAG rs_flatten_dag expands (dag/src/lib.rs Node / Edge).
@@ -140,6 +190,23 @@ pub struct rs_stats {
     pub d2h_ms: f64,
     pub host_total_ms: f64,
     pub write_ms: f64,
+    pub tail_fin_ms: f64,
+    pub tail_fin_bytes: u64,
+    pub tail_fin_launches: u64,
+    pub head_fin_ms: f64,
+    pub head_fin_bytes: u64,
+    pub head_fin_launches: u64,
+    pub small_ms: f64,
+    pub small_bytes: u64,
+    pub small_launches: u64,
+    pub prep_ms: f64,
+    pub prep_launches: u64,
+    pub cluster_dev_ms: f64,
+    pub cluster_bytes: u64,
+    pub cluster_launches: u64,
+    pub giant_ms: f64,
+    pub giant_bytes: u64,
+    pub giant_launches: u64,
 }
 
 #[repr(C)]
@@ -183,4 +250,6 @@ extern "C" {
     pub fn rs_write_substitution_json(path: *const c_char, out: *const rs_output) -> c_int;
     pub fn rs_synth(kind: u32, rows: u64, seed: u64, prime_id: u32, inp: *mut *mut rs_input) -> c_int;
     pub fn rs_flatten_dag(device: c_int, dag: *const rs_dag, inp: *mut *mut rs_input) -> c_int;
+    /// The same into the engine's page-locked buffers (the view lives until the next call on `eng`).
+    pub fn rs_engine_flatten_dag(eng: *mut rs_engine, dag: *const rs_dag, inp: *mut *const rs_input) -> c_int;
 }

@@ -26,7 +26,7 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 def _header_functions():
     txt = open(HDR).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    txt = re.sub(r"^static inline .*$", "", txt, flags=re.M)  # header-only helpers (rs_row_end)
+    txt = re.sub(r"^static inline .*$", "", txt, flags=re.M)  # header-only helpers (rs_rows_begin, rs_rows_next)
     return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(rs_\w+)\s*\(", txt, flags=re.M)))
 
 

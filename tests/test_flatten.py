@@ -184,6 +184,28 @@ def test_flatten_then_simplify():
 
 
 @pytest.mark.gpu
+def test_engine_flatten_dag_pinned():
+    """rs_engine_flatten_dag (page-locked, engine-owned result): the same blocks as rs_flatten_dag and
+    the pyref flattening for DAGs of growing size on ONE engine (its buffers grow and are reused), and
+    the view fed straight to rs_engine_simplify on that engine equals the oracle."""
+    p = R.PRIMES["bn128"]
+    eng = M.Engine(0)
+    for seed, nt in ((3, 4), (4, 9), (5, 6)):
+        nodes, main, no, npb, npr, forb = dagio.gen_dag(300 + seed, p, n_templates=nt, custom_gates=seed % 2 == 1)
+        sys_, b = R.flatten_dag(p, nodes, main, no, npb, npr, forb)
+        d = M.Dag(p, nodes, main, no, npb, npr, forb, "bn128")
+        view = eng.flatten_dag(d)
+        _eq_blocks(blocks_of(view), b, sys_)
+        one = d.flatten(0)
+        assert blocks_of(one.c) == blocks_of(view)
+        fl = rsio.flags("O2")
+        ref, _, _ = rsio.oracle_run(view, fl)
+        got = rsio.output_to_py(eng.simplify(view, fl))
+        assert got == ref, seed
+    eng.close()
+
+
+@pytest.mark.gpu
 def test_flatten_wide_and_deep():
     """A DAG whose instances number in the tens of thousands (shared subtrees expanded many times)."""
     p = R.PRIMES["bn128"]

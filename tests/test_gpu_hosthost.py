@@ -145,14 +145,16 @@ def test_hosthost_streamed_layout(kind, rows, prime):
         got = rsio.output_arrays(o)
         n = int(o.n_constraints)
         for q in range(3):
-            lc, end = o.block(q)
-            assert end is not None, "a run with storage rows streams"
-            beg = np.ctypeslib.as_array(lc.ptr, shape=(n + 1,))
-            e = np.ctypeslib.as_array(end, shape=(n,))
-            assert (beg[:n] <= e).all() and (e <= int(lc.nnz)).all() and int(beg[n]) == int(lc.nnz)
+            lc, lay = o.block(q)
+            assert lay is not None and not lc.ptr, "a run with storage rows streams (ABI 8 layout)"
+            lens = np.ctypeslib.as_array(lay[0], shape=(n,))
+            jumps = np.ctypeslib.as_array(lay[1], shape=(lay[2],)) if lay[2] else np.zeros(0, np.uint64)
+            b = M.abi.row_starts(lens, jumps)
+            e = b + (lens & ~np.uint32(M.abi.ROW_JUMP)).astype(np.int64)
+            assert (e <= int(lc.nnz)).all() and lay[2] <= n
         assert rsio.diff_output_arrays(got, ref) is None
     out = engine().fetch()
-    assert not out.c.a_end and not out.c.b_end and not out.c.c_end
+    assert not out.c.a_len and not out.c.b_len and not out.c.c_len and out.c.a.ptr
     assert rsio.diff_output_arrays(rsio.output_arrays(out.c), ref) is None
     pin.free()
 

@@ -265,7 +265,8 @@ def test_group_survives_rejected_input():
         def work(r):
             engs[r].load(good.inp)
             engs[r].run(fl)
-            outs[r] = rsio.output_to_py(engs[r].fetch().c)
+            o = engs[r].fetch()
+            outs[r] = rsio.output_to_py(o.c)
         th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
         for t in th:
             t.start()

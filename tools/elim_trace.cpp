@@ -28,6 +28,19 @@ struct Cl {
   long ne_i = -1;                        // current non-empty row index
   long dep = -1;                         // latest creator row seen by the current row
   std::map<size_t, size_t> dist_hist;
+  // discovery depth: merges grouped into levels (a key the row starts with: level 0; a key a merge at
+  // level L brings in: L + 1) -- the dependent holder fetches of a loop that fetches every deleted
+  // key's holder as soon as the key is known
+  std::map<uint32_t, int> lvl;
+  int last_lvl = -1, row_depth = 0;
+  size_t depth_sum = 0;
+  std::map<size_t, size_t> depth_hist;
+  void depth_end() {
+    if (row_depth) { depth_hist[row_depth]++; depth_sum += row_depth; }
+    row_depth = 0;
+    last_lvl = -1;
+    lvl.clear();
+  }
   template <class W> void see(const W &w) {
     for (const auto &t : w) {
       auto it = del_at.find(t.k);
@@ -76,6 +89,8 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
     tr::C.row_i++;                                                                  \
     tr::C.row_keys.clear();                                                         \
     for (const Term &t_ : work) tr::C.row_keys.insert(t_.k);                        \
+    tr::C.depth_end();                                                              \
+    for (const Term &t_ : work) tr::C.lvl[t_.k] = 0;                                \
   } while (0)
 #define RC_TRACE_MERGE(key, wlen, hidx, hl)                                          \
   do {                                                                              \
@@ -95,6 +110,9 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
     tr::C.sum_h += (hl);                                                            \
     tr::C.sum_w += (wlen);                                                          \
     if (tr::C.row_keys.count(key)) tr::C.from_row++; else tr::C.introduced++;       \
+    for (const Term &t_ : work) tr::C.lvl.emplace(t_.k, tr::C.last_lvl + 1);        \
+    tr::C.last_lvl = tr::C.lvl[key];                                                \
+    tr::C.row_depth = std::max(tr::C.row_depth, tr::C.last_lvl + 1);                \
   } while (0)
 #define RC_TRACE_INSERT(key, hidx, len)                                             \
   do {                                                                              \
@@ -122,6 +140,7 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
     }                                                                               \
     tr::C.merges_per_row[tr::C.cur_merges]++;                                       \
     tr::C.row_end();                                                                \
+    tr::C.depth_end();                                                              \
     std::lock_guard<std::mutex> lk_(tr::g_mu);                                      \
     auto &c_ = tr::C;                                                               \
     printf("cluster rows=%zu uniq=%zu loop_rows=%zu inserts=%zu lefts=%zu merges=%zu " \
@@ -144,6 +163,8 @@ inline size_t bucket(size_t x) { size_t b = 0; while ((1ull << b) < x + 1) ++b; 
     printf("\n  nonempty=%zu over64=%zu max_sum=%zu max_row=%zu", c_.nonempty_rows, c_.over64, c_.max_sum, c_.max_row); \
     printf("\n  work len (log2):");                                                 \
     for (auto &kv : c_.wlen_hist) printf(" %zu:%zu", kv.first, kv.second);          \
+    printf("\n  discovery depth (levels per row; sum %zu):", c_.depth_sum);          \
+    for (auto &kv : c_.depth_hist) printf(" %zu:%zu", kv.first, kv.second);         \
     printf("\n");                                                                   \
   } while (0)
 
