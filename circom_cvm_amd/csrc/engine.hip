@@ -1456,7 +1456,7 @@ static GiantArgs giant_buffers(rs_engine *E, uint64_t n) {
   if (g_prof_env) {
     G.c_merges = A.get<uint32_t>("gi.c_merges", n);
     G.c_clk = A.get<uint64_t>("gi.c_clk", n);
-    G.sec = A.get<unsigned long long>("gi.sec", 8);
+    G.sec = A.get<unsigned long long>("gi.sec", 32);
   }
   size_t tb = 0;  // the sorts' and scans' temporaries at their final size
   HC(rocprim::radix_sort_pairs(nullptr, tb, G.rkey, G.rkey2, G.rval, G.rval2, (size_t)n, 0, 64, E->stg));
@@ -1482,11 +1482,11 @@ static void giant_launch(rs_engine *E, const ElimArgs &a, GiantArgs G, uint64_t 
   HC(hipGetLastError());
   sort_pairs(E, (const uint64_t *)G.ckey, G.ckey2, (const uint32_t *)G.cidx, G.cidx2, n, 64, "gi", s);
   if (g_prof_env) {
-    HC(hipMemsetAsync(G.sec, 0, 64, s));
+    HC(hipMemsetAsync(G.sec, 0, 256, s));
     HC(hipStreamSynchronize(s));
   }
   const double tl0 = g_prof_env ? now_ms() : 0.0;
-  hipLaunchKernelGGL(k_gi_loop<kGiNW>, dim3((unsigned)std::min<uint64_t>(n, 512)), dim3(kGiT), 0, s, a, G, c);
+  hipLaunchKernelGGL(k_gi_loop, dim3((unsigned)std::min<uint64_t>(n, 512)), dim3(kGhThreads), 0, s, a, G, c);
   HC(hipGetLastError());
   if (g_prof_env) {  // the components' loops: count, the largest by time, merges per microsecond
     HC(hipStreamSynchronize(s));
@@ -1510,15 +1510,13 @@ static void giant_launch(rs_engine *E, const ElimArgs &a, GiantArgs G, uint64_t 
     for (uint32_t i = 0; i < nc && i < 8; ++i)
       fprintf(stderr, "[rs-prof]   component rows %u merges %u: %.1f ms (%.2f us/merge)\n", sz[ord[i]], mg[ord[i]], ck[ord[i]] / 1e5,
               mg[ord[i]] ? ck[ord[i]] / 1e2 / mg[ord[i]] : 0.0);
-    unsigned long long sec[8];
-    HC(hipMemcpy(sec, G.sec, 64, hipMemcpyDeviceToHost));
-    const double tot = (double)(sec[0] + sec[1] + sec[2] + sec[3] + sec[4] + sec[5] + sec[6] + sec[7]);
-    fprintf(stderr, "[rs-prof]   loop sections (clocks per merge; share): pivot %.0f %.2f | holder header %.0f %.2f | rhs %.0f %.2f | "
-            "search+product %.0f %.2f | scan %.0f %.2f | scatter %.0f %.2f | row start %.0f %.2f | other %.0f %.2f\n",
-            sec[0] / (double)std::max<uint64_t>(tm, 1), sec[0] / tot, sec[1] / (double)std::max<uint64_t>(tm, 1), sec[1] / tot,
-            sec[2] / (double)std::max<uint64_t>(tm, 1), sec[2] / tot, sec[3] / (double)std::max<uint64_t>(tm, 1), sec[3] / tot,
-            sec[4] / (double)std::max<uint64_t>(tm, 1), sec[4] / tot, sec[5] / (double)std::max<uint64_t>(tm, 1), sec[5] / tot,
-            sec[6] / (double)std::max<uint64_t>(tm, 1), sec[6] / tot, sec[7] / (double)std::max<uint64_t>(tm, 1), sec[7] / tot);
+    unsigned long long sec[32];
+    HC(hipMemcpy(sec, G.sec, 256, hipMemcpyDeviceToHost));
+    const double nm = (double)std::max<uint64_t>(tm, 1);
+    fprintf(stderr, "[rs-prof]   loop clocks per merge, slot side: decide %.0f | to B' %.0f | combine+B %.0f | rebuild %.0f | row start %.0f | "
+            "row end %.0f | serial %.0f\n", sec[0] / nm, sec[1] / nm, sec[2] / nm, sec[3] / nm, sec[4] / nm, sec[5] / nm, sec[6] / nm);
+    fprintf(stderr, "[rs-prof]   loop clocks per merge, RHS side: decide %.0f | loads %.0f | find %.0f | product %.0f | insert %.0f | B' %.0f | "
+            "B %.0f\n", sec[16] / nm, sec[24] / nm, sec[25] / nm, sec[26] / nm, sec[27] / nm, sec[17] / nm, sec[18] / nm);
   }
   dev_scan_u32(E, G.c_nsub, G.c_dsub, n, s, "gi");
   hipLaunchKernelGGL(k_gi_gather, dim3(gb), dim3(256), 0, s, a, G, c);
@@ -1583,6 +1581,15 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
   // fitted is remembered) -- the pool is the engine's largest buffer: 24x took 20.8 GB on the 20 M-row
   // circuit, and eight in-process ranks did not fit one GPU
   uint64_t want = std::max<uint64_t>(std::max<uint64_t>(1 << 20, 8 * (tot_nnz + n_slots)), E->pool_want);
+  {  // a giant cluster's fill-in: configs[1]'s 559 k-row cluster writes ~170 pool entries a row (its
+     // substitutions' right-hand sides grow along its chains); reserve for it so the first attempt fits
+    uint64_t giant_rows_sum = 0;
+    for (uint64_t i = 0; i < std::min<uint64_t>(n_big, kHeadLimit) && i < D.top_keys.size(); ++i) {
+      const uint64_t r = (0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull;
+      if (r >= kGiantRows) giant_rows_sum += r;
+    }
+    if (!getenv("RS_GI_NOPOOL")) want = std::max<uint64_t>(want, 192 * giant_rows_sum);
+  }
   for (int attempt = 0; attempt < 8; ++attempt) {
     P = get_pool(E, want);
     Pool G{};  // sharded: every rank's exchanged entries (shard_exchange)
@@ -2504,7 +2511,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     uint32_t *fl_d = A.get<uint32_t>("forb.list", nf);
     uint32_t *g_root = A.get<uint32_t>("eq.g_root", nf);
     HC(hipMemsetAsync(g_root, 0, 4 * nf, st));
-    launch(st, k_gather_u32, nf, (const uint32_t *)uf, (const uint32_t *)fl_d, g_root, nf);
+    launch(st, k_uf_roots, nf, uf, (const uint32_t *)fl_d, g_root, nf);
     uint32_t nbf = 0;
     HC(hipMemcpyAsync(&nbf, bfn, 4, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));

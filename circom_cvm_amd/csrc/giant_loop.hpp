@@ -21,17 +21,14 @@
 // leftover is pushed when its row is popped, so the cluster's leftover list is all components'
 // leftovers by descending position (k_gi_compact*).
 //
-// The loop of one component runs in one workgroup of kGiNW waves.  A merge `work = c2*work - c*R`
-// packs the work list (positions [0, len)) and the holder's right-hand side ([len, len + rl)) one
-// entry per lane -- a 72-entry merge of the configs[1] component costs one 256-bit product latency
-// instead of two per lane (the one-wave loop's register merge) -- each side binary-searches the
-// other in LDS, and a block scan of the keep flags places the survivors.  Per-signal state is one
-// u64 word in HBM (gst: forbidden / occurrence count / deleted + the holder's pool header offset), so
-// a holder is one round trip (its header and right-hand side are contiguous in the pool, k_big_prep
-// and d_clear_nn write them so), and the states of a right-hand side's keys are loaded as they arrive
+// The loop of one component runs in one workgroup: the work row in an LDS hash table (k_gi_loop
+// below), a merge one 256-bit product latency and two barriers.  Per-signal state is one u64 word in
+// HBM (gst: forbidden / occurrence count / deleted + the holder's pool header offset), so a holder
+// is one round trip (its header and right-hand side are contiguous in the pool, k_big_prep and
+// d_clear_nn write them so), and the states of a right-hand side's keys are loaded as they arrive
 // and land under the product.  The official per-signal arrays (occ, del, holder_idx, the slot
-// arrays) are kept current as well: rows or merges past the LDS capacity finish on one lane over them
-// (d_gi_serial, d_treat_scalar's logic), and the composition kernels read them afterwards.
+// arrays) are kept current as well: rows or merges past the table's capacity finish on one lane over
+// them (d_gi_serial, d_treat_scalar's logic), and the composition kernels read them afterwards.
 //
 // Included by engine.hip after kernels.hpp, inside namespace rs.
 #pragma once
@@ -40,12 +37,8 @@
 namespace rs {
 
 constexpr uint64_t kGiantRows = 11800;   // head clusters with this many rows take the giant path
-constexpr uint32_t kGiCap = 256;         // LDS work-list capacity (entries); beyond it: one lane
-constexpr int kGiNW = 4;                 // waves per workgroup (kGiT lanes)
-constexpr uint32_t kGiT = 64 * kGiNW;
 constexpr uint64_t kGiForb = ~0ull;      // gst: a forbidden signal
 constexpr uint64_t kGiDel = 1ull << 63;  // gst: deleted; low bits = its holder's pool header offset (else: occurrences)
-static_assert(kGiCap == kGiT, "one work position and one right-hand-side position per lane in the packed merge");
 
 struct GiantArgs {
   uint64_t ci;                 // the cluster's position in the head list (A.big_alive / touch arrays)
@@ -73,15 +66,22 @@ struct GiantArgs {
   uint64_t *c_clk;
   unsigned long long *sec;     // RS_PROF: shader clocks per loop section, summed over the workgroups
 };
-// RS_PROF section clocks of k_gi_loop (thread 0's view; the barriers line the workgroup up with it)
+// Section clocks of k_gi_loop (-DRS_GICLK builds, tools/kclk_build.sh RS_GICLK giclk): thread 0's
+// view (the slots) and thread 129's (the right-hand side); the barriers line the workgroup up with them
+#ifdef RS_GICLK
 #define GI_SEC(i)                                    \
   do {                                               \
-    if (G.sec && tid == 0) {                         \
+    if (G.sec && (tid == 0 || tid == 129)) {         \
       const unsigned long long now_ = clock64();     \
       sec_acc[i] += now_ - sec_t;                    \
       sec_t = now_;                                  \
     }                                                \
   } while (0)
+#else
+#define GI_SEC(i) \
+  do {            \
+  } while (0)
+#endif
 
 // ---- components: union-find over the takeable signals of every row of the cluster (dead rows
 // included: a unique's holder carries its row's other keys into the rows that merge with it)
@@ -246,60 +246,164 @@ __device__ inline bool d_gi_serial(const ElimArgs &A, const GiantArgs &G, Alloc 
   }
 }
 
-struct GiSmem {
-  uint32_t wk[2][kGiCap];
-  uint64_t ws[2][kGiCap];
-  Fe wv[2][kGiCap];
-  uint32_t rk[kGiCap];
-  uint64_t rs[kGiCap];
-  Fe rv[kGiCap];
-  uint32_t sc[2 * kGiCap + 1];  // exclusive scan of the packed positions' keep flags
-  uint32_t lb[2 * kGiCap];      // per packed position: lower bound in the other list
-  uint32_t wsum[2][kGiNW];
-  uint32_t s_fdel[2], s_p3[2];
-  unsigned long long s_best[2];
-  uint32_t s_comp, s_ok, s_m, s_nl;
+// ---- the component loop.  The work row lives in a kGhSlots-slot open-addressing table in LDS, one
+// slot per lane of waves 0-1 (which keep their slot's key / value / state in registers).  A merge
+// work = c2*work - c*R (:338-347) is two barriers: waves 2-3 load the holder's header and
+// right-hand side (one entry per lane, one round trip: header and RHS are contiguous in the pool),
+// multiply c*R and look each key up in the table -- a hit leaves its product in the slot's add
+// cell, a miss claims a free slot -- while waves 0-1 multiply c2*work (one 256-bit product latency
+// for the whole merge, no branch between the two products); after the first barrier every slot
+// combines (hit ? c*R - c2*w : -c2*w, the reference's order of operations), drops the pivot and the
+// cancelled keys (tombstones) and takes part in the next pivot's reduction (LDS atomics over
+// key << 8 | slot: take_signal_4's first deleted key, take_signal_3's largest takeable key); the
+// second barrier publishes it.  No scan and no sort inside the row: it is sorted once, by rank,
+// when it leaves the loop (a new substitution's right-hand side, a leftover).  Rows longer than
+// kGhRowMax and merges that could overflow the table finish on one lane (d_gi_serial) over the
+// official per-signal arrays, which this path keeps current.
+constexpr uint32_t kGhSlots = 128;
+constexpr uint32_t kGhEmpty = 0xffffffffu, kGhTomb = 0xfffffffeu;  // above every signal id (< 2^31)
+constexpr uint32_t kGhRowMax = 96;    // live entries the table takes (load <= 3/4)
+constexpr uint32_t kGhRhsMax = 127;   // right-hand-side entries: lanes 1..127 of waves 2-3 (lane 0: the header)
+constexpr uint32_t kGhUsedMax = 124;  // keys + tombstones before a merge's inserts; above it the table is rebuilt
+constexpr uint32_t kGhThreads = 2 * kGhSlots;
+static_assert(kGhUsedMax + 1 < kGhSlots && kGhRowMax + kGhRhsMax <= 2 * kGhSlots, "the table keeps an empty slot");
+
+struct __attribute__((aligned(16))) GhSmem {
+  uint32_t tk[kGhSlots];  // slot keys: kGhEmpty / kGhTomb / a signal
+  Fe tv[kGhSlots];
+  uint64_t ts[kGhSlots];  // the key's state word (gst)
+  Fe addv[kGhSlots];      // a right-hand-side hit: c*R for the slot's key
+  uint32_t addf[kGhSlots];
+  unsigned long long r_del[2], r_p3[2];  // pivot reductions (by parity): key << 8 | slot
+  uint32_t r_live[2], r_used[2], r_has0[2];
+  unsigned long long r_best;  // take_signal_4 without a deleted key: occurrences << 32 | ~key
   uint64_t s_o;
+  uint32_t s_ps, s_comp, s_ok, s_m, s_nl;
 };
 
-// block exclusive scan of the flags of positions [0, 2 * kGiT) (f0: position tid, f1: tid + kGiT);
-// writes sc[] and returns the total
-__device__ __forceinline__ uint32_t gi_scan2(GiSmem &S, bool f0, bool f1, uint32_t tid) {
-  const uint32_t lane = tid & 63, w = tid >> 6;
-  const uint64_t lt = lane ? ((1ull << lane) - 1ull) : 0ull;
-  const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
-  if (lane == 0) { S.wsum[0][w] = (uint32_t)__popcll(b0); S.wsum[1][w] = (uint32_t)__popcll(b1); }
-  __syncthreads();
-  uint32_t base0 = 0, tot0 = 0, base1 = 0, tot1 = 0;
+// values every lane holds alike (read from one LDS or global address) into scalar registers: the
+// branches on them become scalar branches and the products take them as scalar operands
+__device__ __forceinline__ uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) { return ((uint64_t)uni32((uint32_t)(x >> 32)) << 32) | uni32((uint32_t)x); }
+__device__ __forceinline__ Fe uniFe(const Fe &a) {
+  Fe r;
 #pragma unroll
-  for (int q = 0; q < kGiNW; ++q) {
-    const uint32_t x0 = S.wsum[0][q], x1 = S.wsum[1][q];
-    if (q < (int)w) { base0 += x0; base1 += x1; }
-    tot0 += x0;
-    tot1 += x1;
+  for (int i = 0; i < 4; ++i) r.l[i] = uni64(a.l[i]);
+  return r;
+}
+__device__ __forceinline__ uint32_t gh_hash(uint32_t k) { return (k * 0x9E3779B1u) >> 25; }
+__device__ __forceinline__ uint32_t gh_ld(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// claims the first free (empty or tombstone) slot of K's probe sequence (the table always has one)
+__device__ __forceinline__ uint32_t gh_claim(GhSmem &S, uint32_t K) {
+  uint32_t s = gh_hash(K);
+  for (;;) {
+    const uint32_t t = gh_ld(&S.tk[s]);
+    if (t >= kGhTomb) {
+      if (atomicCAS(&S.tk[s], t, K) == t) return s;
+      continue;  // taken meanwhile: look at the slot again
+    }
+    s = (s + 1) & (kGhSlots - 1);
   }
-  S.sc[tid] = base0 + (uint32_t)__popcll(b0 & lt);
-  S.sc[kGiT + tid] = tot0 + base1 + (uint32_t)__popcll(b1 & lt);
-  if (tid == 0) S.sc[2 * kGiT] = tot0 + tot1;
-  __syncthreads();
-  return tot0 + tot1;
+}
+// the slot holding K, or kGhEmpty.  Keys are placed at the first free slot of their sequence and
+// slots never become empty inside a row (only tombstones), so the first empty slot ends the search;
+// concurrent claims only turn free slots into other keys.
+__device__ __forceinline__ uint32_t gh_find(const GhSmem &S, uint32_t K) {
+  uint32_t s = gh_hash(K);
+  for (uint32_t i = 0; i < kGhSlots; ++i) {
+    const uint32_t t = gh_ld(&S.tk[s]);
+    if (t == K) return s;
+    if (t == kGhEmpty) break;
+    s = (s + 1) & (kGhSlots - 1);
+  }
+  return kGhEmpty;
+}
+// rank of `key` among the table's keys (empty / tombstone slots compare above every signal)
+__device__ __forceinline__ uint32_t gh_rank(const GhSmem &S, uint32_t key) {
+  uint32_t r = 0;
+#pragma unroll 8
+  for (uint32_t i = 0; i < kGhSlots; i += 4) {
+    const uint4 k4 = *reinterpret_cast<const uint4 *>(&S.tk[i]);
+    r += (k4.x < key ? 1u : 0u) + (k4.y < key ? 1u : 0u) + (k4.z < key ? 1u : 0u) + (k4.w < key ? 1u : 0u);
+  }
+  return r;
+}
+// min over the wave (every lane active), by DPP: quad swaps, half-row and row mirrors, then the row
+// broadcasts; lane 63 ends with the minimum.  The compiler's own lowering of a divergent LDS atomic
+// (one iteration per active lane) cost hundreds of cycles per merge.
+template <int ctrl, int rmask>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
+  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, ctrl, rmask, 0xf, false);
+  return o < v ? o : v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = dpp_min_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v = dpp_min_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+  v = dpp_min_step<0x141, 0xf>(v);  // row_half_mirror
+  v = dpp_min_step<0x140, 0xf>(v);  // row_mirror
+  v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// the work side's share of a pivot reduction into set q (reset beforehand); whole waves call it
+__device__ __forceinline__ void gh_reduce(GhSmem &S, uint32_t q, bool p4, uint32_t slot, uint32_t wk, uint64_t wst) {
+  const bool live = wk < kGhTomb;
+  const bool tk = live && wst != kGiForb;
+  if (p4) {  // take_signal_4: the first deleted key
+    const uint32_t dk = tk && (wst & kGiDel) ? wk : kGhEmpty;
+    const uint32_t m = wave_min_u32(dk);
+    if (m != kGhEmpty && dk == m) atomicMin(&S.r_del[q], ((unsigned long long)wk << 8) | slot);
+  } else {  // take_signal_3: the largest takeable key
+    const uint32_t nk = tk ? ~wk : kGhEmpty;
+    const uint32_t m = wave_min_u32(nk);
+    if (m != kGhEmpty && nk == m) atomicMax(&S.r_p3[q], ((unsigned long long)wk << 8) | slot);
+  }
+  const uint64_t bl = __ballot(live), bu = __ballot(wk != kGhEmpty);
+  if ((slot & 63) == 0) {
+    atomicAdd(&S.r_live[q], (uint32_t)__popcll(bl));
+    atomicAdd(&S.r_used[q], (uint32_t)__popcll(bu));
+  }
+  if (live && wk == 0) S.r_has0[q] = 1;
+}
+__device__ __forceinline__ void gh_reset(GhSmem &S, uint32_t q) {
+  S.r_del[q] = ~0ull;
+  S.r_p3[q] = 0;
+  S.r_live[q] = S.r_used[q] = S.r_has0[q] = 0;
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_gi_loop(ElimArgs A, GiantArgs G, uint64_t c) {
-  static_assert(NW == kGiNW, "GiSmem is sized for kGiNW waves");
-  __shared__ GiSmem S;
+// A barrier over LDS only: the merge's two barriers publish LDS writes (slots, add cells, the
+// reductions), never global stores, and __syncthreads()'s workgroup fence would also wait for every
+// outstanding global load -- the next holder's prefetch among them.
+__device__ __forceinline__ void gh_lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G, uint64_t c) {
+  __shared__ GhSmem S;
   const FieldP &F = A.F;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t tid = threadIdx.x;
+  const bool wsd = tid < kGhSlots;   // waves 0-1: the table's slots
+  const uint32_t slot = tid;         // (waves 0-1)
+  const uint32_t j = tid - kGhSlots; // (waves 2-3) 0: the holder's header, 1..: its right-hand side
   const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
   const bool p4 = d_is_p4(A, (uint32_t)(e - b));
   const uint32_t n_uniq = A.n_sub[c];  // the uniques phase's substitutions (k_big_prep); the loop's follow
   Alloc al0;  // thread 0's pool chunk
   al0.chunk = 4096;
   unsigned long long by = 0;
-  unsigned long long sec_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sec_t = G.sec ? clock64() : 0ull;
-  uint32_t step = 0;  // reduction-slot parity
-  if (tid == 0) { S.s_ok = 1; S.s_fdel[0] = S.s_fdel[1] = RS_NONE; S.s_best[0] = S.s_best[1] = ~0ull; S.s_p3[0] = S.s_p3[1] = 0; }
+#ifdef RS_GICLK
+  unsigned long long sec_acc[16] = {}, sec_t = G.sec ? clock64() : 0ull;
+#endif
+  uint32_t q = 0;  // the reduction set the next decision reads
+  uint32_t wk = kGhEmpty;  // (waves 0-1) the slot's key, value, state
+  Fe wv = fe_zero();
+  uint64_t wst = 0;
+  if (tid == 0) {
+    S.s_ok = 1;
+    gh_reset(S, 0);
+    gh_reset(S, 1);
+  }
+  if (wsd) S.addf[slot] = 0;
   for (;;) {
     __syncthreads();
     if (tid == 0) S.s_comp = atomicAdd(&G.scal[1], 1u);
@@ -317,12 +421,12 @@ __global__ __launch_bounds__(64 * NW) void k_gi_loop(ElimArgs A, GiantArgs G, ui
       if (!S.s_ok) break;
       const uint32_t qi = G.rval2[ii];
       const uint64_t r_off = A.row_off[b + qi];
-      uint32_t len = A.row_len[b + qi];
+      const uint32_t len = A.row_len[b + qi];
       const uint32_t *rk0 = A.rows.key + r_off;
       const Fe *rv0 = A.rows.val + r_off;
       by += 36ull * len;
-      if (len > kGiCap) {  // remove_constraint on the global state, then one lane
-        for (uint32_t i = tid; i < len; i += kGiT) {
+      if (len > kGhRowMax) {  // remove_constraint on the global state, then one lane
+        for (uint32_t i = tid; i < len; i += kGhThreads) {
           const uint32_t s = rk0[i];
           const uint64_t st = G.gst[s];
           if (p4 && st != kGiForb && !(st & kGiDel) && st > 0) { G.gst[s] = st - 1; A.occ[s] = (int32_t)(st - 1); }
@@ -335,10 +439,14 @@ __global__ __launch_bounds__(64 * NW) void k_gi_loop(ElimArgs A, GiantArgs G, ui
           S.s_nl = nl;
         }
         __syncthreads();  // thread 0's stores (state words, holders) before the next row reads them
+        GI_SEC(6);
         continue;
       }
-      uint32_t cur = 0;
-      if (tid < len) {  // the row and its keys' states; remove_constraint (:94-106): occurrences - 1
+      // ---- the row into the table; remove_constraint (:94-106): occurrences - 1
+      if (wsd) S.tk[slot] = kGhEmpty;
+      if (tid == 0) S.r_best = ~0ull;
+      __syncthreads();
+      if (tid < len) {
         const uint32_t s = rk0[tid];
         uint64_t st = G.gst[s];
         if (p4 && st != kGiForb && !(st & kGiDel) && st > 0) {
@@ -346,201 +454,209 @@ __global__ __launch_bounds__(64 * NW) void k_gi_loop(ElimArgs A, GiantArgs G, ui
           G.gst[s] = st;
           A.occ[s] = (int32_t)st;
         }
-        S.wk[0][tid] = s;
-        S.wv[0][tid] = rv0[tid];
-        S.ws[0][tid] = st;
+        const uint32_t at = gh_claim(S, s);
+        S.tv[at] = rv0[tid];
+        S.ts[at] = st;
       }
       __syncthreads();
-      GI_SEC(6);
-      while (len > 0) {
-        // ---- the pivot: p4 take_signal_4 (:379-411) first deleted key (ascending), else fewest
-        // occurrences, ties -> the largest id; p3 take_signal_3 (:368-377) the largest takeable key
-        const uint32_t sl = step & 1, sn = sl ^ 1;
-        ++step;
-        {
-          const uint64_t st = tid < len ? S.ws[cur][tid] : kGiForb;
-          const bool tk = st != kGiForb, dl = tk && (st & kGiDel);
-          const uint64_t dm = __ballot(dl), tm = __ballot(tk);
-          const uint32_t w = tid >> 6;
-          if (p4) {
-            if (dm && lane == 0) atomicMin(&S.s_fdel[sl], 64u * w + (uint32_t)(__ffsll((long long)dm) - 1));
-            unsigned long long v = (tk && !dl) ? ((st & 0xffffffffull) << 32) | (0xffffffffu - tid) : ~0ull;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-              const unsigned long long x = __shfl_xor(v, d);
-              v = x < v ? x : v;
-            }
-            if (lane == 0 && v != ~0ull) atomicMin(&S.s_best[sl], v);
-          } else if (tm && lane == 0) {
-            atomicMax(&S.s_p3[sl], 64u * w + (uint32_t)(64 - __clzll(tm)));  // 1 + the largest index
-          }
-          if (tid == 0) { S.s_fdel[sn] = RS_NONE; S.s_best[sn] = ~0ull; S.s_p3[sn] = 0; }
-        }
-        __syncthreads();
-        GI_SEC(0);
-        uint32_t oi = RS_NONE;
+      if (wsd) {
+        wk = S.tk[slot];
+        if (wk < kGhTomb) { wv = S.tv[slot]; wst = S.ts[slot]; }
+        gh_reduce(S, q, p4, slot, wk, wst);
+      }
+      __syncthreads();
+      GI_SEC(4);
+      uint32_t pend_live = 0, pend_rl = 0;  // the merge whose bytes are counted once its result is known
+      bool pend = false;
+      for (;;) {
+        // ---- the decision (set q, published by the last barrier; uniform values into scalars)
+        const unsigned long long rdel = uni64(S.r_del[q]), rp3 = uni64(S.r_p3[q]);
+        const uint32_t live = uni32(S.r_live[q]), used = uni32(S.r_used[q]), has0 = uni32(S.r_has0[q]);
+        // the other set was last read by the decision before the last barrier: thread 0 clears it for
+        // the next reduction (which comes after at least one more barrier)
+        if (tid == 0) gh_reset(S, q ^ 1);
+        q ^= 1;
+        if (pend) by += 36ull * (pend_live + pend_rl + live);
+        pend = false;
+        if (live == 0) break;  // reduced to nothing: no substitution, no leftover
+        uint32_t ps = kGhEmpty;
+        bool merge = false;
         if (p4) {
-          const uint32_t fd = S.s_fdel[sl];
-          const unsigned long long bs = S.s_best[sl];
-          oi = fd != RS_NONE ? fd : (bs != ~0ull ? 0xffffffffu - (uint32_t)(bs & 0xffffffffull) : RS_NONE);
-        } else {
-          oi = S.s_p3[sl] ? S.s_p3[sl] - 1 : RS_NONE;
+          if (rdel != ~0ull) { ps = (uint32_t)(rdel & 255); merge = true; }
+        } else if (rp3) {
+          ps = (uint32_t)(rp3 & 255);
+          merge = (uni64(S.ts[ps]) & kGiDel) != 0;
         }
-        if (oi == RS_NONE) {  // no takeable key: a leftover, unnormalised (:325-327)
-          if (tid == 0) { S.s_o = pool_alloc(A, al0, len); if (S.s_o == RS_NONE) S.s_ok = 0; }
+        GI_SEC(0);
+        if (merge) {
+          // ---- conflict with holder(p): work = c2*work - c*R (:338-347), c = -v_p
+          const uint64_t hdr = uni64(S.ts[ps]) & ~kGiDel;
+          // header and right-hand side in one round trip: the RHS lanes load before the length is known
+          const bool rlane = !wsd && j >= 1 && hdr + j < A.pool_cap;
+          uint32_t K = 0;
+          Fe R = fe_zero();
+          if (rlane) {
+            K = A.pk[hdr + j];
+            R = A.pv[hdr + j];
+          }
+          const uint32_t rl = uni32(A.pk[hdr]);
+          if (rl > kGhRhsMax || live - 1 + rl > kGhRowMax) {  // could pass the table: the rest on one lane
+            if (tid == 0) { S.s_o = pool_alloc(A, al0, live); if (S.s_o == RS_NONE) S.s_ok = 0; }
+            __syncthreads();
+            if (S.s_ok) {
+              const uint64_t o = S.s_o;
+              if (wsd && wk < kGhTomb) {
+                const uint32_t r = gh_rank(S, wk);
+                A.pk[o + r] = wk;
+                A.pv[o + r] = wv;
+              }
+              __syncthreads();
+              if (tid == 0) {
+                uint32_t m = S.s_m, nl = S.s_nl;
+                if (!d_gi_serial(A, G, al0, sub_base, left_base, qi, A.pk + o, A.pv + o, live, m, nl, p4, by)) S.s_ok = 0;
+                S.s_m = m;
+                S.s_nl = nl;
+              }
+            }
+            __syncthreads();
+            GI_SEC(6);
+            break;
+          }
+          if (used + rl > kGhUsedMax) {  // tombstones: rebuild the table from the live slots
+            const uint32_t kp = S.tk[ps];
+            __syncthreads();
+            if (wsd) S.tk[slot] = kGhEmpty;
+            __syncthreads();
+            if (wsd && wk < kGhTomb) {
+              const uint32_t at = gh_claim(S, wk);
+              S.tv[at] = wv;
+              S.ts[at] = wst;
+            }
+            __syncthreads();
+            if (wsd) {
+              wk = S.tk[slot];
+              if (wk < kGhTomb) { wv = S.tv[slot]; wst = S.ts[slot]; }
+              if (wk == kp) S.s_ps = slot;
+            }
+            __syncthreads();
+            ps = uni32(S.s_ps);
+            GI_SEC(3);
+          }
+          const Fe coef = fneg(F, uniFe(S.tv[ps]));
+          Fe c2w;
+          if (!wsd) {
+            if (rlane && j <= rl) {  // the right-hand side: c*R, then into the table
+              const uint64_t st_r = G.gst[K];
+              GI_SEC(8);
+              const uint32_t at = gh_find(S, K);
+              GI_SEC(9);
+              const Fe rv = fmul256(F, coef, R);
+              GI_SEC(10);
+              if (at != kGhEmpty) {
+                S.addv[at] = rv;
+                S.addf[at] = 1;
+              } else if (!fe_is_zero(rv)) {  // a zero-valued RHS key ({0: 0}) only ever adds into the row
+                const uint32_t f = gh_claim(S, K);
+                S.tv[f] = rv;
+                S.ts[f] = st_r;
+              }
+              GI_SEC(11);
+            }
+          } else if (wk < kGhTomb && slot != ps) {
+            c2w = fmul256(F, uniFe(A.pv[hdr]), wv);
+          }
+          gh_lds_barrier();
+          GI_SEC(1);
+          if (wsd) {
+            if (wk < kGhTomb) {
+              bool drop = slot == ps;
+              if (!drop) {
+                const Fe x = S.addf[slot] ? fsub(F, S.addv[slot], c2w) : fneg(F, c2w);
+                S.addf[slot] = 0;
+                drop = fe_is_zero(x);
+                wv = x;
+                S.tv[slot] = x;
+              }
+              if (drop) {
+                S.tk[slot] = kGhTomb;
+                wk = kGhTomb;
+              }
+            } else {
+              const uint32_t t = S.tk[slot];
+              if (t < kGhTomb) { wk = t; wv = S.tv[slot]; wst = S.ts[slot]; }
+            }
+            gh_reduce(S, q, p4, slot, wk, wst);
+          }
+          ++n_merge;
+          pend = true;
+          pend_live = live;
+          pend_rl = rl;
+          gh_lds_barrier();
+          GI_SEC(2);
+          continue;
+        }
+        // ---- the row leaves the loop
+        if (p4) {  // take_signal_4 without a deleted key: fewest occurrences, ties -> the largest id
+          if (wsd && wk < kGhTomb && wst != kGiForb)
+            atomicMin(&S.r_best, ((wst & 0xffffffffull) << 32) | (0xffffffffu - wk));
           __syncthreads();
-          by += 36ull * len;
+          const unsigned long long best = S.r_best;
+          if (best != ~0ull) {
+            if (wsd && wk == 0xffffffffu - (uint32_t)(best & 0xffffffffull)) S.s_ps = slot;
+            __syncthreads();
+            ps = S.s_ps;
+          }
+        }
+        if (ps == kGhEmpty) {  // no takeable key: a leftover, unnormalised (:325-327)
+          by += 36ull * live;
+          if (tid == 0) { S.s_o = pool_alloc(A, al0, live); if (S.s_o == RS_NONE) S.s_ok = 0; }
+          __syncthreads();
           if (S.s_ok) {
             const uint64_t o = S.s_o;
-            if (tid < len) { A.pk[o + tid] = S.wk[cur][tid]; A.pv[o + tid] = S.wv[cur][tid]; }
+            if (wsd && wk < kGhTomb) {
+              const uint32_t r = gh_rank(S, wk);
+              A.pk[o + r] = wk;
+              A.pv[o + r] = wv;
+            }
             if (tid == 0) {
               A.l_off[left_base + S.s_nl] = o;
-              A.l_len[left_base + S.s_nl] = len;
+              A.l_len[left_base + S.s_nl] = live;
               A.tmp[left_base + S.s_nl] = qi;
               S.s_nl = S.s_nl + 1;
             }
           }
-          break;
-        }
-        const uint32_t p = S.wk[cur][oi];
-        const uint64_t stp = S.ws[cur][oi];
-        if (!(stp & kGiDel)) {  // a new substitution: (coefficient, p := rest) (clear_signal_not_normalized)
-          const uint32_t sh = S.wk[cur][0] == 0 ? 0 : 1;  // {0: 0} is inserted when absent
-          const uint32_t mm = len - 1 + sh;
+        } else {  // a new substitution: (coefficient, p := rest) (clear_signal_not_normalized)
+          const uint32_t kp = S.tk[ps];
+          const Fe wpv = S.tv[ps];
+          const uint32_t sh = has0 ? 0u : 1u;  // {0: 0} is inserted when absent
+          const uint32_t mm = live - 1 + sh;
           by += 36ull * mm;
           if (tid == 0) { S.s_o = pool_alloc(A, al0, (uint64_t)mm + 1); if (S.s_o == RS_NONE) S.s_ok = 0; }
           __syncthreads();
           if (S.s_ok) {
             const uint64_t o = S.s_o;
-            if (tid < len && tid != oi) {
-              const uint32_t q = (tid < oi ? tid : tid - 1) + sh;
-              A.pk[o + 1 + q] = S.wk[cur][tid];
-              A.pv[o + 1 + q] = S.wv[cur][tid];
+            if (wsd && wk < kGhTomb && slot != ps) {
+              const uint32_t r = gh_rank(S, wk) - (kp < wk ? 1u : 0u);
+              A.pk[o + 1 + sh + r] = wk;
+              A.pv[o + 1 + sh + r] = wv;
             }
             if (tid == 0) {
-              const Fe cf = fneg(F, S.wv[cur][oi]);
+              const Fe cf = fneg(F, wpv);
               if (sh) { A.pk[o + 1] = 0; A.pv[o + 1] = fe_zero(); }
               A.pk[o] = mm;  // the header: RHS length, coefficient
               A.pv[o] = cf;
-              d_set_holder(A, p, sub_base + S.s_m, cf, o + 1, mm);
+              d_set_holder(A, kp, sub_base + S.s_m, cf, o + 1, mm);
               S.s_m = S.s_m + 1;
-              A.occ[p] = -1;
-              A.del[p] = 1;
-              G.gst[p] = kGiDel | o;
+              A.occ[kp] = -1;
+              A.del[kp] = 1;
+              G.gst[kp] = kGiDel | o;
             }
           }
-          break;
         }
-        // ---- conflict with holder(p): work = c2*work - c*R (:338-347), c = -v_p
-        const uint64_t hdr = stp & ~kGiDel;
-        const uint32_t rl = A.pk[hdr];
-        const Fe c2 = A.pv[hdr];
-        if (rl > kGiCap || len + rl > kGiCap + 1) {  // the merged list could pass the LDS lists: one lane
-          if (tid == 0) { S.s_o = pool_alloc(A, al0, len); if (S.s_o == RS_NONE) S.s_ok = 0; }
-          __syncthreads();
-          if (S.s_ok) {
-            const uint64_t o = S.s_o;
-            if (tid < len) { A.pk[o + tid] = S.wk[cur][tid]; A.pv[o + tid] = S.wv[cur][tid]; }
-            __syncthreads();
-            if (tid == 0) {
-              uint32_t m = S.s_m, nl = S.s_nl;
-              if (!d_gi_serial(A, G, al0, sub_base, left_base, qi, A.pk + o, A.pv + o, len, m, nl, p4, by)) S.s_ok = 0;
-              S.s_m = m;
-              S.s_nl = nl;
-            }
-          }
-          break;
-        }
-        GI_SEC(1);
-        // the right-hand side, one entry per lane, and its keys' states (they land under the product)
-        uint64_t st_r = kGiForb;
-        if (tid < rl) {
-          const uint32_t key = A.pk[hdr + 1 + tid];
-          S.rk[tid] = key;
-          S.rv[tid] = A.pv[hdr + 1 + tid];
-          st_r = G.gst[key];
-        }
-        const Fe coef = fneg(F, S.wv[cur][oi]);
-        __syncthreads();
-        GI_SEC(2);
-        // packed positions: q < len the work entry q, else the RHS entry q - len; each searches the
-        // other list and takes its one product
-        bool hit0 = false, hit1 = false;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t q = tid + h * kGiT;
-          if (q >= len + rl) continue;
-          bool hit;
-          uint32_t lbq;
-          if (q < len) {
-            lbq = lds_lb_e<kGiCap / 64>(S.rk, rl, S.wk[cur][q], hit);
-            S.wv[cur][q] = fmul256(F, c2, S.wv[cur][q]);
-          } else {
-            const uint32_t j = q - len;
-            lbq = lds_lb_e<kGiCap / 64>(S.wk[cur], len, S.rk[j], hit);
-            S.rv[j] = fmul256(F, coef, S.rv[j]);
-          }
-          S.lb[q] = lbq;
-          if (h == 0) hit0 = hit; else hit1 = hit;
-        }
-        if (tid < rl) S.rs[tid] = st_r;
-        __syncthreads();
-        GI_SEC(3);
-        bool keep0 = false, keep1 = false;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t q = tid + h * kGiT;
-          if (q >= len + rl) continue;
-          const bool hit = h == 0 ? hit0 : hit1;
-          bool keep;
-          if (q < len) {  // -c2*v (+ c*rv when the RHS has the key)
-            keep = false;
-            if (q != oi) {
-              const Fe pv = S.wv[cur][q];
-              const Fe x = hit ? fsub(F, S.rv[S.lb[q]], pv) : fneg(F, pv);
-              S.wv[cur][q] = x;
-              keep = !fe_is_zero(x);
-            }
-          } else {  // RHS-only keys: c*rv
-            keep = !hit && !fe_is_zero(S.rv[q - len]);
-          }
-          if (h == 0) keep0 = keep; else keep1 = keep;
-        }
-        const uint32_t nlen = gi_scan2(S, keep0, keep1, tid);
-        GI_SEC(4);
-        uint32_t tot_w = 0;
-        {  // kept work entries = the scan at position len
-          tot_w = S.sc[len];
-        }
-        const uint32_t nx = cur ^ 1;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t q = tid + h * kGiT;
-          const bool keep = h == 0 ? keep0 : keep1;
-          if (!keep) continue;
-          uint32_t pos;
-          if (q < len) {
-            const uint32_t l = S.lb[q];
-            pos = S.sc[q] + (l < rl ? S.sc[len + l] - tot_w : nlen - tot_w);
-            S.wk[nx][pos] = S.wk[cur][q];
-            S.wv[nx][pos] = S.wv[cur][q];
-            S.ws[nx][pos] = S.ws[cur][q];
-          } else {
-            const uint32_t j = q - len, l = S.lb[q];
-            pos = (S.sc[q] - tot_w) + (l < len ? S.sc[l] : tot_w);
-            S.wk[nx][pos] = S.rk[j];
-            S.wv[nx][pos] = S.rv[j];
-            S.ws[nx][pos] = S.rs[j];
-          }
-        }
-        by += 36ull * (len + rl + nlen);
-        ++n_merge;
         __syncthreads();
         GI_SEC(5);
-        cur = nx;
-        len = nlen;
+        break;
       }
-      __syncthreads();
     }
     __syncthreads();
     if (tid == 0) {
@@ -559,10 +675,12 @@ __global__ __launch_bounds__(64 * NW) void k_gi_loop(ElimArgs A, GiantArgs G, ui
   // algorithmic bytes: one atomic per workgroup (thread 0 counted the lane-serial rows)
   by = tid == 0 ? by : 0ull;
   if (tid == 0 && by) atomicAdd(A.bytes_main, by);
-  if (G.sec && tid == 0) {
+#ifdef RS_GICLK
+  if (G.sec && (tid == 0 || tid == 129)) {
     GI_SEC(7);
-    for (int i = 0; i < 8; ++i) atomicAdd(G.sec + i, sec_acc[i]);
+    for (int i = 0; i < 16; ++i) atomicAdd(G.sec + (tid ? 16 : 0) + i, sec_acc[i]);
   }
+#endif
 }
 
 // ---- results back to the cluster's slots: substitutions contiguous after the uniques' (any order:

@@ -283,6 +283,11 @@ __global__ void k_eq_assign(const uint64_t *ptr, const uint32_t *key, uint64_t n
     if (forb[a] && forb[b]) bf_list[atomicAdd(bf_n, 1u)] = (uint32_t)r;
   }
 }
+// the union-find roots of signals idx[i] (k_eq_stats / k_eq_assign compress only the paths from a
+// row's first key, so a signal met only as a second key may sit several links below its root)
+__global__ void k_uf_roots(uint32_t *uf, const uint32_t *idx, uint32_t *dst, uint64_t n) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) dst[i] = uf_find(uf, idx[i]);
+}
 __global__ void k_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t *dst, uint64_t n) {
   for (uint64_t i = gtid(); i < n; i += gstride()) dst[i] = src[idx[i]];
 }

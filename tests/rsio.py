@@ -223,11 +223,12 @@ def oracle_run(inp: RsInput, fl: RsFlags, threads=1):
 
 # --------------------------------------------------------------------------- random systems
 def gen_system(seed: int, p: int, n_sig: int = 60, n_rows: int = 80, n_out: int = 2,
-               n_pub: int = 2, big_cluster: int = 0, density: float = 1.0) -> "R.System":
+               n_pub: int = 2, big_cluster: int = 0, density: float = 1.0, extra_forb: float = 0.0) -> "R.System":
     """Seeded random --O0 system that exercises every branch of the path: eq clusters of size 1
     and > 1 with forbidden ends, duplicate/forbidden constant equalities, linear clusters for
     process_3 and (big_cluster >= 350) process_4, non-linear rows that turn linear in round 1 and
-    in later rounds, constant-A reductions and coefficient cancellations (small p)."""
+    in later rounds, constant-A reductions and coefficient cancellations (small p).  extra_forb: the
+    share of the other signals that are forbidden too (custom-gate signals, forbidden intermediates)."""
     rng = random.Random(seed)
     S = n_sig + 1
     n_priv = max(1, min(4, n_sig - n_out - n_pub))
@@ -291,6 +292,9 @@ def gen_system(seed: int, p: int, n_sig: int = 60, n_rows: int = 80, n_out: int 
             if len([k for k in m if k]) >= 3:
                 rows.append(R.Con({}, {}, m))
     forb = {0} | set(range(1, n_out + n_pub + 1))
+    if extra_forb:
+        frng = random.Random(seed ^ 0x5eed)
+        forb |= {s for s in range(n_out + n_pub + 1, S) if frng.random() < extra_forb}
     return R.System(p, S, n_out, n_pub, n_priv, forb, rows)
 
 

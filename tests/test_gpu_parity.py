@@ -60,6 +60,27 @@ def test_random_small(p):
             check(h.inp, rsio.flags(lvl, rd))
 
 
+@pytest.mark.parametrize("p", [257, R.PRIMES["bn128"]])
+def test_random_forbidden_intermediates(p):
+    """Forbidden signals beyond the public ones (circom's custom-gate signals): equality clusters whose
+    forbidden members sit several union-find links below the root (eq_cluster_simplification
+    :158-187 keeps one `f - rh` row per forbidden member), forbidden-only linear rows and constant
+    equalities on forbidden signals."""
+    m = p - 1
+    # the chain (5, 6), (2, 5) links 6 under 5 under 2: 6 is met only as a second key
+    rows = [R.Con({}, {}, {5: 3, 6: p - 3}), R.Con({}, {}, {2: 1, 5: m}), R.Con({}, {}, {3: 1, 4: m, 6: 2}),
+            R.Con({3: 1}, {4: 1}, {1: 1})]
+    sys_ = R.System(p, 7, 1, 1, 1, {0, 1, 2, 5, 6}, rows)
+    h = rsio.InputHolder(sys_)
+    for lvl in ("O1", "O2"):
+        check(h.inp, rsio.flags(lvl))
+    for seed in range(30):
+        sys_ = rsio.gen_system(5000 + seed, p, n_sig=30 + seed % 40, n_rows=50 + seed % 60, extra_forb=0.1 + 0.02 * (seed % 10))
+        h = rsio.InputHolder(sys_)
+        for lvl, rd in (("O1", None), ("O2", None), ("O2", 1)):
+            check(h.inp, rsio.flags(lvl, rd))
+
+
 @pytest.mark.parametrize("p", [257, R.PRIMES["bn128"], R.PRIMES["bls12381"]])
 def test_random_process4(p):
     for seed in range(6):

@@ -213,6 +213,20 @@ def test_refcpu_vs_pyref_random(p):
             assert rsio.same_result(ref, got) is None, (seed, key)
 
 
+@pytest.mark.parametrize("p", [257, R.PRIMES["bn128"]])
+def test_refcpu_vs_pyref_forbidden_intermediates(p):
+    """Forbidden signals beyond the public ones (custom-gate signals): eq clusters with several
+    forbidden members, forbidden-only linear rows, constant equalities on forbidden signals."""
+    for seed in range(10):
+        sys_ = rsio.gen_system(5000 + seed, p, n_sig=30 + seed % 40, n_rows=50 + seed % 60, extra_forb=0.1 + 0.02 * seed)
+        h = rsio.InputHolder(sys_)
+        for key in ("O1", "O2", "O2r1"):
+            lvl, rd = LEVELS[key]
+            ref = R.simplification(sys_, G.flags_of(lvl, rd))
+            got, _, _ = rsio.oracle_run(h.inp, rsio.flags(lvl, rd), 1 + seed % 3)
+            assert rsio.same_result(ref, got) is None, (seed, key)
+
+
 @pytest.mark.parametrize("old", [False, True])
 def test_refcpu_vs_pyref_process4(old):
     for seed in range(3):

@@ -35,15 +35,17 @@ for name in args.names or list(CONFIGS):
     inp = M.Input.synth(kind, rows, seed, prime)
     pin = M.PinnedInput(inp.c)
     best = None
+    all_ms = []
     for _ in range(args.reps):
         t0 = time.perf_counter()
         out = eng.simplify(pin.c, fl)
         dt = time.perf_counter() - t0
         st = eng.stats()
+        all_ms.append(round(dt * 1000, 1))
         if best is None or dt < best[0]:
             best = (dt, st.as_dict())
     dt, st = best
-    line = {"config": name, "rows": inp.rows(), "ms": round(dt * 1000, 2), "Mrows_per_s": round(inp.rows() / dt / 1e6, 2),
+    line = {"config": name, "rows": inp.rows(), "ms": round(dt * 1000, 2), "Mrows_per_s": round(inp.rows() / dt / 1e6, 2), "all_ms": all_ms,
             "stats": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()}}
     if args.check:
         import rsio
