@@ -270,13 +270,18 @@ static_assert(kGhUsedMax + 1 < kGhSlots && kGhRowMax + kGhRhsMax <= 2 * kGhSlots
 
 struct __attribute__((aligned(16))) GhSmem {
   uint32_t tk[kGhSlots];  // slot keys: kGhEmpty / kGhTomb / a signal
-  Fe tv[kGhSlots];
+  Fe tv[kGhSlots];        // slot values (row start and rebuilds; the merges keep them in registers)
   uint64_t ts[kGhSlots];  // the key's state word (gst)
-  Fe addv[kGhSlots];      // a right-hand-side hit: c*R for the slot's key
-  uint32_t addf[kGhSlots];
-  unsigned long long r_del[2], r_p3[2];  // pivot reductions (by parity): key << 8 | slot
-  uint32_t r_live[2], r_used[2], r_has0[2];
+  Fe rv[kGhSlots];        // c*R of right-hand-side entry j (wave 3)
+  uint32_t sj[kGhSlots];  // per slot: j + 1 of the right-hand-side entry that hit or claimed it (wave 2), else 0
+  // per-wave reduction records of the two slot waves, by parity: the wave's pivot candidate
+  // (key << 8 | slot, ~0 if none), its state word and value, live / used counts, key 0 present
+  unsigned long long w_key[2][2];
+  uint64_t w_st[2][2];
+  Fe w_val[2][2];
+  uint32_t w_live[2][2], w_used[2][2], w_has0[2][2];
   unsigned long long r_best;  // take_signal_4 without a deleted key: occurrences << 32 | ~key
+  Fe s_pv;                    // that pivot's value
   uint64_t s_o;
   uint32_t s_ps, s_comp, s_ok, s_m, s_nl;
 };
@@ -347,44 +352,40 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
-// the work side's share of a pivot reduction into set q (reset beforehand); whole waves call it
-__device__ __forceinline__ void gh_reduce(GhSmem &S, uint32_t q, bool p4, uint32_t slot, uint32_t wk, uint64_t wst) {
+// a slot wave's share of a pivot reduction into set q: the wave's candidate by DPP (take_signal_4:
+// the smallest deleted key; take_signal_3: the largest takeable key), written with its state and
+// value by the lane that holds it, so the decision needs one LDS round trip and no atomics
+__device__ __forceinline__ void gh_reduce(GhSmem &S, uint32_t q, bool p4, uint32_t slot, uint32_t wk, uint64_t wst, const Fe &wv) {
+  const uint32_t w = slot >> 6;
   const bool live = wk < kGhTomb;
   const bool tk = live && wst != kGiForb;
-  if (p4) {  // take_signal_4: the first deleted key
-    const uint32_t dk = tk && (wst & kGiDel) ? wk : kGhEmpty;
-    const uint32_t m = wave_min_u32(dk);
-    if (m != kGhEmpty && dk == m) atomicMin(&S.r_del[q], ((unsigned long long)wk << 8) | slot);
-  } else {  // take_signal_3: the largest takeable key
-    const uint32_t nk = tk ? ~wk : kGhEmpty;
-    const uint32_t m = wave_min_u32(nk);
-    if (m != kGhEmpty && nk == m) atomicMax(&S.r_p3[q], ((unsigned long long)wk << 8) | slot);
+  const uint32_t cand = p4 ? (tk && (wst & kGiDel) ? wk : kGhEmpty) : (tk ? ~wk : kGhEmpty);
+  const uint32_t m = wave_min_u32(cand);
+  if (m != kGhEmpty && cand == m) {
+    S.w_key[q][w] = ((unsigned long long)wk << 8) | slot;
+    S.w_st[q][w] = wst;
+    S.w_val[q][w] = wv;
   }
-  const uint64_t bl = __ballot(live), bu = __ballot(wk != kGhEmpty);
+  const uint64_t bl = __ballot(live), bu = __ballot(wk != kGhEmpty), b0 = __ballot(live && wk == 0);
   if ((slot & 63) == 0) {
-    atomicAdd(&S.r_live[q], (uint32_t)__popcll(bl));
-    atomicAdd(&S.r_used[q], (uint32_t)__popcll(bu));
+    if (m == kGhEmpty) S.w_key[q][w] = ~0ull;
+    S.w_live[q][w] = (uint32_t)__popcll(bl);
+    S.w_used[q][w] = (uint32_t)__popcll(bu);
+    S.w_has0[q][w] = b0 ? 1u : 0u;
   }
-  if (live && wk == 0) S.r_has0[q] = 1;
-}
-__device__ __forceinline__ void gh_reset(GhSmem &S, uint32_t q) {
-  S.r_del[q] = ~0ull;
-  S.r_p3[q] = 0;
-  S.r_live[q] = S.r_used[q] = S.r_has0[q] = 0;
 }
 
-// A barrier over LDS only: the merge's two barriers publish LDS writes (slots, add cells, the
+// A barrier over LDS only: the merge's two barriers publish LDS writes (slots, products, the
 // reductions), never global stores, and __syncthreads()'s workgroup fence would also wait for every
-// outstanding global load -- the next holder's prefetch among them.
+// outstanding global load.
 __device__ __forceinline__ void gh_lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G, uint64_t c) {
   __shared__ GhSmem S;
   const FieldP &F = A.F;
-  const uint32_t tid = threadIdx.x;
-  const bool wsd = tid < kGhSlots;   // waves 0-1: the table's slots
-  const uint32_t slot = tid;         // (waves 0-1)
-  const uint32_t j = tid - kGhSlots; // (waves 2-3) 0: the holder's header, 1..: its right-hand side
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool wsd = tid < kGhSlots;  // waves 0-1: the table's slots; wave 2: lookups / claims; wave 3: c*R
+  const uint32_t slot = tid;
   const uint64_t b = A.cl_off[c], e = A.cl_off[c + 1];
   const bool p4 = d_is_p4(A, (uint32_t)(e - b));
   const uint32_t n_uniq = A.n_sub[c];  // the uniques phase's substitutions (k_big_prep); the loop's follow
@@ -398,12 +399,8 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
   uint32_t wk = kGhEmpty;  // (waves 0-1) the slot's key, value, state
   Fe wv = fe_zero();
   uint64_t wst = 0;
-  if (tid == 0) {
-    S.s_ok = 1;
-    gh_reset(S, 0);
-    gh_reset(S, 1);
-  }
-  if (wsd) S.addf[slot] = 0;
+  if (tid == 0) S.s_ok = 1;
+  if (wsd) S.sj[slot] = 0;
   for (;;) {
     __syncthreads();
     if (tid == 0) S.s_comp = atomicAdd(&G.scal[1], 1u);
@@ -462,42 +459,43 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
       if (wsd) {
         wk = S.tk[slot];
         if (wk < kGhTomb) { wv = S.tv[slot]; wst = S.ts[slot]; }
-        gh_reduce(S, q, p4, slot, wk, wst);
+        gh_reduce(S, q, p4, slot, wk, wst, wv);
       }
       __syncthreads();
       GI_SEC(4);
       uint32_t pend_live = 0, pend_rl = 0;  // the merge whose bytes are counted once its result is known
       bool pend = false;
       for (;;) {
-        // ---- the decision (set q, published by the last barrier; uniform values into scalars)
-        const unsigned long long rdel = uni64(S.r_del[q]), rp3 = uni64(S.r_p3[q]);
-        const uint32_t live = uni32(S.r_live[q]), used = uni32(S.r_used[q]), has0 = uni32(S.r_has0[q]);
-        // the other set was last read by the decision before the last barrier: thread 0 clears it for
-        // the next reduction (which comes after at least one more barrier)
-        if (tid == 0) gh_reset(S, q ^ 1);
+        // ---- the decision: set q's two wave records (one LDS round trip), into scalars
+        const unsigned long long k0 = uni64(S.w_key[q][0]), k1 = uni64(S.w_key[q][1]);
+        const uint64_t st0 = uni64(S.w_st[q][0]), st1 = uni64(S.w_st[q][1]);
+        const Fe v0 = uniFe(S.w_val[q][0]), v1 = uniFe(S.w_val[q][1]);
+        const uint32_t live = uni32(S.w_live[q][0] + S.w_live[q][1]);
+        const uint32_t used = uni32(S.w_used[q][0] + S.w_used[q][1]);
+        const uint32_t has0 = uni32(S.w_has0[q][0] | S.w_has0[q][1]);
         q ^= 1;
         if (pend) by += 36ull * (pend_live + pend_rl + live);
         pend = false;
         if (live == 0) break;  // reduced to nothing: no substitution, no leftover
-        uint32_t ps = kGhEmpty;
-        bool merge = false;
-        if (p4) {
-          if (rdel != ~0ull) { ps = (uint32_t)(rdel & 255); merge = true; }
-        } else if (rp3) {
-          ps = (uint32_t)(rp3 & 255);
-          merge = (uni64(S.ts[ps]) & kGiDel) != 0;
-        }
+        // p4: the smaller key (~0: none); p3: the larger valid key
+        const bool w1 = p4 ? k1 < k0 : (k0 == ~0ull || (k1 != ~0ull && k1 > k0));
+        const unsigned long long kw = w1 ? k1 : k0;
+        const uint64_t pst = w1 ? st1 : st0;
+        const Fe pval = w1 ? v1 : v0;
+        const bool any = kw != ~0ull;
+        uint32_t ps = any ? (uint32_t)(kw & 255) : kGhEmpty;
+        const bool merge = any && (pst & kGiDel) != 0;  // p4's candidates are deleted keys
         GI_SEC(0);
         if (merge) {
           // ---- conflict with holder(p): work = c2*work - c*R (:338-347), c = -v_p
-          const uint64_t hdr = uni64(S.ts[ps]) & ~kGiDel;
-          // header and right-hand side in one round trip: the RHS lanes load before the length is known
-          const bool rlane = !wsd && j >= 1 && hdr + j < A.pool_cap;
+          const uint64_t hdr = pst & ~kGiDel;
+          // header and right-hand side in one round trip: waves 2-3 load before the length is known
+          const bool rlane = !wsd && lane >= 1 && hdr + lane < A.pool_cap;
           uint32_t K = 0;
           Fe R = fe_zero();
           if (rlane) {
-            K = A.pk[hdr + j];
-            R = A.pv[hdr + j];
+            if (wave == 2) K = A.pk[hdr + lane];
+            R = A.pv[hdr + lane];
           }
           const uint32_t rl = uni32(A.pk[hdr]);
           if (rl > kGhRhsMax || live - 1 + rl > kGhRowMax) {  // could pass the table: the rest on one lane
@@ -523,8 +521,7 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
             break;
           }
           if (used + rl > kGhUsedMax) {  // tombstones: rebuild the table from the live slots
-            const uint32_t kp = S.tk[ps];
-            __syncthreads();
+            const uint32_t kp = (uint32_t)(kw >> 8);
             if (wsd) S.tk[slot] = kGhEmpty;
             __syncthreads();
             if (wsd && wk < kGhTomb) {
@@ -542,25 +539,28 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
             ps = uni32(S.s_ps);
             GI_SEC(3);
           }
-          const Fe coef = fneg(F, uniFe(S.tv[ps]));
           Fe c2w;
-          if (!wsd) {
-            if (rlane && j <= rl) {  // the right-hand side: c*R, then into the table
-              const uint64_t st_r = G.gst[K];
-              GI_SEC(8);
-              const uint32_t at = gh_find(S, K);
-              GI_SEC(9);
-              const Fe rv = fmul256(F, coef, R);
-              GI_SEC(10);
+          if (wave == 3) {  // c*R, entry j = lane (+ 64)
+            const Fe coef = fneg(F, pval);
+            for (uint32_t jj = lane; jj <= rl; jj += 64) {
+              if (jj == 0) continue;
+              const Fe Rj = jj == lane ? R : A.pv[hdr + jj];
+              S.rv[jj] = fmul256(F, coef, Rj);
+            }
+          } else if (wave == 2) {  // each key into the table: a hit marks its slot, a miss claims one
+            for (uint32_t jj = lane; jj <= rl; jj += 64) {
+              if (jj == 0) continue;
+              const uint32_t Kj = jj == lane ? K : A.pk[hdr + jj];
+              const Fe Rj = jj == lane ? R : A.pv[hdr + jj];
+              const uint64_t st_r = G.gst[Kj];
+              const uint32_t at = gh_find(S, Kj);
               if (at != kGhEmpty) {
-                S.addv[at] = rv;
-                S.addf[at] = 1;
-              } else if (!fe_is_zero(rv)) {  // a zero-valued RHS key ({0: 0}) only ever adds into the row
-                const uint32_t f = gh_claim(S, K);
-                S.tv[f] = rv;
+                S.sj[at] = jj + 1;
+              } else if (!fe_is_zero(Rj)) {  // a zero-valued RHS key ({0: 0}) only ever adds into the row
+                const uint32_t f = gh_claim(S, Kj);
                 S.ts[f] = st_r;
+                S.sj[f] = jj + 1;
               }
-              GI_SEC(11);
             }
           } else if (wk < kGhTomb && slot != ps) {
             c2w = fmul256(F, uniFe(A.pv[hdr]), wv);
@@ -568,24 +568,25 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
           gh_lds_barrier();
           GI_SEC(1);
           if (wsd) {
+            const uint32_t sjv = S.sj[slot];
+            if (sjv) S.sj[slot] = 0;
             if (wk < kGhTomb) {
               bool drop = slot == ps;
               if (!drop) {
-                const Fe x = S.addf[slot] ? fsub(F, S.addv[slot], c2w) : fneg(F, c2w);
-                S.addf[slot] = 0;
+                const Fe x = sjv ? fsub(F, S.rv[sjv - 1], c2w) : fneg(F, c2w);
                 drop = fe_is_zero(x);
                 wv = x;
-                S.tv[slot] = x;
               }
               if (drop) {
                 S.tk[slot] = kGhTomb;
                 wk = kGhTomb;
               }
-            } else {
-              const uint32_t t = S.tk[slot];
-              if (t < kGhTomb) { wk = t; wv = S.tv[slot]; wst = S.ts[slot]; }
+            } else if (sjv) {  // a key the right-hand side brought in
+              wk = S.tk[slot];
+              wst = S.ts[slot];
+              wv = S.rv[sjv - 1];
             }
-            gh_reduce(S, q, p4, slot, wk, wst);
+            gh_reduce(S, q, p4, slot, wk, wst, wv);
           }
           ++n_merge;
           pend = true;
@@ -596,15 +597,19 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
           continue;
         }
         // ---- the row leaves the loop
+        uint32_t kp = any ? (uint32_t)(kw >> 8) : 0u;
+        Fe wpv = pval;
         if (p4) {  // take_signal_4 without a deleted key: fewest occurrences, ties -> the largest id
           if (wsd && wk < kGhTomb && wst != kGiForb)
             atomicMin(&S.r_best, ((wst & 0xffffffffull) << 32) | (0xffffffffu - wk));
           __syncthreads();
-          const unsigned long long best = S.r_best;
+          const unsigned long long best = uni64(S.r_best);
           if (best != ~0ull) {
-            if (wsd && wk == 0xffffffffu - (uint32_t)(best & 0xffffffffull)) S.s_ps = slot;
+            kp = 0xffffffffu - (uint32_t)(best & 0xffffffffull);
+            if (wsd && wk == kp) { S.s_ps = slot; S.s_pv = wv; }
             __syncthreads();
-            ps = S.s_ps;
+            ps = uni32(S.s_ps);
+            wpv = uniFe(S.s_pv);
           }
         }
         if (ps == kGhEmpty) {  // no takeable key: a leftover, unnormalised (:325-327)
@@ -626,8 +631,6 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
             }
           }
         } else {  // a new substitution: (coefficient, p := rest) (clear_signal_not_normalized)
-          const uint32_t kp = S.tk[ps];
-          const Fe wpv = S.tv[ps];
           const uint32_t sh = has0 ? 0u : 1u;  // {0: 0} is inserted when absent
           const uint32_t mm = live - 1 + sh;
           by += 36ull * mm;
