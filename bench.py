@@ -241,6 +241,7 @@ def main():
     ap.add_argument("--no-flatten", action="store_true", help="skip the rs_flatten_dag extra measurement")
     ap.add_argument("--no-templated", action="store_true", help="skip the template-replicated extra circuit")
     ap.add_argument("--no-o1", action="store_true", help="skip the --O1 extra (the metric circuit at circom's default level)")
+    ap.add_argument("--no-linear1m", action="store_true", help="skip BASELINE configs[1] (1 M purely linear rows, one run)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,6 +311,25 @@ def main():
                             f"(SURVEY 8(d) config 5's replication), host -> host"}
         tpin.free()
         tinp.free()
+    # ---- extra: BASELINE configs[1], 1 M purely linear rows (synth_linear seed 1: one 559 k-row cluster
+    # whose largest takeable component -- 100 k rows, 9.9 M merges -- runs the giant path's table loop;
+    # latency-bound).  One host -> host run (the pool is sized for it up front); parity at
+    # reduced size in tests/test_gpu_giant.py
+    lin = None
+    if rank == 0 and world == 1 and not args.no_linear1m:
+        linp = M.Input.synth(1, 1_000_000, 1, args.prime)
+        lpin = M.PinnedInput(linp.c)
+        t0 = time.perf_counter()
+        eng.simplify(lpin.c, fl)
+        ldt = time.perf_counter() - t0
+        lst = eng.stats()
+        lin = {"value": round(linp.rows() / ldt, 1), "unit": "constraints/s", "ms_per_step": round(ldt * 1000.0, 1),
+               "steps": 1, "constraints": linp.rows(), "max_cluster": int(lst.max_cluster),
+               "giant_ms": round(lst.giant_ms, 1), "giant_merges": int(lst.giant_merges),
+               "merges_per_us": round(lst.giant_merges / max(lst.giant_ms * 1000.0, 1e-9), 3),
+               "workload": f"synth_linear rows=1000000 seed=1 {args.prime} --O2 (BASELINE configs[1]), host -> host"}
+        lpin.free()
+        linp.free()
     # ---- extra: --O1, circom's default since 2.2.0 (circom/src/input_user.rs:304): the same circuit,
     # host -> host; no linear elimination, the linear rows join lconst (constraint_simplification.rs:575-577)
     o1 = None
@@ -416,6 +436,8 @@ def main():
             line["flatten_dag"] = flat
         if tmpl is not None:
             line["templated"] = tmpl
+        if lin is not None:
+            line["linear1M"] = lin
         if o1 is not None:
             got1 = o1.pop("_arrays", None)
             if got1 is not None:

@@ -1719,6 +1719,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipEventRecord(E->evx[10], E->st2));
         if (!giants.empty()) {  // beside the speculative loop, joined before the head's inversion
           HC(hipStreamWaitEvent(E->stg, E->evx[10], 0));
+          HC(hipMemsetAsync(GA.scal + 5, 0, 4, E->stg));  // the merge count over this run's giants
           HC(hipEventRecord(E->evgt[0], E->stg));
           ElimArgs ag = a;
           ag.bytes_main = a.bytes + 7;
@@ -1970,6 +1971,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         HC(hipEventElapsedTime(&mg, E->evgt[0], E->evgt[1]));
         E->stats.giant_ms += mg;
         E->stats.giant_launches++;
+        uint32_t nmg = 0;
+        HC(hipMemcpy(&nmg, GA.scal + 5, 4, hipMemcpyDeviceToHost));
+        E->stats.giant_merges += nmg;
       }
       if (n_tail) {
         float m0 = 0, m1 = 0, m2 = 0;

@@ -54,7 +54,7 @@ struct GiantArgs {
   uint32_t *cidx, *cidx2;
   uint32_t *c_nsub, *c_nleft;  // per component: substitutions / leftovers it made
   uint32_t *c_dsub;            // exclusive scan of c_nsub
-  uint32_t *scal;              // [0] components, [1] next component, [3] substitutions, [4] leftovers
+  uint32_t *scal;              // [0] components, [1] next component, [3] substitutions, [4] leftovers, [5] merges
   uint32_t *t_sig;             // compaction temporaries (per substitution / per position)
   Fe *t_coef;
   uint64_t *t_off;
@@ -665,6 +665,7 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
     if (tid == 0) {
       G.c_nsub[comp] = S.s_m;
       G.c_nleft[comp] = S.s_nl;
+      if (n_merge) atomicAdd(&G.scal[5], n_merge);
       if (G.c_clk) {
         G.c_clk[comp] = wall_clock64() - clk0;
         G.c_merges[comp] = n_merge;

@@ -238,6 +238,7 @@ typedef struct rs_stats {
   double giant_ms;             /* the giant path (giant_loop.hpp): component loops of the largest clusters */
   uint64_t giant_bytes;
   uint64_t giant_launches;
+  uint64_t giant_merges;        /* merges work = c2*work - c*R the giant path's table loop performed (configs[1]: 21.6 M) */
 } rs_stats;
 
 typedef struct rs_engine rs_engine;

@@ -207,6 +207,7 @@ pub struct rs_stats {
     pub giant_ms: f64,
     pub giant_bytes: u64,
     pub giant_launches: u64,
+    pub giant_merges: u64,
 }
 
 #[repr(C)]

@@ -16,7 +16,7 @@ TAG=${1:-round4}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu --no-flatten --no-templated --no-o1"
+B="python3 bench.py --no-cpu --no-flatten --no-templated --no-o1 --no-linear1m"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- \
   $B --steps 5 --warmup 2 > $OUT/trace_bench.log 2>&1
 echo "trace done"
