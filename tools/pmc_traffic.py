@@ -24,7 +24,34 @@ GROUPS = {
     "k_big_main<256> (tail)": ("k_big_main<256u>", "k_p3_fast"),
     "k_frames_wave<0> (non-linear)": ("k_frames_wave<0>",),
     "k_frames_wave<1> (rounds)": ("k_frames_wave<1>",),
+    "k_batch_inv_flat + k_big_finish<4> (tail normalisation + composition)": ("k_big_finish<4>", "k_batch_inv_flat"),
+    "k_batch_inv_tree .. k_big_emit (head normalisation + composition)": (
+        "k_big_finish<8>", "k_batch_inv_tree", "k_normalize(", "k_compose_level<", "k_compose_rest<", "k_compose_big(",
+        "k_big_emit<"),
+    "k_eliminate (clusters under 32 rows)": ("k_eliminate(",),
+    "build_clusters (k_cl_*, pair sort, arena replays)": ("k_cl_link(", "k_cl_root(", "k_cl_count(", "k_cl_replay_wave<",
+                                                          "k_cl_replay_lane("),
+    "k_gi_* (giant clusters' component loops)": ("k_gi_loop(", "k_gi_state(", "k_gi_union(", "k_gi_rowkey(",
+                                                "k_gi_segment(", "k_gi_gather(", "k_gi_scatter("),
 }
+
+
+def coverage(stats_csv):
+    """Share of the trace's kernel time the groups cover (rocprofv3 --stats kernel_stats.csv; the
+    runtime's own copy / fill kernels are left out of the total)."""
+    tot, cov, per = 0.0, 0.0, {}
+    for r in csv.DictReader(open(stats_csv)):
+        name, ns = r["Name"], float(r["TotalDurationNs"])
+        if name.startswith("__amd_rocclr_"):
+            continue
+        tot += ns
+        for g, pats in GROUPS.items():
+            if any(p in name for p in pats):
+                cov += ns
+                per[g] = per.get(g, 0.0) + ns
+                break
+    return {"covered": round(cov / tot, 4) if tot else None, "kernel_ms_total": round(tot / 1e6, 2),
+            "group_ms": {g: round(v / 1e6, 2) for g, v in per.items()}, "source": stats_csv}
 
 
 def per_dispatch(d, counter):
@@ -55,6 +82,7 @@ def main():
     ap.add_argument("--calib", default=None, help="profiles/roundN_pmc_calib.json (tools/pmc_calib.py): bytes moved "
                     "from the counters with the factors of the gather / emit patterns instead of FETCH_SIZE x2")
     ap.add_argument("--bench", default="bench.py --steps K --warmup 0 --no-cpu", help="what the passes ran (for the record)")
+    ap.add_argument("--stats", default=None, help="rocprofv3 --stats kernel_stats.csv of the bench: the groups' coverage")
     args = ap.parse_args()
     fe = per_dispatch(args.fetch_dir, "FETCH_SIZE")
     wr = per_dispatch(args.write_dir, "WRITE_SIZE")
@@ -99,6 +127,9 @@ def main():
         sys.stderr.write(f"{name}: FETCH_SIZE(x2) {fetch / 1e6:.1f} MB + WRITE_SIZE {write / 1e6:.1f} MB per launch"
                          + (f"; write requests {det.get('wrreq')} ({det.get('wrreq_64B')} of 64 B)" if "wrreq" in det else "")
                          + "\n")
+    if args.stats:
+        res["coverage"] = coverage(args.stats)
+        sys.stderr.write(f"coverage of the kernel time: {res['coverage']['covered']}\n")
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)
 
