@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
         // ---- the decision: set q's two wave records (one LDS round trip), into scalars
         const unsigned long long k0 = uni64(S.w_key[q][0]), k1 = uni64(S.w_key[q][1]);
         const uint64_t st0 = uni64(S.w_st[q][0]), st1 = uni64(S.w_st[q][1]);
-        const Fe v0 = uniFe(S.w_val[q][0]), v1 = uniFe(S.w_val[q][1]);
+        const Fe v0 = S.w_val[q][0], v1 = S.w_val[q][1];  // values stay per lane (vector registers): scalars are scarce
         const uint32_t live = uni32(S.w_live[q][0] + S.w_live[q][1]);
         const uint32_t used = uni32(S.w_used[q][0] + S.w_used[q][1]);
         const uint32_t has0 = uni32(S.w_has0[q][0] | S.w_has0[q][1]);
@@ -563,7 +563,7 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
               }
             }
           } else if (wk < kGhTomb && slot != ps) {
-            c2w = fmul256(F, uniFe(A.pv[hdr]), wv);
+            c2w = fmul256(F, A.pv[hdr], wv);
           }
           gh_lds_barrier();
           GI_SEC(1);
