@@ -304,18 +304,17 @@ def test_one_rank_fails_others_released():
             e.close()
 
 
-def _run_20m_world4():
-    """The body of test_sharded_hosthost_bls12381_20m_world4, run in a child process (python
-    tests/test_gpu_sharded.py 20m): its engines each hold the whole 20 M-row problem (~51 GB of device
-    memory), which leaves no room for the engines the earlier tests of this process keep -- and eight
-    of them do not fit the card at all, so the 20 M case runs at world 4 and world 8 at 2 M."""
+def _run_20m(world):
+    """The body of test_sharded_hosthost_bls12381_20m_world{4,8}, run in a child process (python
+    tests/test_gpu_sharded.py 20m WORLD): its engines each hold the whole 20 M-row problem (~36 GB of
+    device memory at world 1), which leaves no room for the engines the earlier tests of this process
+    keep; eight of them fit the card's 309 GB."""
     import sys
     import time
-    world = 4
     t0 = time.time()
 
     def say(what):  # progress (a quiet minute reads as a hang on the GPU box)
-        print(f"[20M world 4] {what} at {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+        print(f"[20M world {world}] {what} at {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
 
     def tick():
         while True:
@@ -345,21 +344,22 @@ def _run_20m_world4():
     say("arrays equal on every rank")
 
 
-def test_sharded_hosthost_bls12381_20m_world4():
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_hosthost_bls12381_20m(world):
     """BASELINE configs[4] at its stated size: --prime bls12381, the 20 M-row mixed circuit, ONE circuit
-    over 4 ranks host -> host (split upload, sharded elimination with the exchange, split result
+    over 4 and 8 ranks host -> host (split upload, sharded elimination with the exchange, split result
     copy), every rank array for array equal to the single-GPU oracle.  In one child process on one GPU
-    (4 engines and an in-process group made for it)."""
+    (the engines and an in-process group made for it)."""
     import os
     import subprocess
     import sys
     release_groups()
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "20m"], stdout=sys.__stderr__, stderr=sys.__stderr__,
-                       timeout=280, cwd=os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "20m", str(world)], stdout=sys.__stderr__,
+                       stderr=sys.__stderr__, timeout=290, cwd=os.path.dirname(os.path.abspath(__file__)))
     assert r.returncode == 0, f"child exited with {r.returncode}"
 
 
 if __name__ == "__main__":
     import sys
-    if sys.argv[1:] == ["20m"]:
-        _run_20m_world4()
+    if sys.argv[1:2] == ["20m"]:
+        _run_20m(int(sys.argv[2]) if len(sys.argv) > 2 else 4)
