@@ -44,3 +44,22 @@ for s, e, q, n in call:
         print(f"{(s - T0) / 1e6:8.2f} {(e - s) / 1e6:7.2f} {q:>4} {n}")
 end = max(e for _, e, _, _ in call)
 print(f"end {(end - T0) / 1e6:.2f} ms; busy per stream: " + ", ".join(f"{q} {v / 1e6:.1f}" for q, v in sorted(busy.items())))
+# the link after the input: D2H-idle gaps (no device -> host copy in flight) between the end of the
+# last host -> device copy and the end of the call
+h2d = [e for s, e, q, n in call if n == "copy HOST_TO_DEVICE"]
+d2h = sorted((s, e) for s, e, q, n in call if n == "copy DEVICE_TO_HOST")
+if h2d and d2h:
+    t_in = max(h2d)
+    gaps, cov = [], t_in
+    for s, e in d2h:
+        if e <= t_in:
+            continue
+        if s > cov:
+            gaps.append(((cov - T0) / 1e6, (s - cov) / 1e6))
+        cov = max(cov, e)
+    if end > cov:
+        gaps.append(((cov - T0) / 1e6, (end - cov) / 1e6))
+    big = [g for g in gaps if g[1] > 0.5]
+    print(f"H2D ends {(t_in - T0) / 1e6:.2f} ms; D2H-idle gaps after it over 0.5 ms (start, length): "
+          + (", ".join(f"{a:.2f}+{b:.2f}" for a, b in big) if big else "none")
+          + f"; longest {max((g[1] for g in gaps), default=0.0):.2f} ms")
