@@ -340,3 +340,92 @@ def test_json_decimal_edges():
         cj = os.path.join(tmp, "c.json")
         abi.check(abi.lib().rs_write_constraints_json(cj.encode(), C.byref(h.out)))
         assert open(cj).read() == '{\n"constraints": [\n]\n}'
+
+
+def _streamed_copy(o, rng):
+    """ABI 8's streamed layout of CSR result `o` (rs_engine_simplify's form): each block's rows in a
+    shuffled storage order with unused entries between runs, u32 lengths with RS_ROW_JUMP, jump tables.
+    Returns (RsOutput, keepalive arrays)."""
+    keep = []
+    s = abi.RsOutput()
+    s.n_constraints = o.n_constraints
+    s.n_labels, s.label_to_wire, s.n_wires = o.n_labels, o.label_to_wire, o.n_wires
+    s.no_private_inputs_witness = o.no_private_inputs_witness
+    n = int(o.n_constraints)
+    for q, nm in enumerate("abc"):
+        lc = getattr(o, nm)
+        ptr, col, val = abi.block_csr(lc)
+        lens = np.diff(ptr.astype(np.int64))
+        # storage: rows cut into runs (a random split), runs placed in a shuffled order with gaps
+        cuts = sorted(set([0, n] + [int(x) for x in rng.choice(np.arange(1, max(n, 2)), size=min(n // 2, 6), replace=False)]))
+        runs = [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1) if cuts[i] < cuts[i + 1]]
+        order = list(range(len(runs)))
+        rng.shuffle(order)
+        start = np.zeros(n, np.int64)
+        pos = 0
+        ncol, nval = [], []
+        for ri in order:
+            lo, hi = runs[ri]
+            pos += int(rng.integers(0, 3))  # unused entries before the run
+            ncol.append(np.full(pos - sum(len(x) for x in ncol), 0xdeadbeef, np.uint32))
+            nval.append(np.full(4 * (pos - sum(len(x) for x in nval) // 4), 7, np.uint64))
+            for r in range(lo, hi):
+                start[r] = pos
+                a, b = int(ptr[r]), int(ptr[r + 1])
+                ncol.append(col[a:b])
+                nval.append(val[4 * a:4 * b])
+                pos += b - a
+        c2 = np.concatenate(ncol) if ncol else np.zeros(0, np.uint32)
+        v2 = np.concatenate(nval) if nval else np.zeros(0, np.uint64)
+        c2 = np.ascontiguousarray(np.concatenate([c2, np.zeros(1, np.uint32)]))
+        v2 = np.ascontiguousarray(np.concatenate([v2, np.zeros(4, np.uint64)]))
+        ln = lens.astype(np.uint32)
+        jumps = []
+        for r in range(n):
+            prev_end = start[r - 1] + lens[r - 1] if r else 0
+            if start[r] != prev_end:
+                ln[r] |= np.uint32(abi.ROW_JUMP)
+                jumps.append(start[r])
+        jt = np.ascontiguousarray(np.array(jumps + [0], np.uint64))
+        keep += [c2, v2, ln, jt]
+        L = abi.RsLc()
+        L.n_rows, L.nnz = n, pos
+        L.ptr = C.POINTER(C.c_uint64)()
+        L.col = c2.ctypes.data_as(C.POINTER(C.c_uint32))
+        L.val = v2.ctypes.data_as(C.POINTER(C.c_uint64))
+        setattr(s, nm, L)
+        setattr(s, nm + "_len", ln.ctypes.data_as(C.POINTER(C.c_uint32)))
+        setattr(s, nm + "_jump", jt.ctypes.data_as(C.POINTER(C.c_uint64)))
+        setattr(s, nm + "_njump", len(jumps))
+    return s, keep
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_streamed_row_layout_readers_and_writers(seed):
+    """ABI 8's streamed result layout (lengths + RS_ROW_JUMP + jump tables, include/rs_simplify.h
+    rs_rows_next): the host .r1cs / constraints-json writers and abi.block_csr read it exactly as the
+    CSR form of the same result."""
+    rng = np.random.default_rng(seed)
+    sys_ = rsio.gen_system(90 + seed, R.PRIMES["bn128"], n_sig=80, n_rows=120)
+    h = rsio.InputHolder(sys_)
+    lib = rsio.oracle_lib()
+    out = C.POINTER(abi.RsOutput)()
+    ms, rounds = C.c_double(), C.c_uint64()
+    assert lib.refcpu_simplify(C.byref(h.inp), C.byref(rsio.flags("O2")), 1, C.byref(out), C.byref(ms), C.byref(rounds)) == 0
+    try:
+        o = out.contents
+        st, keep = _streamed_copy(o, rng)
+        assert any(getattr(st, nm + "_njump") for nm in "abc")
+        for q in range(3):
+            a = abi.block_csr(*o.block(q))
+            b = abi.block_csr(*st.block(q))
+            assert all(np.array_equal(x, y) for x, y in zip(a, b))
+        with tempfile.TemporaryDirectory() as tmp:
+            for name, fn in (("r1cs", lambda p, x: abi.lib().rs_write_r1cs(p, C.byref(h.inp), C.byref(x))),
+                             ("json", lambda p, x: abi.lib().rs_write_constraints_json(p, C.byref(x)))):
+                p1, p2 = os.path.join(tmp, "csr." + name), os.path.join(tmp, "st." + name)
+                abi.check(fn(p1.encode(), o))
+                abi.check(fn(p2.encode(), st))
+                assert open(p1, "rb").read() == open(p2, "rb").read(), name
+    finally:
+        lib.refcpu_output_free(out)
