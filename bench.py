@@ -105,6 +105,9 @@ KERNELS = (  # (name, stats fields: ms, bytes, launches)
     ("k_eliminate (clusters under 32 rows)", "small_ms", "small_bytes", "small_launches"),
     ("build_clusters (k_cl_*, pair sort, arena replays)", "cluster_dev_ms", "cluster_bytes", "cluster_launches"),
     ("k_gi_* (giant clusters' component loops)", "giant_ms", "giant_bytes", "giant_launches"),
+    ("input checks (k_check_ptr, k_check_keys, k_sort_validate)", "check_ms", "check_bytes", "check_launches"),
+    ("ragged conversion + linear frames (k_make_ragged, k_lin_*frames*)", "ragged_ms", "ragged_bytes", "ragged_launches"),
+    ("result gathers (k_snap_gather*, k_lc_*, k_gather_late, k_gather_rows)", "gather_ms", "gather_bytes", "gather_launches"),
 )
 
 

@@ -164,6 +164,50 @@ static void launch(hipStream_t st, K kernel, uint64_t n, Args... args) {
   HC(hipGetLastError());
 }
 
+// A kernel group timed by HIP event pairs around each of its launches, on whichever stream they run
+// (rs_stats: the input checks, the ragged conversion, the result gathers); `bytes` its algorithmic
+// bytes (what the launches must read and write at least), both summed until collect()
+struct KGroup {
+  std::vector<hipEvent_t> ev;
+  size_t n = 0;
+  uint64_t bytes = 0;
+  void mark(hipStream_t s) {
+    if (n == ev.size()) {
+      hipEvent_t e;
+      HC(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+    HC(hipEventRecord(ev[n++], s));
+  }
+  template <class F>
+  void run(hipStream_t s, uint64_t b, F &&f) {
+    mark(s);
+    f();
+    mark(s);
+    bytes += b;
+  }
+  // ms of the pairs so far (waits for them), launches (0 or 1: one group run per call), bytes; reset
+  void collect(double &ms, uint64_t &by, uint64_t &launches) {
+    double t = 0;
+    for (size_t i = 0; i + 1 < n; i += 2) {
+      float m = 0;
+      HC(hipEventSynchronize(ev[i + 1]));
+      HC(hipEventElapsedTime(&m, ev[i], ev[i + 1]));
+      t += m;
+    }
+    ms += t;
+    by += bytes;
+    launches += n ? 1 : 0;
+    n = 0;
+    bytes = 0;
+  }
+  void destroy() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    n = 0;
+  }
+};
+
 }  // namespace rs
 #include "comm.hpp"
 namespace rs {
@@ -285,6 +329,9 @@ struct rs_engine {
   hipEvent_t evgt[3] = {};
   hipEvent_t ev_sm[3] = {};   // its start / k_eliminate done / its work done (the tail's second group too)
   hipEvent_t ev_chunk[2] = {};
+  // rs_stats groups timed launch by launch: [0] input checks (copy stream), [1] ragged conversion and
+  // the linear rows' frames, [2] result gathers (snapshots, late rows, the compact CSR)
+  KGroup kg[3];
   int snap_rc = 0;
   // the final row views, for the compact CSR built on demand (rs_engine_fetch / the .r1cs writer)
   // when the streamed run skipped it
@@ -450,12 +497,25 @@ static void load_enqueue(rs_engine *E, const rs_input *in, bool staged) {
   int *vf = E->A.get<int>("vflag", 10);
   HC(hipMemsetAsync(vf, 0, 40, E->stc));
   hipStream_t s = E->stc;
+  KGroup &kg = E->kg[0];
+  kg.n = 0;
+  kg.bytes = 0;
+  // algorithmic bytes: the row pointers; + the keys (k_check_keys); + keys and values (k_sort_validate)
   auto check = [&](const rs_engine::Blk &B, int g) {
-    launch(s, k_check_ptr, B.n + 1, (const uint64_t *)B.ptr, B.n, B.nnz, vf + 2 * g);
+    kg.run(s, 8 * (B.n + 1), [&] { launch(s, k_check_ptr, B.n + 1, (const uint64_t *)B.ptr, B.n, B.nnz, vf + 2 * g); });
+  };
+  auto check_keys = [&](const rs_engine::Blk &B, int pw, int ew, int *uw) {
+    if (B.n)
+      kg.run(s, 8 * (B.n + 1) + 4 * B.nnz, [&] {
+        launch(s, k_check_keys, B.n, (const uint64_t *)B.ptr, (const uint32_t *)B.key, B.n, E->S, (const int *)(vf + pw), vf + ew, uw);
+      });
   };
   // k_sort_validate of block B: skipped when the row pointers' word `pw` is set, verdict into `ew`
   auto sort_validate = [&](const rs_engine::Blk &B, int pw, int ew) {
-    if (B.n) launch(s, k_sort_validate, B.n, E->F, (const uint64_t *)B.ptr, B.key, B.val, B.n, E->S, (const int *)(vf + pw), vf + ew);
+    if (B.n)
+      kg.run(s, 8 * (B.n + 1) + 36 * B.nnz, [&] {
+        launch(s, k_sort_validate, B.n, E->F, (const uint64_t *)B.ptr, B.key, B.val, B.n, E->S, (const int *)(vf + pw), vf + ew);
+      });
   };
   auto verdict = [&](int g, int words) {
     HC(hipMemcpyAsync(E->h_vflag + 2 * g, vf + 2 * g, 4 * words, hipMemcpyDeviceToHost, s));
@@ -469,8 +529,7 @@ static void load_enqueue(rs_engine *E, const rs_input *in, bool staged) {
   check(E->eq, 0);
   sort_validate(E->ce, 0, 1);
   if (staged) {
-    if (E->eq.n) launch(s, k_check_keys, E->eq.n, (const uint64_t *)E->eq.ptr, (const uint32_t *)E->eq.key, E->eq.n, E->S,
-                        (const int *)vf, vf + 1, (int *)nullptr);
+    check_keys(E->eq, 0, 1, nullptr);
   } else {
     sort_validate(E->eq, 0, 1);
   }
@@ -479,8 +538,7 @@ static void load_enqueue(rs_engine *E, const rs_input *in, bool staged) {
   upload_block(E, in->linear, E->lin, "in.lin", staged ? kUpKeys : kUpAll);
   check(E->lin, 1);
   if (staged) {
-    if (E->lin.n) launch(s, k_check_keys, E->lin.n, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, E->lin.n, E->S,
-                         (const int *)(vf + 2), vf + 3, vf + 8);
+    check_keys(E->lin, 2, 3, vf + 8);
     HC(hipMemcpyAsync(E->h_vflag + 8, vf + 8, 4, hipMemcpyDeviceToHost, s));
     verdict(1, 2);
     upload_block(E, in->linear, E->lin, "in.lin", kUpVals);
@@ -2416,11 +2474,13 @@ static void ensure_csr(rs_engine *E) {
     const uint64_t *ptr = A.get<uint64_t>(std::string(nm[q]) + ".ptr", n_out + 1);
     uint32_t *col = A.get<uint32_t>(std::string(nm[q]) + ".col", tot);
     uint64_t *val = A.get<uint64_t>(std::string(nm[q]) + ".val", 4 * tot);
-    if (n_keep) launch(st, k_gather_rows, n_keep, E->F, E->fin_parts[q], E->fin_keep_ids, n_keep, ptr, col, val);
-    for (int x = 0; x < 2; ++x) {
-      const uint64_t o = n_keep + (x ? E->fin_xn[0] : 0);
-      if (E->fin_xn[x]) launch(st, k_gather_rows, E->fin_xn[x], E->F, E->fin_xq[x][q], E->fin_x_ids[x], E->fin_xn[x], ptr + o, col, val);
-    }
+    E->kg[2].run(st, 24 * n_out + 72 * tot, [&] {  // kg[2]: 72 B an entry, the row's id / extent / ptr
+      if (n_keep) launch(st, k_gather_rows, n_keep, E->F, E->fin_parts[q], E->fin_keep_ids, n_keep, ptr, col, val);
+      for (int x = 0; x < 2; ++x) {
+        const uint64_t o = n_keep + (x ? E->fin_xn[0] : 0);
+        if (E->fin_xn[x]) launch(st, k_gather_rows, E->fin_xn[x], E->F, E->fin_xq[x][q], E->fin_x_ids[x], E->fin_xn[x], ptr + o, col, val);
+      }
+    });
   }
   E->csr_ready = true;
 }
@@ -2430,6 +2490,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   hipStream_t st = E->st;
   E->stats = rs_stats{};
   E->stats.world = E->comm ? (uint64_t)E->comm->world : 1;
+  for (int g = 1; g < 3; ++g) {  // (kg[0]: the load's checks, recorded before the run)
+    E->kg[g].n = 0;
+    E->kg[g].bytes = 0;
+  }
   E->A.defer = false;  // an exchange a failed run left mid-way
   double T0 = now_ms();
   bool apply_linear = !fl->flag_s;
@@ -2631,8 +2695,14 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   ce.len = A.get<uint32_t>("ce.len", ce.n);
   ce.key = A.get<uint32_t>("ce.key", E->ce.nnz);
   ce.val = A.get<Fe>("ce.val", E->ce.nnz);
-  if (ce.n) launch(st, k_make_ragged, ce.n, E->F, (const uint64_t *)E->ce.ptr, (const uint32_t *)E->ce.key, (const Fe *)E->ce.val,
-                   ce.n, (uint64_t)0, ce.off, ce.len, ce.key, ce.val);
+  // kg[1]'s algorithmic bytes: k_make_ragged reads the CSR and writes the ragged copy, 72 B an entry
+  // and 20 a row; the linear rows' frames read what they rewrite (+ eq_rep / ce_has per entry)
+  KGroup &kg1 = E->kg[1];
+  if (ce.n)
+    kg1.run(st, 72 * E->ce.nnz + 20 * ce.n + 8, [&] {
+      launch(st, k_make_ragged, ce.n, E->F, (const uint64_t *)E->ce.ptr, (const uint32_t *)E->ce.key, (const Fe *)E->ce.val, ce.n,
+             (uint64_t)0, ce.off, ce.len, ce.key, ce.val);
+    });
   lin.n = E->lin.n;
   lin.off = A.get<uint64_t>("lin.off", lin.n);
   lin.len = A.get<uint32_t>("lin.len", lin.n);
@@ -2692,8 +2762,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     lin_fixed = A.get<uint8_t>("lin.fixed", lin.n);
     HC(hipMemsetAsync(unc, 0, 4, st));
     HC(hipMemsetAsync(lin_fixed, 0, lin.n, st));
-    launch(st, k_lin_keyframes, lin.n, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, lin.n, lin,
-           (const int32_t *)eq_rep, (const uint8_t *)ce_has, unc, unc_list, unc_cap);
+    kg1.run(st, 13 * E->lin.nnz + 20 * lin.n + 8, [&] {
+      launch(st, k_lin_keyframes, lin.n, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, lin.n, lin,
+             (const int32_t *)eq_rep, (const uint8_t *)ce_has, unc, unc_list, unc_cap);
+    });
     int hu = 0;
     HC(hipMemcpyAsync(&hu, unc, 4, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
@@ -2729,15 +2801,19 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   if (!keys_first) {
     load_wait(E, 2);
     if (lin.n) {
-      launch(st, k_make_ragged, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
-             lin.n, (uint64_t)1, lin.off, lin.len, lin.key, lin.val);
-      launch(st, k_linear_frames12, lin.n, E->F, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val);
+      kg1.run(st, 72 * E->lin.nnz + 20 * lin.n + 8 + 77 * E->lin.nnz + 16 * lin.n, [&] {
+        launch(st, k_make_ragged, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
+               lin.n, (uint64_t)1, lin.off, lin.len, lin.key, lin.val);
+        launch(st, k_linear_frames12, lin.n, E->F, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val);
+      });
     }
   }
   const std::function<void()> linear_values = [&]() {
     load_wait(E, 2);
-    launch(st, k_lin_valframes, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
-           lin.n, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val, (const uint8_t *)lin_fixed);
+    kg1.run(st, 77 * E->lin.nnz + 20 * lin.n + 8, [&] {
+      launch(st, k_lin_valframes, lin.n, E->F, (const uint64_t *)E->lin.ptr, (const uint32_t *)E->lin.key, (const Fe *)E->lin.val,
+             lin.n, lin, (const int32_t *)eq_rep, (const uint8_t *)ce_has, (const Fe *)ce_val, (const uint8_t *)lin_fixed);
+    });
   };
   if (g_prof_env) fprintf(stderr, "[rs-prof] linear rows: %s\n", keys_first ? "keys first" : "keys + values");
   HC(hipStreamSynchronize(st));
@@ -2752,8 +2828,11 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     R.len = A.get<uint32_t>(std::string(nm) + ".len", R.n);
     R.key = A.get<uint32_t>(std::string(nm) + ".key", B.nnz);
     R.val = A.get<Fe>(std::string(nm) + ".val", B.nnz);
-    if (R.n) launch(st, k_make_ragged, R.n, E->F, (const uint64_t *)B.ptr, (const uint32_t *)B.key, (const Fe *)B.val, R.n,
-                    (uint64_t)0, R.off, R.len, R.key, R.val);
+    if (R.n)
+      kg1.run(st, 72 * B.nnz + 20 * R.n + 8, [&] {
+        launch(st, k_make_ragged, R.n, E->F, (const uint64_t *)B.ptr, (const uint32_t *)B.key, (const Fe *)B.val, R.n, (uint64_t)0,
+               R.off, R.len, R.key, R.val);
+      });
   };
   // the non-linear blocks are staged where the frames first need them: their upload (group 2)
   // overlaps the clustering and elimination
@@ -2875,11 +2954,18 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       const std::string xn = std::string("out.") + "abc"[q];
       uint32_t *col = A.get<uint32_t>(xn + ".xcol", cap);
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
-      if (ev[q]) launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
-                        (const uint64_t *)nullptr);
+      // kg[2]'s algorithmic bytes: 72 an entry (key + value read, canonical key + value written) and
+      // what a row's selection reads (its flag; its extent when selected)
+      if (ev[q])
+        E->kg[2].run(E->stc, 13 * n_nl + 72 * ev[q], [&] {
+          launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
+                 (const uint64_t *)nullptr);
+        });
       if (q == 2 && lc_e) {
         const DRows lcv = lc.view(A);
-        launch(E->stc, k_lc_snap, lc_e, E->F, (const uint32_t *)lcv.key, (const Fe *)lcv.val, lc_e, col + et.c, val + 4 * et.c);
+        E->kg[2].run(E->stc, 72 * lc_e, [&] {
+          launch(E->stc, k_lc_snap, lc_e, E->F, (const uint32_t *)lcv.key, (const Fe *)lcv.val, lc_e, col + et.c, val + 4 * et.c);
+        });
       }
       void *hc = shard ? (void *)(sh_col(E, q) + CM->rank * E->sh_cap[q]) : pin_get(E, 3 + q, 4 * cap);
       void *hv = shard ? (void *)(sh_val(E, q) + 4 * CM->rank * E->sh_cap[q]) : pin_get(E, 6 + q, 32 * cap);
@@ -2931,8 +3017,10 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint32_t *col = A.get<uint32_t>(xn + ".xcol", 1);
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 1);
       if (!e2[q]) continue;
-      launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
-             (const uint64_t *)nl_late);
+      E->kg[2].run(E->stc, 21 * n_nl + 72 * e2[q], [&] {
+        launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
+               (const uint64_t *)nl_late);
+      });
       HC(hipEventRecord(E->ev_snapq[3 + q], E->stc));
       snap_push(E, {(uint32_t *)E->snap_host[2 * q] + b, col + b, 4 * e2[q], E->ev_snapq[3 + q]});
       snap_push(E, {(uint64_t *)E->snap_host[2 * q + 1] + 4 * b, val + 4 * b, 32 * e2[q], E->ev_snapq[3 + q]});
@@ -3186,7 +3274,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       uint32_t *col = A.get<uint32_t>(xn + ".xcol", 1);
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 1);
       if (!e3[q]) continue;
-      launch(E->stc, k_snap_gather_st, n_st, E->F, cp[q], (const U3 *)elen, (const U3 *)eoff3, b, q, n_st, col, val);
+      E->kg[2].run(E->stc, 24 * n_st + 72 * e3[q], [&] {
+        launch(E->stc, k_snap_gather_st, n_st, E->F, cp[q], (const U3 *)elen, (const U3 *)eoff3, b, q, n_st, col, val);
+      });
       HC(hipEventRecord(E->ev_snapq[3 + q], E->stc));
       snap_push(E, {(uint32_t *)E->snap_host[2 * q] + b, col + b, 4 * e3[q], E->ev_snapq[3 + q]});
       snap_push(E, {(uint64_t *)E->snap_host[2 * q + 1] + 4 * b, val + 4 * b, 32 * e3[q], E->ev_snapq[3 + q]});
@@ -3747,14 +3837,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       A.grow_keep<uint64_t>(xv, 4 * ext, 4 * base, E->stc, st);
       uint32_t *col = A.get<uint32_t>(xc, ext);
       uint64_t *val = A.get<uint64_t>(xv, 4 * ext);
-      if (own) launch(st, k_gather_late, own, E->F, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
-                      (const uint8_t *)so_dirty, (const uint64_t *)lptr, col + base, val + 4 * base);
-      if (xl_n[0])
-        launch(st, k_gather_late, xl_n[0], E->F, xq[0], (const uint32_t *)x_ids[0], xl_n[0], (const uint32_t *)nullptr,
-               (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + xl_at[0]), col + base, val + 4 * base);
-      if (xl_n[1])
-        launch(st, k_lc_gather_late, xl_n[1], E->F, xq[1], (const uint32_t *)x_ids[1], xl_n[1], E->lc_snap_n,
-               (const uint64_t *)(lptr + xl_at[1]), col + base, val + 4 * base);
+      E->kg[2].run(st, 30 * (own + xl_n[0] + xl_n[1]) + 72 * L, [&] {
+        if (own) launch(st, k_gather_late, own, E->F, *parts[q], own_ids, own, (const uint32_t *)st_ids, (const uint8_t *)so_early,
+                        (const uint8_t *)so_dirty, (const uint64_t *)lptr, col + base, val + 4 * base);
+        if (xl_n[0])
+          launch(st, k_gather_late, xl_n[0], E->F, xq[0], (const uint32_t *)x_ids[0], xl_n[0], (const uint32_t *)nullptr,
+                 (const uint8_t *)nullptr, (const uint8_t *)nullptr, (const uint64_t *)(lptr + xl_at[0]), col + base, val + 4 * base);
+        if (xl_n[1])
+          launch(st, k_lc_gather_late, xl_n[1], E->F, xq[1], (const uint32_t *)x_ids[1], xl_n[1], E->lc_snap_n,
+                 (const uint64_t *)(lptr + xl_at[1]), col + base, val + 4 * base);
+      });
     }
     if (shard) {  // a share past its capacity: the region regrows and every rank copies its whole layout
       uint64_t over = 0;
@@ -3804,6 +3896,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     fprintf(stderr, "\n");
   }
   E->stats.h2d_wait_ms = E->h2d_wait_ms;
+  E->kg[0].collect(E->stats.check_ms, E->stats.check_bytes, E->stats.check_launches);
+  E->kg[1].collect(E->stats.ragged_ms, E->stats.ragged_bytes, E->stats.ragged_launches);
+  E->kg[2].collect(E->stats.gather_ms, E->stats.gather_bytes, E->stats.gather_launches);
   {  // B_alg: the in-kernel counters + input / output entries and rows + the label map
     const uint64_t z_in = E->ce.nnz + E->eq.nnz + E->lin.nnz + E->na.nnz + E->nb.nnz + E->nc.nnz;
     const uint64_t r_in = E->ce.n + E->eq.n + E->lin.n + E->na.n;
@@ -3926,6 +4021,7 @@ void rs_engine_destroy(rs_engine *E) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto &ev : E->ev_grp)
     if (ev) (void)hipEventDestroy(ev);
+  for (auto &g : E->kg) g.destroy();
   if (E->stc) (void)hipStreamDestroy(E->stc);
   if (E->stx) (void)hipStreamDestroy(E->stx);
   if (E->str) (void)hipStreamDestroy(E->str);

@@ -239,6 +239,15 @@ typedef struct rs_stats {
   uint64_t giant_bytes;
   uint64_t giant_launches;
   uint64_t giant_merges;        /* merges work = c2*work - c*R the giant path's table loop performed (configs[1]: 21.6 M) */
+  double check_ms;             /* the input's device checks (k_check_ptr, k_check_keys, k_sort_validate; copy stream) */
+  uint64_t check_bytes;        /* row pointers, keys (+ values: k_sort_validate) read */
+  uint64_t check_launches;
+  double ragged_ms;            /* CSR -> ragged rows (k_make_ragged) and the linear rows' eq / constant frames */
+  uint64_t ragged_bytes;       /* 72 B an entry converted, 77 B an entry framed, + per-row extents */
+  uint64_t ragged_launches;
+  double gather_ms;            /* the result's gathers: snapshots, late rows, the compact CSR */
+  uint64_t gather_bytes;       /* 72 B an entry gathered (read + canonical write) + per-row selection */
+  uint64_t gather_launches;
 } rs_stats;
 
 typedef struct rs_engine rs_engine;

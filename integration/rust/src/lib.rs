@@ -208,6 +208,15 @@ pub struct rs_stats {
     pub giant_bytes: u64,
     pub giant_launches: u64,
     pub giant_merges: u64,
+    pub check_ms: f64,
+    pub check_bytes: u64,
+    pub check_launches: u64,
+    pub ragged_ms: f64,
+    pub ragged_bytes: u64,
+    pub ragged_launches: u64,
+    pub gather_ms: f64,
+    pub gather_bytes: u64,
+    pub gather_launches: u64,
 }
 
 #[repr(C)]

@@ -33,6 +33,12 @@ GROUPS = {
                                                           "k_cl_replay_lane("),
     "k_gi_* (giant clusters' component loops)": ("k_gi_loop(", "k_gi_state(", "k_gi_union(", "k_gi_rowkey(",
                                                 "k_gi_segment(", "k_gi_gather(", "k_gi_scatter("),
+    "input checks (k_check_ptr, k_check_keys, k_sort_validate)": ("k_sort_validate(", "k_check_ptr(", "k_check_keys("),
+    "ragged conversion + linear frames (k_make_ragged, k_lin_*frames*)": ("k_make_ragged(", "k_lin_valframes(",
+                                                                          "k_lin_keyframes(", "k_linear_frames12("),
+    "result gathers (k_snap_gather*, k_lc_*, k_gather_late, k_gather_rows)": ("k_snap_gather(", "k_snap_gather_st(",
+                                                                              "k_lc_snap(", "k_gather_late(",
+                                                                              "k_lc_gather_late(", "k_gather_rows("),
 }
 
 
