@@ -1702,6 +1702,11 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
 
     a.prof = (getenv("RS_DEBUG") || getenv("RS_PROF")) && n_big ? E->A.get<unsigned long long>("el.prof", kProfWords * n_big) : nullptr;
     if (a.prof) HC(hipMemsetAsync(a.prof, 0, 8 * kProfWords * n_big, E->st));
+    a.fclk = nullptr;
+#ifdef RS_FINCLK
+    a.fclk = E->A.get<unsigned long long>("el.fclk", 32);
+    HC(hipMemsetAsync(a.fclk, 0, 8 * 32, E->st));
+#endif
     a.bytes_main = a.bytes + 1;
     a.bytes_fin = a.bytes + 2;
     HC(hipMemsetAsync(a.bytes, 0, 64, E->st));
@@ -2114,6 +2119,19 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         }
         fprintf(stderr, "\n");
       }
+#ifdef RS_FINCLK
+      if (a.fclk) {
+        unsigned long long c[32];
+        HC(hipMemcpy(c, a.fclk, sizeof c, hipMemcpyDeviceToHost));
+        for (int t = 0; t < 2; ++t) {
+          const unsigned long long *d = c + 16 * t;
+          fprintf(stderr, "[rs-prof] tail finish clocks (%s, ms summed over waves): dag %.1f release %.1f | groups %.1f over %llu "
+                  "substitutions (%llu sent on) | whole wave %.1f over %llu (rhs entries %llu, serial %llu) | levels %llu\n",
+                  t ? "workgroup teams" : "wave teams", d[0] / 1e5, d[1] / 1e5, d[2] / 1e5, d[3], d[9], d[4] / 1e5, d[5], d[7],
+                  d[6], d[10]);
+        }
+      }
+#endif
       if (n_tail) {  // the tail's k_big_finish: per-cluster compose time, Kahn levels
         double tn = 0, tc = 0;
         std::map<int, uint64_t> lh;

@@ -539,6 +539,7 @@ struct ElimArgs {
   unsigned long long *bytes;  // algorithmic bytes (SURVEY 8(d) B_alg terms of this kernel)
   unsigned long long *bytes_main, *bytes_fin;  // the same, for k_big_main and k_big_finish
   unsigned long long *prof;   // debug: 16 words per big cluster (see run_linear_simplification), or null
+  unsigned long long *fclk;   // RS_FINCLK builds: the tail finish's section clocks (wall_clock64 ticks), or null
   uint64_t *big_touch_off;    // per big cluster: touched-signal list in the pool (k_big_prep)
   uint32_t *big_touch_n;
   uint32_t *big_alive;        // per big cluster: #rows left for the ordered loop
@@ -2049,6 +2050,10 @@ __device__ inline bool d_compose_serial(const ElimArgs &A, Alloc &al, uint64_t s
 
 constexpr uint32_t kComposeCap = 256;  // entries one wave composes in LDS
 constexpr uint32_t kFinWaveBelow = 512;  // tail clusters under this many rows finish on one wave (k_big_finish)
+#ifndef RS_FIN_G
+#define RS_FIN_G 8
+#endif
+constexpr uint32_t kFinG = RS_FIN_G, kFinPer = 64 / kFinG;  // k_big_finish: lanes per composition group, groups per wave
 
 // Composition of slot `sl` by one wave as a k-way merge of sorted runs (every dependency already
 // final; the same result as d_compose_wave): run 0 = the slot's own (non-deleted) entries, run 1 + j =
@@ -2325,6 +2330,125 @@ __device__ inline int d_compose_wave(const ElimArgs &A, Alloc &al, uint64_t sl, 
   return 0;
 }
 
+// Up to 64 / G compositions at once by one wave, G lanes each -- the same result as d_compose_wave.
+// Most substitutions of the tail's clusters are short (the metric circuit's: 2.6 right-hand-side
+// entries composing to 3.7), so one composition by a whole wave is a chain of dependent loads with
+// the wave idle; G-lane groups overlap 64 / G of those chains.  Group g = lane / G composes slot `sl`
+// (group-uniform; ~0: none) in its share of the wave's buffers (4G entries of S / V, G of dex / dof /
+// dmu).  Returns the ballot of the group leaders (lane % G == 0) whose composition does not fit (right-
+// hand side over G entries, or over 4G composed): the caller composes those with the whole wave.
+// oom: the pool is exhausted (group-uniform).
+template <uint32_t G>
+__device__ inline uint64_t d_compose_groups(const ElimArgs &A, Alloc &al, uint64_t sl, uint64_t *S, Fe *V, uint32_t *dex,
+                                            uint64_t *dof, Fe *dmu, unsigned long long &by, bool &oom) {
+  static_assert(G >= 2 && G <= 32 && (G & (G - 1)) == 0, "group size");
+  constexpr uint32_t CAP = 4 * G;
+  const FieldP &F = A.F;
+  const uint32_t lane = threadIdx.x & 63, g = lane / G, li = lane % G, g0 = g * G;
+  uint64_t *gS = S + g * CAP;
+  Fe *gV = V + g * CAP;
+  uint32_t *gdex = dex + g0;
+  uint64_t *gdof = dof + g0;
+  Fe *gdmu = dmu + g0;
+  const uint64_t gmask = ((1ull << G) - 1ull) << g0;
+  const uint64_t ltg = (lane ? ((1ull << lane) - 1ull) : 0ull) & gmask;
+  const bool has = sl != ~0ull;
+  uint64_t off = 0;
+  uint32_t len = 0;
+  if (has) {
+    off = A.h_off[sl];
+    len = A.h_len[sl];
+  }
+  bool fit = has && len <= G;
+  uint32_t key = 0, dl = 0;
+  Fe val = fe_zero();
+  int32_t hs = -1;
+  uint64_t doff = 0;
+  if (fit && li < len) {
+    key = A.pk[off + li];
+    val = A.pv[off + li];
+    hs = A.holder_idx[key];
+    if (hs >= 0) { dl = A.h_len[hs]; doff = A.h_off[hs]; }
+  }
+  const uint64_t dm = __ballot(hs >= 0) & gmask, om = __ballot(fit && li < len && hs < 0) & gmask;
+  uint32_t x = dl;  // inclusive prefix of the dependency lengths over the group
+#pragma unroll
+  for (uint32_t d = 1; d < G; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, G);
+    if (li >= d) x += y;
+  }
+  const uint32_t tot = __shfl(x, g0 + G - 1), n_own = (uint32_t)__popcll(om), D = (uint32_t)__popcll(dm);
+  const uint32_t E = n_own + tot;
+  fit = fit && E <= CAP;
+  if (fit && hs >= 0) {
+    const uint32_t r = (uint32_t)__popcll(dm & ltg);
+    gdex[r] = x - dl;
+    gdof[r] = doff;
+    gdmu[r] = val;
+  }
+  if (fit && li < len && hs < 0) {
+    const uint32_t q = (uint32_t)__popcll(om & ltg);
+    gS[q] = ((uint64_t)key << 32) | q;
+    gV[q] = val;
+  }
+  const uint32_t Ef = fit ? E : 0u;
+  for (uint32_t q = Ef + li; q < CAP; q += G) gS[q] = ~0ull;  // (the gather below writes [n_own, E))
+  wave_sync();
+  for (uint32_t e = li; e < (fit ? tot : 0u); e += G) {  // c_t * R(t), one product per entry
+    uint32_t lo = 0, hi = D;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (gdex[mid] <= e) lo = mid; else hi = mid;
+    }
+    const uint64_t src = gdof[lo] + (e - gdex[lo]);
+    const uint32_t q = n_own + e;
+    gS[q] = ((uint64_t)A.pk[src] << 32) | q;
+    gV[q] = fmul(F, gdmu[lo], A.pv[src]);
+  }
+  uint32_t np2 = 1;  // wave-uniform: the largest group's power of two
+  while (np2 < Ef) np2 <<= 1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) np2 = max(np2, (uint32_t)__shfl_xor(np2, d));
+  wave_sync();
+  for (uint32_t k = 2; k <= np2; k <<= 1) {  // bitonic sort of (key, position), every group at once
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = li; t < np2 / 2; t += G) {
+        const uint32_t i = (t / j) * 2 * j + (t % j), pr = i + j;
+        const uint64_t a = gS[i], c = gS[pr];
+        if ((a > c) == ((i & k) == 0)) { gS[i] = c; gS[pr] = a; }
+      }
+      wave_sync();
+    }
+  }
+  uint64_t o = 0;
+  if (fit && li == 0) o = pool_alloc(A, al, Ef ? Ef : 1);
+  o = __shfl(o, g0);
+  oom = fit && o == RS_NONE;
+  const bool go = fit && !oom;
+  uint32_t run = 0;
+  for (uint32_t cb = 0; cb < (go ? Ef : 0u); cb += G) {  // one output entry per distinct key, values summed
+    const uint32_t p = cb + li;
+    const uint32_t k0 = p < Ef ? (uint32_t)(gS[p] >> 32) : 0u;
+    const bool head = p < Ef && (p == 0 || (uint32_t)(gS[p - 1] >> 32) != k0);
+    const uint64_t hm = __ballot(head) & gmask;
+    if (head) {
+      Fe v = gV[(uint32_t)gS[p]];
+      for (uint32_t q = p + 1; q < Ef && (uint32_t)(gS[q] >> 32) == k0; ++q) v = fadd(F, v, gV[(uint32_t)gS[q]]);
+      const uint64_t w = o + run + (uint32_t)__popcll(hm & ltg);
+      A.pk[w] = k0;
+      A.pv[w] = v;
+    }
+    run += (uint32_t)__popcll(hm);
+  }
+  if (go && li == 0) {
+    A.h_off[sl] = o;
+    A.h_len[sl] = run;
+    by += 36ull * (len + tot + run);
+  }
+  wave_sync();
+  return __ballot(has && !fit && li == 0);
+}
+
 // the per-wave composition buffers of k_big_finish / k_compose_level, seen as d_compose_merge scratch
 __device__ __forceinline__ MergeScratch merge_scratch_small(uint64_t *S, Fe *V, uint32_t *dex, uint64_t *dof, Fe *dmu) {
   MergeScratch M;
@@ -2585,7 +2709,13 @@ __device__ inline void d_finish_cluster(const ElimArgs &A, Alloc &al, uint64_t c
       }
       uint32_t nf = T.nf, done = nf;
       uint32_t *cur = fr0, *nxt = fr1;
+#ifdef RS_FINCLK
+      unsigned long long fc[10] = {wall_clock64() - t_3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
       while (nf && T.ok) {
+#ifdef RS_FINCLK
+        unsigned long long tl0 = wall_clock64();
+#endif
         team_sync<NT>();
         if (tid == 0) T.nf = 0;
         team_sync<NT>();
@@ -2598,18 +2728,49 @@ __device__ inline void d_finish_cluster(const ElimArgs &A, Alloc &al, uint64_t c
         }
         team_sync<NT>();
         nf = T.nf;
+#ifdef RS_FINCLK
+        fc[1] += wall_clock64() - tl0;
+#endif
         {  // one wave per substitution of the frontier
           const uint32_t wv_ = tid >> 6, nw = nt >> 6;
           const uint32_t bw = wave0 + wv_;  // this wave's buffers
           uint64_t *bS = bufs.S + bw * kComposeCap, *bdof = bufs.dof + bw * 64;
           Fe *bV = bufs.V + bw * kComposeCap, *bdmu = bufs.dmu + bw * 64;
           uint32_t *bdex = bufs.dex + bw * 64;
-          for (uint32_t f = wv_; f < nf; f += nw) {
-            const uint64_t sl = b + nxt[f];
-            const int rc = d_compose_wave_any(A, al, sl, bS, bV, bdex, bdof, bdmu, by);
-            if (rc == 2) { if ((tid & 63) == 0) T.ok = 0; continue; }
-            if (rc == 1 && (tid & 63) == 0 && !d_compose_serial(A, al, sl, by)) T.ok = 0;
-            wave_sync();
+          // kFinG-lane groups take kFinPer substitutions at once; the ones too long for a group
+          // follow one by one on the whole wave
+          for (uint32_t f0 = wv_ * kFinPer; f0 < nf; f0 += nw * kFinPer) {
+            const uint32_t f = f0 + (tid & 63) / kFinG;
+            const uint64_t sl = f < nf ? b + nxt[f] : ~0ull;
+            bool oom = false;
+#ifdef RS_FINCLK
+            const unsigned long long tc0 = wall_clock64();
+#endif
+            uint64_t fbk = d_compose_groups<kFinG>(A, al, sl, bS, bV, bdex, bdof, bdmu, by, oom);
+#ifdef RS_FINCLK
+            fc[2] += wall_clock64() - tc0;
+            fc[3] += min(nf - f0, kFinPer);
+            fc[9] += __popcll(fbk);
+#endif
+            if (__ballot(oom) && (tid & 63) == 0) T.ok = 0;
+            while (fbk) {
+              const uint32_t l = (uint32_t)__ffsll((unsigned long long)fbk) - 1;
+              fbk &= fbk - 1;
+              const uint64_t sl2 = __shfl(sl, l);
+#ifdef RS_FINCLK
+              const unsigned long long tc1 = wall_clock64();
+              fc[7] += A.h_len[sl2];
+#endif
+              const int rc = d_compose_wave_any(A, al, sl2, bS, bV, bdex, bdof, bdmu, by);
+#ifdef RS_FINCLK
+              fc[4] += wall_clock64() - tc1;
+              fc[5]++;
+              if (rc == 1) fc[6]++;
+#endif
+              if (rc == 2) { if ((tid & 63) == 0) T.ok = 0; continue; }
+              if (rc == 1 && (tid & 63) == 0 && !d_compose_serial(A, al, sl2, by)) T.ok = 0;
+              wave_sync();
+            }
           }
         }
         done += nf;
@@ -2618,6 +2779,11 @@ __device__ inline void d_finish_cluster(const ElimArgs &A, Alloc &al, uint64_t c
         team_sync<NT>();  // T.ok is read by every lane in the loop condition
       }
       team_sync<NT>();
+#ifdef RS_FINCLK
+      if (A.fclk && (tid & 63) == 0)
+        for (int j = 0; j < 10; ++j) atomicAdd(&A.fclk[(NT == 64 ? 0 : 16) + j], fc[j]);
+      if (A.fclk && tid == 0) atomicAdd(&A.fclk[NT == 64 ? 10 : 26], (unsigned long long)levels);
+#endif
       if (T.ok && done != m) { if (tid == 0) { T.ok = 0; atomicOr(A.err, 32); } }
     }
   }
