@@ -2880,24 +2880,42 @@ __global__ __launch_bounds__(64 * NW) void k_compose_level(ElimArgs A, const uin
     *zero_cnt = 0;
     *zero_big = 0;
   }
-  for (uint64_t f = (uint64_t)blockIdx.x * NW + wv_; f < n; f += total) {
-    const uint64_t item = cur[f];
+  // each wave takes kFinPer frontier substitutions at once, one per kFinG-lane group (d_compose_groups);
+  // the ones too long for a group follow on the whole wave, and the ones too long for its buffers go to
+  // k_compose_big, which releases their dependents itself
+  const uint32_t li = lane % kFinG;
+  for (uint64_t f0 = ((uint64_t)blockIdx.x * NW + wv_) * kFinPer; f0 < n; f0 += total * kFinPer) {
+    const uint64_t f = f0 + lane / kFinG;
+    const bool valid = f < n;
+    const uint64_t item = valid ? cur[f] : 0ull;
     const uint32_t ci = (uint32_t)(item >> 32), q = (uint32_t)item;
-    const uint32_t c = ids[ci];
-    const uint64_t b = A.cl_off[c];
-    const uint32_t m = A.n_sub[c];
+    const uint32_t c = valid ? ids[ci] : 0u;
+    const uint64_t b = valid ? A.cl_off[c] : 0ull;
+    const uint32_t m = valid ? A.n_sub[c] : 0u;
+    uint64_t bigm = 0;  // groups whose substitution went to k_compose_big
     if (level > 0) {
-      const int rc = d_compose_wave_any(A, al, b + q, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
-      if (rc == 2 && lane == 0) atomicOr(A.err, 8);
-      if (rc == 1) {  // too long for this wave's LDS: k_compose_big composes it and releases its dependents
-        if (lane == 0) A.cf_big[atomicAdd(A.cf_nbig, 1ull)] = item;
-        continue;
+      bool oom = false;
+      const uint64_t sl = valid ? b + q : ~0ull;
+      uint64_t fbk = d_compose_groups<kFinG>(A, al, sl, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by, oom);
+      if (oom && li == 0) atomicOr(A.err, 8);
+      while (fbk) {
+        const uint32_t l = (uint32_t)__ffsll((unsigned long long)fbk) - 1;
+        fbk &= fbk - 1;
+        const uint64_t sl2 = __shfl(sl, l);
+        const int rc = d_compose_wave_any(A, al, sl2, cw_S[wv_], cw_V[wv_], cw_dex[wv_], cw_dof[wv_], cw_dmu[wv_], by);
+        if (rc == 2 && lane == 0) atomicOr(A.err, 8);
+        if (rc == 1) {  // too long for this wave's LDS
+          const uint64_t it2 = __shfl(item, l);
+          if (lane == 0) A.cf_big[atomicAdd(A.cf_nbig, 1ull)] = it2;
+          bigm |= 1ull << (l / kFinG);
+        }
+        wave_sync();
       }
-      wave_sync();
     }
+    if (!valid || ((bigm >> (lane / kFinG)) & 1)) continue;
     uint32_t *deg = A.pk + A.cf_deg[ci], *dcnt = deg + m;
     const uint32_t *dl = A.pk + A.cf_dl[ci];
-    for (uint32_t t = dcnt[q] + lane; t < dcnt[q + 1]; t += 64) {
+    for (uint32_t t = dcnt[q] + li; t < dcnt[q + 1]; t += kFinG) {
       const uint32_t d = dl[t];
       if (atomicSub(&deg[d], 1u) == 1u) {
         nxt[atomicAdd(n_nxt, 1ull)] = ((uint64_t)ci << 32) | d;
@@ -2995,12 +3013,21 @@ __global__ __launch_bounds__(64 * NW) void k_compose_rest(ElimArgs A, const uint
     uint32_t nf = s_nf;
     uint32_t *cu = fr0, *nx = fr1;
     while (nf) {
-      for (uint32_t f = wv; f < nf; f += NW) {
-        const uint64_t sl = b + cu[f];
-        const int rc = d_compose_wave_any(A, al, sl, cw_S[wv], cw_V[wv], cw_dex[wv], cw_dof[wv], cw_dmu[wv], by);
-        if (rc == 2 && lane == 0) atomicOr(A.err, 8);
-        if (rc == 1 && lane == 0 && !d_compose_serial(A, al, sl, by)) atomicOr(A.err, 8);
-        wave_sync();
+      for (uint32_t f0 = wv * kFinPer; f0 < nf; f0 += NW * kFinPer) {  // kFinPer at once (d_compose_groups)
+        const uint32_t f = f0 + lane / kFinG;
+        const uint64_t sl = f < nf ? b + cu[f] : ~0ull;
+        bool oom = false;
+        uint64_t fbk = d_compose_groups<kFinG>(A, al, sl, cw_S[wv], cw_V[wv], cw_dex[wv], cw_dof[wv], cw_dmu[wv], by, oom);
+        if (oom && lane % kFinG == 0) atomicOr(A.err, 8);
+        while (fbk) {
+          const uint32_t l = (uint32_t)__ffsll((unsigned long long)fbk) - 1;
+          fbk &= fbk - 1;
+          const uint64_t sl2 = __shfl(sl, l);
+          const int rc = d_compose_wave_any(A, al, sl2, cw_S[wv], cw_V[wv], cw_dex[wv], cw_dof[wv], cw_dmu[wv], by);
+          if (rc == 2 && lane == 0) atomicOr(A.err, 8);
+          if (rc == 1 && lane == 0 && !d_compose_serial(A, al, sl2, by)) atomicOr(A.err, 8);
+          wave_sync();
+        }
       }
       __syncthreads();
       if (tid == 0) s_nf = 0;
