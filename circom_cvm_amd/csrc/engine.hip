@@ -3981,7 +3981,14 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->stx, hipStreamNonBlocking));
     HC(hipStreamCreateWithFlags(&E->str, hipStreamNonBlocking));
-    HC(hipStreamCreateWithFlags(&E->ste, hipStreamNonBlocking));
+    {  // the small clusters and the tail's second group: least priority, so the tail's first group (the
+       // first frames pass's critical path) finds CUs before their wide finish does
+      int lo = 0, hi = 0;
+      if (getenv("RS_STE_DEFAULT") || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+          hipStreamCreateWithPriority(&E->ste, hipStreamNonBlocking, lo) != hipSuccess)
+        HC(hipStreamCreateWithFlags(&E->ste, hipStreamNonBlocking));
+      if (g_prof_env) fprintf(stderr, "[rs-prof] stream priorities: least %d greatest %d\n", lo, hi);
+    }
     HC(hipStreamCreateWithFlags(&E->stg, hipStreamNonBlocking));
     for (auto &ev : E->evg) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     for (auto &g : E->evt)
