@@ -312,6 +312,8 @@ struct rs_engine {
     hipEvent_t ready;  // its gather is done
   };
   hipEvent_t ev_snapq[6] = {};  // the parts' gathers of the first / second snapshot
+  hipEvent_t ev_snaph[3] = {};  // the parts' gathers of the first pass's second half
+  hipEvent_t ev_fh[2] = {};     // the first pass in halves: first half done / second half starts
   std::mutex snap_m;
   std::condition_variable snap_cv;
   std::deque<SnapJob> snap_q;  // jobs the D2H thread has not started; closed: no more will come
@@ -2926,14 +2928,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   // stream while the run goes on.  late: rows a second frames pass still has to do (nullptr: none).
   uint8_t *so_early = nullptr;
   U3 *so_eoff = nullptr;
-  auto snap_take = [&](const uint64_t *late) {
+  bool fh_split = false;  // the last nl_phase ran in two halves (ev_fh)
+  // hi_rows < n_nl: the first pass's first half only (snap_take_h2 takes the rest once it is done)
+  auto snap_take = [&](const uint64_t *late, uint64_t hi_rows) {
     if (!E->stream_out || !n_nl) return;
     so_early = A.get<uint8_t>("so.early", n_nl);
     so_eoff = A.get<U3>("so.eoff", n_nl);
     U3 *elen = A.get<U3>("so.elen", n_nl);
     Comm *CM = E->comm.get();
     const bool shard = CM && CM->world > 1;
-    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, shard ? E->nl_lo : (uint64_t)0, shard ? E->nl_hi : n_nl, so_early, elen);
+    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, shard ? E->nl_lo : (uint64_t)0, shard ? E->nl_hi : hi_rows, so_early, elen);
     const U3 et = excl_scan_u3(E, elen, so_eoff, n_nl, "so");
     // single engine: the lconst rows so far (final as they enter the heap) go behind the C part
     E->lc_snap_n = shard ? 0 : lc.n;
@@ -2968,7 +2972,9 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       E->snap_hint[q] = std::max(E->snap_hint[q], ev[q]);
       // the device early region = the head of the layout's arrays; the late rows follow it
       // room for the second snapshot's rows too (the largest early region so far, else a margin)
-      const uint64_t cap = std::max<uint64_t>(ev[q] + std::max<uint64_t>(ev[q] / 4, 1 << 16), E->snap_hint[q]);
+      // (a first half: room for the whole pass, scaled by rows)
+      const uint64_t est = hi_rows < n_nl && hi_rows ? (uint64_t)((double)ev[q] * n_nl / hi_rows) : ev[q];
+      const uint64_t cap = std::max<uint64_t>(est + std::max<uint64_t>(est / 4, 1 << 16), E->snap_hint[q]);
       const std::string xn = std::string("out.") + "abc"[q];
       uint32_t *col = A.get<uint32_t>(xn + ".xcol", cap);
       uint64_t *val = A.get<uint64_t>(xn + ".xval", 4 * cap);
@@ -2977,7 +2983,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (ev[q])
         E->kg[2].run(E->stc, 13 * n_nl + 72 * ev[q], [&] {
           launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
-                 (const uint64_t *)nullptr);
+                 (const uint64_t *)nullptr, (uint64_t)0);
         });
       if (q == 2 && lc_e) {
         const DRows lcv = lc.view(A);
@@ -3037,7 +3043,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (!e2[q]) continue;
       E->kg[2].run(E->stc, 21 * n_nl + 72 * e2[q], [&] {
         launch(E->stc, k_snap_gather, n_nl, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
-               (const uint64_t *)nl_late);
+               (const uint64_t *)nl_late, (uint64_t)0);
       });
       HC(hipEventRecord(E->ev_snapq[3 + q], E->stc));
       snap_push(E, {(uint32_t *)E->snap_host[2 * q] + b, col + b, 4 * e2[q], E->ev_snapq[3 + q]});
@@ -3049,7 +3055,57 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       fprintf(stderr, "[rs-prof] stream: second snapshot %llu / %llu / %llu entries (%.1f MB)\n", (unsigned long long)e2[0],
               (unsigned long long)e2[1], (unsigned long long)e2[2], 36e-6 * (e2[0] + e2[1] + e2[2]));
   };
-  auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1) {
+  // split < n (phase 1): the frames of rows [0, split), `between` (the first half's snapshot), then the
+  // rest; the kernel time excludes what runs between
+  // The first pass's second half (single engine): its rows [h, n_nl) that are done and stayed storage
+  // rows go behind the first half's in the regions sized at the first snapshot, when they fit (else
+  // they stay late and the capacity hint grows).
+  auto snap_take_h2 = [&](uint64_t h) {
+    if (!E->snap_on || (E->comm && E->comm->world > 1)) return;
+    HC(hipStreamWaitEvent(st, E->ev_snap, 0));  // the first half's gathers read the flags rewritten here
+    U3 *elen = A.get<U3>("so.elenh", n_nl), *eoffh = A.get<U3>("so.eoffh", n_nl);
+    launch(st, k_snap_lens_rng, n_nl, sa, sb, sc, (const uint64_t *)nl_late, h, n_nl, n_nl, elen);
+    const U3 et = excl_scan_u3(E, elen, eoffh, n_nl, "soh");
+    const uint64_t e2[3] = {et.a, et.b, et.c};
+    for (int q = 0; q < 3; ++q) E->snap_hint[q] = std::max(E->snap_hint[q], E->snap_e[q] + e2[q]);
+    for (int q = 0; q < 3; ++q)
+      if (E->snap_e[q] + e2[q] > E->snap_cap[q]) return;
+    launch(st, k_snap_mark_sel, n_nl, (const U3 *)elen, (const U3 *)eoffh, U3{E->snap_e[0], E->snap_e[1], E->snap_e[2]}, n_nl,
+           so_early, so_eoff);
+    const DRows *src[3] = {&sa, &sb, &sc};
+    const char *nm[3] = {"soh.a", "soh.b", "soh.c"};
+    DRows cp[3];
+    for (int q = 0; q < 3; ++q) {  // copies of the row views (the second pass and the rounds re-point rows)
+      cp[q] = *src[q];
+      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
+      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
+      HC(hipMemcpyAsync(cp[q].off + h, src[q]->off + h, 8 * (n_nl - h), hipMemcpyDeviceToDevice, st));
+      HC(hipMemcpyAsync(cp[q].len + h, src[q]->len + h, 4 * (n_nl - h), hipMemcpyDeviceToDevice, st));
+    }
+    HC(hipEventRecord(E->ev_snap0, st));
+    HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
+    for (int q = 0; q < 3; ++q) {
+      const uint64_t b = E->snap_e[q];
+      const std::string xn = std::string("out.") + "abc"[q];
+      uint32_t *col = A.get<uint32_t>(xn + ".xcol", 1);
+      uint64_t *val = A.get<uint64_t>(xn + ".xval", 1);
+      if (!e2[q]) continue;
+      E->kg[2].run(E->stc, 13 * (n_nl - h) + 72 * e2[q], [&] {
+        launch(E->stc, k_snap_gather, n_nl - h, E->F, cp[q], (const uint8_t *)so_early, (const U3 *)so_eoff, q, n_nl, col, val,
+               (const uint64_t *)nullptr, h);
+      });
+      HC(hipEventRecord(E->ev_snaph[q], E->stc));
+      snap_push(E, {(uint32_t *)E->snap_host[2 * q] + b, col + b, 4 * e2[q], E->ev_snaph[q]});
+      snap_push(E, {(uint64_t *)E->snap_host[2 * q + 1] + 4 * b, val + 4 * b, 32 * e2[q], E->ev_snaph[q]});
+      E->snap_e[q] = b + e2[q];
+    }
+    HC(hipEventRecord(E->ev_snap, E->stc));
+    if (g_prof_env)
+      fprintf(stderr, "[rs-prof] stream: the first pass's second half %llu / %llu / %llu entries (%.1f MB)\n", (unsigned long long)e2[0],
+              (unsigned long long)e2[1], (unsigned long long)e2[2], 36e-6 * (e2[0] + e2[1] + e2[2]));
+  };
+  auto nl_phase = [&](int phase, const uint32_t *ids, uint64_t n, hipEvent_t e0, hipEvent_t e1, uint64_t split = ~0ull,
+                      const std::function<void()> &between = {}) {
     stage_nl();
     NLArgs a{};
     a.fr = fr;
@@ -3098,7 +3154,21 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     a.xlist = w.big;
     a.n_xlist = w.n_big;
     HC(hipEventRecord(e0, st));
-    launch_capped(st, k_frames_wave<0>, n, kFwBlocks, w);
+    fh_split = split < n;
+    if (fh_split) {
+      w.n = split;
+      launch_capped(st, k_frames_wave<0>, split, kFwBlocks, w);
+      launch(st, k_nl_fill, n, a);  // the rows over a batch listed so far
+      HC(hipEventRecord(E->ev_fh[0], st));
+      between();
+      HC(hipMemsetAsync(w.n_big, 0, 4, st));
+      HC(hipEventRecord(E->ev_fh[1], st));
+      w.x0 = split;
+      w.n = n;
+      launch_capped(st, k_frames_wave<0>, n - split, kFwBlocks, w);
+    } else {
+      launch_capped(st, k_frames_wave<0>, n, kFwBlocks, w);
+    }
     launch(st, k_nl_fill, n, a);  // a grid for every row: the list may be long, idle lanes leave at once
     HC(hipEventRecord(e1, st));
     if (g_prof_env) {
@@ -3131,7 +3201,15 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   auto nl_ms = [&](hipEvent_t e0, hipEvent_t e1) {
     float ms = 0;
     HC(hipEventSynchronize(e1));
-    HC(hipEventElapsedTime(&ms, e0, e1));
+    if (fh_split) {  // the two halves, without the snapshot between them
+      float m2 = 0;
+      HC(hipEventElapsedTime(&ms, e0, E->ev_fh[0]));
+      HC(hipEventElapsedTime(&m2, E->ev_fh[1], e1));
+      ms += m2;
+      fh_split = false;
+    } else {
+      HC(hipEventElapsedTime(&ms, e0, e1));
+    }
     E->stats.apply_kernel_ms += ms;
   };
   // rows that touch none of the largest clusters go through the frames while those clusters are
@@ -3148,8 +3226,14 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
                        (const uint64_t *)ea.cl_off, ids, hmark);
     HC(hipGetLastError());
     fr.h_off = ea.h_off; fr.h_len = ea.h_len; fr.pk = ea.pk; fr.pv = ea.pv;
-    nl_phase(1, nullptr, n_nl, E->evx[8], E->evx[9]);
-    snap_take(nl_late);
+    // the first pass in two halves with a snapshot after each (single engine, streamed): the result
+    // stream starts after half the pass
+    const bool halves = E->stream_out && !(E->comm && E->comm->world > 1) && n_nl >= (getenv("RS_HALVES_MIN") ? strtoull(getenv("RS_HALVES_MIN"), nullptr, 10) : (1ull << 20)) &&
+                       !getenv("RS_NO_HALVES");
+    const uint64_t h = halves ? n_nl / 2 : n_nl;
+    nl_phase(1, nullptr, n_nl, E->evx[8], E->evx[9], h, [&] { snap_take(nl_late, h); });
+    if (!halves) snap_take(nl_late, n_nl);
+    else snap_take_h2(h);
     nl_split = true;
   };
 
@@ -3190,7 +3274,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (nl_split) nl_ms(E->evx[8], E->evx[9]);
     if (!nl_split) {
       nl_phase(0, nullptr, n_nl, E->ev0, E->ev1);
-      snap_take(nullptr);
+      snap_take(nullptr, n_nl);
       nl_ms(E->ev0, E->ev1);
     } else if (n_late) {
       nl_phase(2, nl_lids, n_late, E->ev0, E->ev1);
@@ -4015,6 +4099,8 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipEventCreateWithFlags(&E->ev_snap0, hipEventDisableTiming));
     for (auto &ev : E->ev_chunk) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     for (auto &ev : E->ev_snapq) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (auto &ev : E->ev_snaph) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (auto &ev : E->ev_fh) HC(hipEventCreate(&ev));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {

@@ -58,6 +58,7 @@ struct FrameWaveArgs {
   int cap_by_row;           // caps indexed by row (rounds) or by list position (non-linear pass)
   const uint32_t *ids;      // list position -> row (nullptr: identity)
   uint64_t n;
+  uint64_t x0;              // the list positions [x0, n) (the first pass in two halves: a snapshot after each)
   const uint64_t *late;     // non-linear phase 1: rows left for phase 2 (by row), else null
   uint32_t *big;            // out: rows too large for a batch -- positions (non-linear) or rows (rounds)
   unsigned *n_big;
@@ -775,7 +776,7 @@ __global__ __launch_bounds__(256, FW_OCC) void k_frames_wave(FrameWaveArgs A) {
 #endif
   const uint64_t nw = (uint64_t)gridDim.x * kFwWaves;
   uint32_t fx_n = 0, fx_terms = 0;  // the fix-pass queue (uniform)
-  for (uint64_t base = ((uint64_t)blockIdx.x * kFwWaves + wv) * 64; base < A.n; base += nw * 64) {
+  for (uint64_t base = A.x0 + ((uint64_t)blockIdx.x * kFwWaves + wv) * 64; base < A.n; base += nw * 64) {
     const uint64_t x = base + lane;
     bool act = x < A.n;
     uint64_t r = 0, ioff[3] = {0, 0, 0}, ooff[3] = {0, 0, 0};

@@ -45,12 +45,29 @@ __global__ void k_snap_mark2(const uint64_t *late, const U3 *elen, const U3 *eof
   }
 }
 
+// The first pass in two halves (single engine): the second half's rows [lo, hi) that are done and
+// stayed storage rows -- elen[i] their part lengths (else 0); k_snap_mark_sel makes every row with
+// lengths early at base + its offset.
+__global__ void k_snap_lens_rng(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t lo, uint64_t hi, uint64_t n, U3 *elen) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    const bool ok = i >= lo && i < hi && !(late && late[i]) && (a.len[i] | b.len[i]) != 0;
+    elen[i] = ok ? U3{a.len[i], b.len[i], c.len[i]} : U3{0, 0, 0};
+  }
+}
+__global__ void k_snap_mark_sel(const U3 *elen, const U3 *eoff2, U3 base, uint64_t n, uint8_t *early, U3 *eoff) {
+  for (uint64_t i = gtid(); i < n; i += gstride()) {
+    if ((elen[i].a | elen[i].b) == 0) continue;
+    early[i] = 1;
+    eoff[i] = U3{base.a + eoff2[i].a, base.b + eoff2[i].b, base.c + eoff2[i].c};
+  }
+}
+
 // the early rows of one part, canonical, at their early-region offsets (R: a copy of the row views
 // taken at the snapshot, so later rounds may move the rows meanwhile; only: the second snapshot's
-// rows, else every early row)
+// rows, else every early row; rows below lo are skipped -- the first pass's second half)
 __global__ void k_snap_gather(FieldP F, DRows R, const uint8_t *early, const U3 *eoff, int q, uint64_t n, uint32_t *col,
-                              uint64_t *val, const uint64_t *only) {
-  for (uint64_t r = gtid(); r < n; r += gstride()) {
+                              uint64_t *val, const uint64_t *only, uint64_t lo) {
+  for (uint64_t r = lo + gtid(); r < n; r += gstride()) {
     if (!early[r] || (only && !only[r])) continue;
     const uint64_t o = u3_sel(eoff[r], q), s = R.off[r];
     const uint32_t len = R.len[r];
