@@ -314,6 +314,7 @@ struct rs_engine {
   hipEvent_t ev_snapq[6] = {};  // the parts' gathers of the first / second snapshot
   hipEvent_t ev_snaph[3] = {};  // the parts' gathers of the first pass's second half
   hipEvent_t ev_fh[2] = {};     // the first pass in halves: first half done / second half starts
+  hipEvent_t ev_nlc = nullptr;  // the non-linear blocks' ragged conversion (copy stream) done
   std::mutex snap_m;
   std::condition_variable snap_cv;
   std::deque<SnapJob> snap_q;  // jobs the D2H thread has not started; closed: no more will come
@@ -2842,15 +2843,15 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   // ======================= obtain_and_simplify_non_linear (non_linear_utils.rs:6-31): setup
   const uint64_t n_nl = E->na.n;
   DRows ia{}, ib{}, ic{};
-  auto mk_in = [&](rs_engine::Blk &B, DRows &R, const char *nm) {
+  auto mk_in = [&](rs_engine::Blk &B, DRows &R, const char *nm, hipStream_t ms) {
     R.n = B.n;
     R.off = A.get<uint64_t>(std::string(nm) + ".off", R.n);
     R.len = A.get<uint32_t>(std::string(nm) + ".len", R.n);
     R.key = A.get<uint32_t>(std::string(nm) + ".key", B.nnz);
     R.val = A.get<Fe>(std::string(nm) + ".val", B.nnz);
     if (R.n)
-      kg1.run(st, 72 * B.nnz + 20 * R.n + 8, [&] {
-        launch(st, k_make_ragged, R.n, E->F, (const uint64_t *)B.ptr, (const uint32_t *)B.key, (const Fe *)B.val, R.n, (uint64_t)0,
+      kg1.run(ms, 72 * B.nnz + 20 * R.n + 8, [&] {
+        launch(ms, k_make_ragged, R.n, E->F, (const uint64_t *)B.ptr, (const uint32_t *)B.key, (const Fe *)B.val, R.n, (uint64_t)0,
                R.off, R.len, R.key, R.val);
       });
   };
@@ -2860,9 +2861,15 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
   auto stage_nl = [&]() {
     if (nl_staged) return;
     load_wait(E, 3);
-    mk_in(E->na, ia, "nla");
-    mk_in(E->nb, ib, "nlb");
-    mk_in(E->nc, ic, "nlc");
+    // the conversion on the copy stream (in order after the blocks' upload and checks), beside what
+    // the main stream still runs (the tail's finish): the frames wait for it there
+    static const bool on_main = getenv("RS_NLC_MAIN") != nullptr;
+    hipStream_t cs = on_main ? st : E->stc;
+    mk_in(E->na, ia, "nla", cs);
+    mk_in(E->nb, ib, "nlb", cs);
+    mk_in(E->nc, ic, "nlc", cs);
+    HC(hipEventRecord(E->ev_nlc, cs));
+    HC(hipStreamWaitEvent(st, E->ev_nlc, 0));
     nl_staged = true;
   };
   // storage rows live in one growable heap of (key, value) entries, owned by the engine
@@ -4101,6 +4108,7 @@ int rs_engine_create(int device, rs_engine **eng) {
     for (auto &ev : E->ev_snapq) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     for (auto &ev : E->ev_snaph) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     for (auto &ev : E->ev_fh) HC(hipEventCreate(&ev));
+    HC(hipEventCreateWithFlags(&E->ev_nlc, hipEventDisableTiming));
     *eng = E.release();
     return RS_OK;
   } catch (const RsError &e) {
