@@ -25,6 +25,8 @@
 
 #include <cstring>
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <unistd.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -4045,6 +4047,46 @@ extern "C" {
 
 int rs_abi_version(void) { return RS_ABI_VERSION; }
 
+namespace rs {
+// The host side of a call (synchronisations, the clustering's host replay, the result stream's thread)
+// is latency-bound; on a multi-socket host a thread placed on the far socket from the GPU ran every
+// call ~5 ms slower (the metric circuit, 42 vs 47-49 ms, process to process).  So the thread that
+// creates an engine -- and the threads it starts later, which inherit it -- is bound to the CPUs of
+// the GPU's own NUMA node (sysfs local_cpulist of its PCI function) that its affinity allows.
+// RS_NO_CPU_BIND=1 leaves the affinity alone; returns the CPUs bound to (0: unchanged).
+static int bind_near_gpu(int device) {
+  if (getenv("RS_NO_CPU_BIND")) return 0;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return 0;
+  for (char *c = bus; *c; ++c) *c = (char)tolower(*c);
+  const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+  FILE *f = fopen(path.c_str(), "r");
+  if (!f) return 0;
+  char buf[4096] = {0};
+  const size_t got = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[got] = 0;
+  cpu_set_t allowed, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return 0;
+  int n = 0;
+  for (char *p = buf; *p && *p != '\n';) {  // "a-b,c,d-e"
+    char *e = nullptr;
+    const long a = strtol(p, &e, 10);
+    if (e == p) break;
+    long b = a;
+    p = e;
+    if (*p == '-') b = strtol(p + 1, &p, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (c >= 0 && CPU_ISSET(c, &allowed)) { CPU_SET(c, &want); ++n; }
+    if (*p == ',') ++p;
+  }
+  if (n == 0 || n == CPU_COUNT(&allowed)) return 0;
+  if (pthread_setaffinity_np(pthread_self(), sizeof want, &want) != 0) return 0;
+  return n;
+}
+}  // namespace rs
+
 int rs_engine_create(int device, rs_engine **eng) {
   try {
     int n = 0;
@@ -4056,6 +4098,10 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipSetDevice(device));
     hipDeviceProp_t prop;
     HC(hipGetDeviceProperties(&prop, device));
+    {
+      const int nb = bind_near_gpu(device);
+      if (g_prof_env && nb) fprintf(stderr, "[rs-prof] engine thread bound to the GPU's %d local CPUs\n", nb);
+    }
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
       set_error(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only");
       return RS_E_NODEVICE;
