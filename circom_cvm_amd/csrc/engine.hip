@@ -3239,7 +3239,7 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     // stream starts after half the pass
     const bool halves = E->stream_out && !(E->comm && E->comm->world > 1) && n_nl >= (getenv("RS_HALVES_MIN") ? strtoull(getenv("RS_HALVES_MIN"), nullptr, 10) : (1ull << 20)) &&
                        !getenv("RS_NO_HALVES");
-    static const double frac = getenv("RS_HALF_FRAC") ? atof(getenv("RS_HALF_FRAC")) : 0.5;
+    const double frac = getenv("RS_HALF_FRAC") ? atof(getenv("RS_HALF_FRAC")) : 0.5;
     const uint64_t h = halves ? std::max<uint64_t>(1, std::min<uint64_t>(n_nl - 1, (uint64_t)(n_nl * frac))) : n_nl;
     nl_phase(1, nullptr, n_nl, E->evx[8], E->evx[9], h, [&] { snap_take(nl_late, h); });
     if (!halves) snap_take(nl_late, n_nl);

@@ -159,6 +159,24 @@ def test_hosthost_streamed_layout(kind, rows, prime):
     pin.free()
 
 
+@pytest.mark.parametrize("kind,rows,frac", [(0, 400_000, "0.5"), (5, 300_000, "0.2"), (2, 200_000, "0.9")])
+def test_hosthost_first_pass_halves(kind, rows, frac, monkeypatch):
+    """The first frames pass in two parts with a snapshot after each (engine.hip nl_phase / snap_take_h2;
+    by default only from 1 M non-linear rows on): forced here on smaller circuits and at other split
+    points, the streamed result equals the oracle's on every call, and the off switch gives the same."""
+    inp = M.Input.synth(kind, rows, 11, "bn128")
+    pin = M.PinnedInput(inp.c)
+    fl = rsio.flags("O2")
+    ref, _ = rsio.oracle_arrays(inp.c, fl, threads=16)
+    monkeypatch.setenv("RS_HALVES_MIN", "2")
+    monkeypatch.setenv("RS_HALF_FRAC", frac)
+    for _ in range(3):  # the first call sizes the regions from its first part; later ones reuse them
+        assert rsio.diff_output_arrays(rsio.output_arrays(engine().simplify(pin.c, fl)), ref) is None
+    monkeypatch.setenv("RS_NO_HALVES", "1")
+    assert rsio.diff_output_arrays(rsio.output_arrays(engine().simplify(pin.c, fl)), ref) is None
+    pin.free()
+
+
 @pytest.mark.parametrize("level,rounds", [("O1", None), ("O2", 1), ("O2", 2)])
 def test_hosthost_streamed_levels(level, rounds):
     """The streamed result at --O1 (every linear row joins lconst and goes with the first early region)
