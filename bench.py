@@ -91,6 +91,7 @@ def shard_seed(seed: int, rank: int) -> int:
 
 
 KERNELS = (  # (name, stats fields: ms, bytes, launches)
+    # the first three are ONE kernel each between their HIP events (SINGLE below); the rest are groups
     ("k_big_spec<12> (head)", "head_main_ms", "head_main_bytes", "head_launches"),
     # the tail's byte counter includes k_p3_fast's clusters (its PMC traffic is added likewise);
     # the time is k_big_main's
@@ -109,6 +110,55 @@ KERNELS = (  # (name, stats fields: ms, bytes, launches)
     ("ragged conversion + linear frames (k_make_ragged, k_lin_*frames*)", "ragged_ms", "ragged_bytes", "ragged_launches"),
     ("result gathers (k_snap_gather*, k_lc_*, k_gather_late, k_gather_rows)", "gather_ms", "gather_bytes", "gather_launches"),
 )
+
+
+# entries whose HIP-event pair brackets exactly one kernel launch, with that kernel's rocprof name: the
+# headline roofline's "dominant kernel" is chosen among these by device time (a group's span can hold
+# several kernels, host waits and syncs -- the clustering's did -- so it is reported, not ranked)
+SINGLE = {
+    "k_big_spec<12> (head)": "rs::k_big_spec<12>(",
+    "k_big_main<256> (tail)": "rs::k_big_main<256u>(",
+    "k_frames_wave<0> (non-linear)": "rs::k_frames_wave<0>(",
+}
+
+
+def kernel_profile():
+    """Per-kernel rows (calls, average ns) of the newest committed rocprofv3 --kernel-trace --stats summary
+    of the metric circuit (profiles/round*_kernel_stats.csv; the templated circuit's file is not it)."""
+    import csv
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "round*_kernel_stats.csv"))
+                   if re.fullmatch(r"round\d+_kernel_stats\.csv", os.path.basename(f)))
+    if not files:
+        return [], None
+    with open(files[-1]) as f:
+        rows = [(r["Name"], int(r["Calls"]), float(r["AverageNs"]), float(r["TotalDurationNs"])) for r in csv.DictReader(f)]
+    rows.sort(key=lambda r: -r[3])
+    return rows, os.path.relpath(files[-1], ROOT)
+
+
+def link_probe(mib: int = 512):
+    """The box's PCIe link between HBM and page-locked host memory: H2D and D2H of `mib` MiB in 32 MiB
+    chunks (the input's and the result stream's pattern), best of 3 each -- so a host -> host number can
+    be read against the link it ran on (torch tensors; freed before the measurement starts)."""
+    import torch
+    chunk = 32 << 20
+    dev = torch.empty(mib << 20, dtype=torch.uint8, device="cuda")
+    host = torch.empty(mib << 20, dtype=torch.uint8, pin_memory=True)
+    res = {}
+    for name, src, dst in (("h2d_GBps", host, dev), ("d2h_GBps", dev, host)):
+        best = 0.0
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for o in range(0, mib << 20, chunk):
+                dst[o:o + chunk].copy_(src[o:o + chunk], non_blocking=True)
+            torch.cuda.synchronize()
+            best = max(best, (mib << 20) / (time.perf_counter() - t0) / 1e9)
+        res[name] = round(best, 1)
+    del dev, host
+    torch.cuda.empty_cache()
+    res["what"] = f"{mib} MiB in 32 MiB chunks between HBM and pinned host memory, best of 3 (torch), before the timed region"
+    return res
 
 
 def pmc_traffic():
@@ -212,7 +262,8 @@ def _prime_value(name: str) -> int:
 def timed_steps(eng, inp_c, fl, steps, barrier):
     """K host -> host steps between barriers; per-kernel device time/bytes summed over them."""
     acc = {k: [0.0, 0, 0] for k, *_ in KERNELS}
-    tot = {"alg_bytes": 0, "total_ms": 0.0, "h2d_wait_ms": 0.0, "d2h_ms": 0.0, "host_total_ms": 0.0}
+    tot = {"alg_bytes": 0, "total_ms": 0.0, "h2d_wait_ms": 0.0, "d2h_ms": 0.0, "host_total_ms": 0.0,
+           "cluster_ms": 0.0, "cluster_host_ms": 0.0}
     barrier()
     t0 = time.perf_counter()
     out = None
@@ -245,6 +296,7 @@ def main():
     ap.add_argument("--no-templated", action="store_true", help="skip the template-replicated extra circuit")
     ap.add_argument("--no-o1", action="store_true", help="skip the --O1 extra (the metric circuit at circom's default level)")
     ap.add_argument("--no-linear1m", action="store_true", help="skip BASELINE configs[1] (1 M purely linear rows, one run)")
+    ap.add_argument("--no-link", action="store_true", help="skip the PCIe link probe")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,6 +320,12 @@ def main():
             dist.barrier()
 
     fl = M.make_flags("O2", device=local)
+    link = None
+    if not args.no_link:
+        try:
+            link = link_probe()
+        except Exception as e:  # noqa: BLE001 -- a missing torch / device leaves the field out, not the bench
+            link = {"error": str(e)[:200]}
     # ---- the headline: the metric circuit (ONE circuit over all ranks when N > 1), host -> host
     inp = M.Input.synth(0, args.rows, args.seed, args.prime)
     n_rows = inp.rows()
@@ -380,9 +438,11 @@ def main():
         K = args.steps
         ms_step = dt * 1000.0 / K
         value = n_rows * K / dt
-        # the dominant kernel: the largest device time over the timed region
-        k_name = max(acc, key=lambda k: acc[k][0])
+        # the dominant kernel: the largest device time over the timed region among the entries that time
+        # one kernel (SINGLE); rocprof's own summary of the same bench names the same kernel first
+        k_name = max((k for k in acc if k in SINGLE), key=lambda k: acc[k][0])
         traffic_tab, traffic_src = pmc_traffic()
+        prof_rows, prof_src = kernel_profile()
 
         def kline(k):
             ms, by, n = acc[k]
@@ -422,6 +482,7 @@ def main():
                          "traffic_source": traffic_src, "avg_launch_ms": dom["avg_launch_ms"],
                          "alg_bytes_per_launch": dom["alg_bytes_per_launch"],
                          "launches_per_step": dom["launches_per_step"],
+                         "timing": "HIP events around each launch of this one kernel on the stream it runs on",
                          "path": {"alg_bytes_per_step": int(tot["alg_bytes"] / K), "T_simplify_ms": round(ms_step, 3),
                                   "achieved": round(path_ach, 2), "frac": round(path_ach / HBM_PEAK_GBS, 5)},
                          "kernels": {k: kline(k) for k in acc if acc[k][2]}},
@@ -433,6 +494,27 @@ def main():
                              "ms_per_step": round(dt_hbm * 1000.0 / K, 3),
                              "what": "rs_engine_run: input already in HBM -> result in HBM (no PCIe)"},
         }
+        if prof_rows:
+            # the same kernel in the committed rocprofv3 summary: its average launch and the roofline
+            # fraction recomputed from it (the line's frac must follow from the profile)
+            pat = SINGLE[k_name]
+            hit = next((r for r in prof_rows if pat in r[0]), None)
+            top = prof_rows[0]
+            rf = line["roofline"]
+            rf["profile"] = {"source": prof_src, "top_kernel": top[0], "top_kernel_share": round(top[3] / sum(r[3] for r in prof_rows), 4)}
+            if hit is not None:
+                pavg = hit[2] / 1e6
+                pach = dom["alg_bytes_per_launch"] / (pavg / 1000.0) / 1e9
+                rf["profile"].update({"kernel": hit[0], "calls": hit[1], "avg_launch_ms": round(pavg, 4),
+                                      "avg_over_bench": round(pavg / max(dom["avg_launch_ms"], 1e-9), 3),
+                                      "achieved_from_profile": round(pach, 3), "frac_from_profile": round(pach / HBM_PEAK_GBS, 6)})
+        # the clustering group's span (HIP events on the main stream) split into the device-busy part and
+        # the host's round trips inside it (synchronisations, the host replay)
+        line["clustering"] = {"span_ms": round(acc["build_clusters (k_cl_*, pair sort, arena replays)"][0] / K, 3),
+                              "host_wait_ms": round(tot["cluster_host_ms"] / K, 3),
+                              "host_ms": round(tot["cluster_ms"] / K, 3)}
+        if link is not None:
+            line["link"] = link
         if write is not None:
             line["write_r1cs"] = write
         if flat is not None:

@@ -126,7 +126,8 @@ class RsStats(C.Structure):
                 ("tail_fin_ms", C.c_double), ("tail_fin_bytes", C.c_uint64), ("tail_fin_launches", C.c_uint64), ("head_fin_ms", C.c_double), ("head_fin_bytes", C.c_uint64), ("head_fin_launches", C.c_uint64), ("small_ms", C.c_double), ("small_bytes", C.c_uint64), ("small_launches", C.c_uint64), ("prep_ms", C.c_double), ("prep_launches", C.c_uint64), ("cluster_dev_ms", C.c_double), ("cluster_bytes", C.c_uint64), ("cluster_launches", C.c_uint64), ("giant_ms", C.c_double), ("giant_bytes", C.c_uint64), ("giant_launches", C.c_uint64), ("giant_merges", C.c_uint64),
                 ("check_ms", C.c_double), ("check_bytes", C.c_uint64), ("check_launches", C.c_uint64),
                 ("ragged_ms", C.c_double), ("ragged_bytes", C.c_uint64), ("ragged_launches", C.c_uint64),
-                ("gather_ms", C.c_double), ("gather_bytes", C.c_uint64), ("gather_launches", C.c_uint64)]
+                ("gather_ms", C.c_double), ("gather_bytes", C.c_uint64), ("gather_launches", C.c_uint64),
+                ("cluster_host_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

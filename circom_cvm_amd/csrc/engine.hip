@@ -279,7 +279,8 @@ struct rs_engine {
     size_t cap = 0;
   };
   Pin pin[40];  // a/b/c: ptr, col, val; label_to_wire; spare; rs_engine_write_r1cs's two staging buffers;
-                // a/b/c row ends (streamed result); [16..17] the host replay's staging; [20..38]
+                // a/b/c row ends (streamed result); [16..17] the host replay's staging; [18..19] the
+                // clustering's read-backs; [20..38]
                 // rs_engine_flatten_dag's result (19 arrays)
   rs_input flat_view{};  // rs_engine_flatten_dag's result (views pin[20..38])
   rs_output view{};
@@ -322,6 +323,8 @@ struct rs_engine {
   std::deque<SnapJob> snap_q;  // jobs the D2H thread has not started; closed: no more will come
   bool snap_closed = true;
   std::thread snap_thread;
+  cpu_set_t near_cpus;  // the GPU's NUMA-local CPUs the creator's mask allowed (near_gpu_cpus)
+  int near_n = 0;
   hipStream_t stx = nullptr;  // the early region's D2H stream
   hipStream_t str = nullptr;  // the host replay's copies (small; never behind the bulk copies)
   hipStream_t ste = nullptr;  // the small clusters' elimination (k_eliminate), beside the tail's chain
@@ -614,17 +617,21 @@ static void h2d(rs_engine *E, void *dst, const void *src, size_t bytes) {
 }
 
 // ---------------------------------------------------------------- scans
-static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, uint64_t n, const char *tag) {
+static void *pin_get(rs_engine *E, int slot, size_t bytes);
+static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, uint64_t n, const char *tag,
+                              double *waited = nullptr) {
   if (n == 0) return 0;
   size_t tb = 0;
   HC(rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), E->st));
   void *tmp = E->A.get<uint8_t>(std::string("scan.tmp.") + tag, tb);
   HC(rocprim::exclusive_scan(tmp, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), E->st));
-  uint64_t last_in = 0, last_out = 0;
-  HC(hipMemcpyAsync(&last_in, in + n - 1, 8, hipMemcpyDeviceToHost, E->st));
-  HC(hipMemcpyAsync(&last_out, out + n - 1, 8, hipMemcpyDeviceToHost, E->st));
+  uint64_t *h = (uint64_t *)pin_get(E, 18, 64) + 4;  // pinned read-back words [4..5] (no staged copy)
+  HC(hipMemcpyAsync(h, in + n - 1, 8, hipMemcpyDeviceToHost, E->st));
+  HC(hipMemcpyAsync(h + 1, out + n - 1, 8, hipMemcpyDeviceToHost, E->st));
+  const double t0 = waited ? now_ms() : 0.0;
   HC(hipStreamSynchronize(E->st));
-  return last_in + last_out;
+  if (waited) *waited += now_ms() - t0;
+  return h[0] + h[1];
 }
 
 // one scan over three capacity columns at once (separate [a..][b..][c..] blocks keep neighbouring
@@ -690,6 +697,14 @@ static void sort_pairs(rs_engine *E, const K *kin, K *kout, const V *vin, V *vou
   HC(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, s));
   void *tmp = E->A.get<uint8_t>(std::string("sort.tmp.") + tag, tb);
   HC(rocprim::radix_sort_pairs(tmp, tb, kin, kout, vin, vout, (size_t)n, 0, end_bit, s));
+}
+// device-only exclusive scan of u64 on stream s (no read-back)
+static void dev_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s, const char *tag) {
+  if (!n) return;
+  size_t tb = 0;
+  HC(rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+  void *tmp = E->A.get<uint8_t>(std::string("scan.tmp.") + tag, tb);
+  HC(rocprim::exclusive_scan(tmp, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
 }
 // device-only exclusive scan of u32 on stream s (no read-back; tmp sized on first use)
 static void dev_scan_u32(rs_engine *E, const uint32_t *in, uint32_t *out, uint64_t n, hipStream_t s, const char *tag) {
@@ -1201,6 +1216,9 @@ static void host_replay(uint32_t n, const uint64_t *qo, const uint32_t *st, cons
   }
 }
 
+__global__ void k_put_u64(uint64_t *p, uint64_t v) {
+  if (gtid() == 0) *p = v;
+}
 static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, const uint8_t *d_forb, ElimOut &eo) {
   Arena &A = E->A;
   hipStream_t st = E->st;
@@ -1210,16 +1228,38 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   D.cl_off = A.get<uint64_t>("el.cl", 1);
   HC(hipMemsetAsync(D.cl_off, 0, 8, st));
   if (n == 0) return D;
+  // the host's share of the span: time blocked in the read-backs' synchronisations and in the host
+  // replay (rs_stats.cluster_host_ms); RS_PROF prints the host clock at each step
+  double &hw = E->stats.cluster_host_ms;
+  std::vector<std::pair<const char *, double>> marks;
+  auto mark = [&](const char *w) {
+    if (g_prof_env) marks.emplace_back(w, now_ms());
+  };
+  auto sync = [&](hipStream_t s) {
+    const double t = now_ms();
+    HC(hipStreamSynchronize(s));
+    hw += now_ms() - t;
+  };
+  struct PrintMarks {
+    std::vector<std::pair<const char *, double>> &m;
+    ~PrintMarks() {
+      if (m.size() < 2) return;
+      fprintf(stderr, "[rs-prof] clustering host clock (ms from the start):");
+      for (size_t i = 1; i < m.size(); ++i) fprintf(stderr, " %s %.2f", m[i].first, m[i].second - m[0].second);
+      fprintf(stderr, "\n");
+    }
+  } print_marks{marks};
+  mark("start");
   HC(hipEventRecord(E->evc[0], st));
   uint64_t *npairs = A.get<uint64_t>("cl.np", n);
   unsigned long long *stat = A.get<unsigned long long>("cl.stat", 8);
   HC(hipMemsetAsync(stat, 0, 64, st));
   launch_capped(st, k_cl_count, n, 1024, V, npairs, stat);
   uint64_t *poff = A.get<uint64_t>("cl.poff", n);
-  const uint64_t P = excl_scan_u64(E, npairs, poff, n, "cl1");
-  unsigned long long hs[2];
+  unsigned long long *hs = (unsigned long long *)pin_get(E, 18, 64);  // pinned: no staged copy
   HC(hipMemcpyAsync(hs, stat, 16, hipMemcpyDeviceToHost, st));
-  HC(hipStreamSynchronize(st));
+  const uint64_t P = excl_scan_u64(E, npairs, poff, n, "cl1", &hw);  // (its read-back synchronises)
+  mark("pairs");
   D.tot_nnz = hs[0];
   const uint64_t n_act = hs[1];
   if (n_act == 0) return D;
@@ -1247,7 +1287,8 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   sort_pairs(E, (const uint64_t *)rk, rk2, (const uint32_t *)ri, srow, n, 64, "cl2");
   uint64_t *flag = A.get<uint64_t>("cl.flag", n_act), *fscan = A.get<uint64_t>("cl.fscan", n_act);
   launch(st, k_cl_flag, n_act, (const uint64_t *)rk2, n_act, flag);
-  const uint64_t n_cl = excl_scan_u64(E, flag, fscan, n_act, "cl2");
+  const uint64_t n_cl = excl_scan_u64(E, flag, fscan, n_act, "cl2", &hw);
+  mark("clusters");
   D.cl_off = A.get<uint64_t>("el.cl", n_cl + 1);
   uint32_t *cid = A.get<uint32_t>("cl.cid", n_act), *gpos = A.get<uint32_t>("cl.gpos", n);
   uint64_t *qn = A.get<uint64_t>("cl.qn", n_act), *q_off = A.get<uint64_t>("cl.qoff", n_act + 1);
@@ -1255,8 +1296,12 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   HC(hipMemsetAsync(n_ordered, 0, 4 * n_cl, st));
   launch(st, k_cl_starts, n_act, (const uint64_t *)rk2, (const uint64_t *)fscan, (const uint32_t *)srow,
          (const uint64_t *)npairs, n_act, n_cl, D.cl_off, cid, gpos, qn, (const uint8_t *)has_unique, n_ordered);
-  const uint64_t Q = excl_scan_u64(E, qn, q_off, n_act, "cl3");
-  h2d(E, q_off + n_act, &Q, 8);
+  // the stream holds every active row's pairs once: Q = P (no read-back, and no host-to-device copy
+  // of the total queued behind the input's upload on the copy engine)
+  const uint64_t Q = P;
+  dev_scan_u64(E, qn, q_off, n_act, st, "cl3");
+  hipLaunchKernelGGL(k_put_u64, dim3(1), dim3(64), 0, st, q_off + n_act, Q);
+  HC(hipGetLastError());
   uint32_t *stream = A.get<uint32_t>("cl.stream", Q);
   launch(st, k_cl_stream, n_act, (const uint32_t *)srow, (const uint64_t *)poff, (const uint32_t *)prevrow,
          (const uint32_t *)gpos, (const uint32_t *)cid, (const uint64_t *)D.cl_off, (const uint64_t *)q_off, n_act,
@@ -1267,13 +1312,16 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   unsigned long long *cnt = stat + 2;
   launch_capped(st, k_cl_sizekey, n_cl, 1024, (const uint64_t *)D.cl_off, n_cl, (const uint32_t *)srow, (const uint32_t *)V.len, sk, si, cnt);
   sort_pairs(E, (const uint64_t *)sk, sk2, (const uint32_t *)si, sorted, n_cl, 64, "cl3");
-  unsigned long long hc[5];
-  // the size keys of the largest clusters (the head's; the giant path reads their row counts)
+  // the size keys of the largest clusters (the head's; the giant path reads their row counts) and the
+  // class counts, into pinned memory in one read-back
   const uint64_t n_top = std::min<uint64_t>(n_cl, kHeadLimit);
-  D.top_keys.assign(n_top, 0);
+  unsigned long long *hcb = (unsigned long long *)pin_get(E, 19, 8 * (8 + kHeadLimit));
+  unsigned long long *hc = hcb;
   HC(hipMemcpyAsync(hc, cnt, 40, hipMemcpyDeviceToHost, st));
-  HC(hipMemcpyAsync(D.top_keys.data(), sk2, 8 * n_top, hipMemcpyDeviceToHost, st));
-  HC(hipStreamSynchronize(st));
+  if (n_top) HC(hipMemcpyAsync(hcb + 8, sk2, 8 * n_top, hipMemcpyDeviceToHost, st));
+  sync(st);
+  D.top_keys.assign(hcb + 8, hcb + 8 + n_top);
+  mark("sizes");
   const uint64_t first = n_top ? D.top_keys[0] : 0;
   // replay of the arena merges -> row order inside every cluster
   D.perm = A.get<uint32_t>("el.perm", n_act);
@@ -1304,7 +1352,8 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
            (const uint64_t *)q_off, (const uint32_t *)n_ordered, d_meta);
     uint64_t *meta = (uint64_t *)pin_get(E, 16, 40 * nh);
     HC(hipMemcpyAsync(meta, d_meta, 40 * nh, hipMemcpyDeviceToHost, E->str));
-    HC(hipStreamSynchronize(E->str));
+    sync(E->str);
+    mark("replay meta");
     HC(hipEventRecord(E->evx[6], st));
     HC(hipStreamWaitEvent(E->st2, E->evx[6], 0));
     std::vector<uint64_t> todo;
@@ -1338,7 +1387,8 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
         on += qn;
         o += qn + 1;
       }
-      HC(hipStreamSynchronize(E->str));
+      sync(E->str);
+      mark("replay staged");
       std::atomic<uint64_t> next_t{0};
       auto work = [&] {  // a few host threads, largest cluster first (the list is size-ordered)
         for (uint64_t t; (t = next_t.fetch_add(1)) < nt;) {
@@ -1349,17 +1399,21 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
           host_replay(n_i, rel.data(), hst + o_q[t], hsrow + o_n[t], hperm + o_n[t]);
         }
       };
-      const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-      const uint64_t n_th = std::min<uint64_t>({nt, (uint64_t)hw, 16});
+      const unsigned hwc = std::max(1u, std::thread::hardware_concurrency());
+      const uint64_t n_th = std::min<uint64_t>({nt, (uint64_t)hwc, 16});
+      const double tr0 = now_ms();
       std::vector<std::thread> th;
       for (uint64_t k = 1; k < n_th; ++k) th.emplace_back(work);
       work();
       for (auto &t : th) t.join();
+      hw += now_ms() - tr0;
+      mark("replayed");
       for (uint64_t t = 0; t < nt; ++t) {
         const uint64_t i = todo[t];
         HC(hipMemcpyAsync(D.perm + meta[5 * i], hperm + o_n[t], 4 * meta[5 * i + 1], hipMemcpyHostToDevice, E->st2));
       }
-      HC(hipStreamSynchronize(E->st2));  // the staging block is reused by the next round's replay
+      sync(E->st2);  // the staging block is reused by the next round's replay
+      mark("orders back");
     }
     if (g_prof_env)
       fprintf(stderr, "[rs-prof] host replay: %llu clusters (%llu order-free), %llu rows, %llu pairs, %.2f ms\n", (unsigned long long)nh,
@@ -1964,7 +2018,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       err = 0;
       for (uint64_t x : CM->gather_u64(mine, E->st)) err |= (int)x;
     }
-    if (err & 8) {
+    if ((err & 8) && !(err & kGiErrBounds)) {  // pool exhausted (a bounds violation fails below instead)
       size_t fr_ = 0, tot_ = 0;
       (void)hipMemGetInfo(&fr_, &tot_);
       if (getenv("RS_PROF")) {
@@ -4050,11 +4104,14 @@ int rs_abi_version(void) { return RS_ABI_VERSION; }
 namespace rs {
 // The host side of a call (synchronisations, the clustering's host replay, the result stream's thread)
 // is latency-bound; on a multi-socket host a thread placed on the far socket from the GPU ran every
-// call ~5 ms slower (the metric circuit, 42 vs 47-49 ms, process to process).  So the thread that
-// creates an engine -- and the threads it starts later, which inherit it -- is bound to the CPUs of
-// the GPU's own NUMA node (sysfs local_cpulist of its PCI function) that its affinity allows.
-// RS_NO_CPU_BIND=1 leaves the affinity alone; returns the CPUs bound to (0: unchanged).
-static int bind_near_gpu(int device) {
+// call ~5 ms slower (the metric circuit, 42 vs 47-49 ms, process to process).  So for the duration of
+// each engine call the calling thread -- and the threads the call starts (host replay, result stream,
+// writer), which inherit it -- runs on the CPUs of the GPU's own NUMA node (sysfs local_cpulist of its
+// PCI function) that the caller's affinity allows; the caller's own mask is restored when the call
+// returns (CpuNear), so a host thread pool created later, or an engine on the other socket, is not
+// narrowed by an earlier one.  near_gpu_cpus: that node's CPU set among the creator's allowed CPUs
+// (the count; 0: no binding, e.g. RS_NO_CPU_BIND=1, one node, or no sysfs entry).
+static int near_gpu_cpus(int device, cpu_set_t *want_out) {
   if (getenv("RS_NO_CPU_BIND")) return 0;
   char bus[64] = {0};
   if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return 0;
@@ -4082,8 +4139,25 @@ static int bind_near_gpu(int device) {
     if (*p == ',') ++p;
   }
   if (n == 0 || n == CPU_COUNT(&allowed)) return 0;
-  if (pthread_setaffinity_np(pthread_self(), sizeof want, &want) != 0) return 0;
+  *want_out = want;
   return n;
+}
+// RAII: the calling thread on the engine's GPU-near CPUs for one call (those its own mask allows),
+// its mask restored on return
+struct CpuNear {
+  cpu_set_t old;
+  bool set = false;
+  explicit CpuNear(const rs_engine *E);
+  ~CpuNear() {
+    if (set) (void)pthread_setaffinity_np(pthread_self(), sizeof old, &old);
+  }
+};
+CpuNear::CpuNear(const rs_engine *E) {
+  if (!E || !E->near_n || pthread_getaffinity_np(pthread_self(), sizeof old, &old) != 0) return;
+  cpu_set_t want;
+  CPU_AND(&want, &old, &E->near_cpus);
+  if (CPU_COUNT(&want) == 0 || CPU_EQUAL(&want, &old)) return;
+  set = pthread_setaffinity_np(pthread_self(), sizeof want, &want) == 0;
 }
 }  // namespace rs
 
@@ -4098,16 +4172,15 @@ int rs_engine_create(int device, rs_engine **eng) {
     HC(hipSetDevice(device));
     hipDeviceProp_t prop;
     HC(hipGetDeviceProperties(&prop, device));
-    {
-      const int nb = bind_near_gpu(device);
-      if (g_prof_env && nb) fprintf(stderr, "[rs-prof] engine thread bound to the GPU's %d local CPUs\n", nb);
-    }
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
       set_error(std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only");
       return RS_E_NODEVICE;
     }
     std::unique_ptr<rs_engine> E(new rs_engine());
     E->device = device;
+    CPU_ZERO(&E->near_cpus);
+    E->near_n = near_gpu_cpus(device, &E->near_cpus);
+    if (g_prof_env && E->near_n) fprintf(stderr, "[rs-prof] engine calls run on the GPU's %d local CPUs\n", E->near_n);
     E->n_cu = (uint32_t)prop.multiProcessorCount;
     HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
     {  // the second stream carries the critical path (the largest clusters' chain): high priority
@@ -4228,6 +4301,7 @@ void rs_engine_destroy(rs_engine *E) {
 }
 
 int rs_engine_load(rs_engine *E, const rs_input *in) {
+  CpuNear cpu_near_(E);  // the caller's affinity is restored on return
   CallScope cs(E);
   try {
     HC(hipSetDevice(E->device));
@@ -4249,6 +4323,7 @@ int rs_engine_load(rs_engine *E, const rs_input *in) {
 }
 
 int rs_engine_run(rs_engine *E, const rs_flags *fl) {
+  CpuNear cpu_near_(E);  // the caller's affinity is restored on return
   CallScope cs(E);
   try {
     if (!E->loaded) { set_error("engine has no input"); return RS_E_INVALID; }
@@ -4478,6 +4553,7 @@ static void fetch_result_shared(rs_engine *E, rs_output *o, bool own_log) {
 }  // namespace rs
 
 int rs_engine_fetch(rs_engine *E, rs_output **out) {
+  CpuNear cpu_near_(E);  // the caller's affinity is restored on return
   try {
     if (!E->have_result) { set_error("no result"); return RS_E_INVALID; }
     HC(hipSetDevice(E->device));
@@ -4501,6 +4577,7 @@ int rs_engine_fetch(rs_engine *E, rs_output **out) {
 }
 
 int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, const rs_output **out) {
+  CpuNear cpu_near_(E);  // the caller's affinity is restored on return
   CallScope cs(E);
   try {
     const double t0 = now_ms();
@@ -4542,6 +4619,7 @@ int rs_engine_simplify(rs_engine *E, const rs_input *in, const rs_flags *fl, con
 // rs_write_r1cs on the fetched output): the constraint section is built on the device (writer.hpp)
 // and streamed to the file through two pinned staging buffers; the small sections follow.  o0_r1cs (optional): custom-gate sections as rs_write_r1cs_gates.
 int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
+  CpuNear cpu_near_(E);  // the caller's affinity is restored on return
   try {
     if (!E->have_result) { set_error("no result"); return RS_E_INVALID; }
     HC(hipSetDevice(E->device));
@@ -4901,6 +4979,7 @@ int rs_flatten_dag(int device, const rs_dag *dag, rs_input **in) {
 }
 
 int rs_engine_flatten_dag(rs_engine *E, const rs_dag *dag, const rs_input **in) {
+  CpuNear cpu_near_(E);  // the caller's affinity is restored on return
   if (!E || !dag || !in) { set_error("rs_engine_flatten_dag: null argument"); return RS_E_INVALID; }
   *in = nullptr;
   try {

@@ -39,6 +39,11 @@ namespace rs {
 constexpr uint64_t kGiantRows = 11800;   // head clusters with this many rows take the giant path
 constexpr uint64_t kGiForb = ~0ull;      // gst: a forbidden signal
 constexpr uint64_t kGiDel = 1ull << 63;  // gst: deleted; low bits = its holder's pool header offset (else: occurrences)
+// err bit of a giant-path bounds violation (a table probe that finds no free slot, a slot / position /
+// pool offset outside its cluster or the pool): the run fails with RS_E_INTERNAL instead of touching
+// memory out of range.  None is reachable when the invariants hold; the guards keep a broken one from
+// becoming an illegal access (round 5's scratch run s5i faulted in this path).
+constexpr int kGiErrBounds = 128;
 
 struct GiantArgs {
   uint64_t ci;                 // the cluster's position in the head list (A.big_alive / touch arrays)
@@ -96,8 +101,12 @@ __global__ void k_gi_state(ElimArgs A, GiantArgs G, uint64_t c) {
       if (A.forb[s]) { G.gst[s] = kGiForb; continue; }
       G.uf[s] = s;
       uint64_t st;
-      if (A.del[s]) st = kGiDel | (A.h_off[A.holder_idx[s]] - 1);  // k_big_prep / d_clear_nn: header before the RHS
-      else st = A.occ[s] < 0 ? 0ull : (uint64_t)A.occ[s];         // process_3 keeps no counts
+      if (A.del[s]) {  // k_big_prep / d_clear_nn: header before the RHS
+        const int32_t hi = A.holder_idx[s];
+        const uint64_t ho = hi >= 0 ? A.h_off[hi] : 0;
+        if (hi < 0 || ho == 0 || ho > A.pool_cap) { atomicOr(A.err, kGiErrBounds); G.gst[s] = kGiForb; continue; }
+        st = kGiDel | (ho - 1);
+      } else st = A.occ[s] < 0 ? 0ull : (uint64_t)A.occ[s];         // process_3 keeps no counts
       G.gst[s] = st;
     }
   }
@@ -193,10 +202,11 @@ __global__ __launch_bounds__(1024) void k_gi_segment(ElimArgs A, GiantArgs G) {
 // slot bases and the state word kept current)
 __device__ inline bool d_gi_serial(const ElimArgs &A, const GiantArgs &G, Alloc &al, uint64_t sub_base, uint64_t left_base,
                                    uint32_t qi, const uint32_t *k, const Fe *v, uint32_t len, uint32_t &m, uint32_t &nl, bool p4,
-                                   unsigned long long &by) {
+                                   unsigned long long &by, uint64_t slot_end) {
   const FieldP &F = A.F;
   for (;;) {
     if (len == 0) return true;
+    if (left_base + nl >= slot_end || sub_base + m >= slot_end) { atomicOr(A.err, kGiErrBounds); return false; }
     uint32_t oi = RS_NONE;
     int32_t occ_ret = -1;
     for (uint32_t i = 0; i < len; ++i) {
@@ -237,6 +247,7 @@ __device__ inline bool d_gi_serial(const ElimArgs &A, const GiantArgs &G, Alloc 
     }
     uint64_t w_off;
     uint32_t w_len;
+    if (A.h_off[hi] + A.h_len[hi] > A.pool_cap) { atomicOr(A.err, kGiErrBounds); return false; }
     by += 36ull * (len + A.h_len[hi]);
     if (!d_merge(A, al, k, v, len, oi, fneg(F, v[oi]), A.h_coef[hi], A.h_off[hi], A.h_len[hi], w_off, w_len)) return false;
     k = A.pk + w_off;
@@ -300,10 +311,11 @@ __device__ __forceinline__ uint32_t gh_hash(uint32_t k) { return (k * 0x9E3779B1
 __device__ __forceinline__ uint32_t gh_ld(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// claims the first free (empty or tombstone) slot of K's probe sequence (the table always has one)
+// claims the first free (empty or tombstone) slot of K's probe sequence (the table always has one
+// when the loads are bounded as below; a full table returns kGhEmpty and the caller flags the run)
 __device__ __forceinline__ uint32_t gh_claim(GhSmem &S, uint32_t K) {
   uint32_t s = gh_hash(K);
-  for (;;) {
+  for (uint32_t i = 0; i < 4 * kGhSlots; ++i) {  // each failed CAS means another lane took a slot
     const uint32_t t = gh_ld(&S.tk[s]);
     if (t >= kGhTomb) {
       if (atomicCAS(&S.tk[s], t, K) == t) return s;
@@ -311,6 +323,7 @@ __device__ __forceinline__ uint32_t gh_claim(GhSmem &S, uint32_t K) {
     }
     s = (s + 1) & (kGhSlots - 1);
   }
+  return kGhEmpty;
 }
 // the slot holding K, or kGhEmpty.  Keys are placed at the first free slot of their sequence and
 // slots never become empty inside a row (only tombstones), so the first empty slot ends the search;
@@ -380,6 +393,13 @@ __device__ __forceinline__ void gh_reduce(GhSmem &S, uint32_t q, bool p4, uint32
 // outstanding global load.
 __device__ __forceinline__ void gh_lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// thread 0's pool allocation in the loop: RS_NONE (and the run flagged) past the pool
+__device__ __forceinline__ uint64_t gi_alloc(const ElimArgs &A, Alloc &al, uint64_t n) {
+  const uint64_t o = pool_alloc(A, al, n);
+  if (o != RS_NONE && o + n > A.pool_cap) { atomicOr(A.err, kGiErrBounds); return RS_NONE; }
+  return o;
+}
+
 __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G, uint64_t c) {
   __shared__ GhSmem S;
   const FieldP &F = A.F;
@@ -405,10 +425,16 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
     __syncthreads();
     if (tid == 0) S.s_comp = atomicAdd(&G.scal[1], 1u);
     __syncthreads();
-    const uint32_t kc = S.s_comp;
-    if (kc >= G.scal[0] || !S.s_ok) break;
+    const uint32_t kc = S.s_comp, n_comp = G.scal[0];
+    if (kc >= n_comp || !S.s_ok) break;
     const uint32_t comp = G.cidx2[kc];
-    const uint32_t start = G.c_start[comp], size = G.c_size[comp];
+    const uint32_t n_loop = A.big_alive[G.ci];
+    // the component's range of the sorted row list (uniform: every thread reads the same words)
+    const uint32_t start = comp < n_comp ? G.c_start[comp] : 0u, size = comp < n_comp ? G.c_size[comp] : 0u;
+    if (comp >= n_comp || (uint64_t)start + size > n_loop || (uint64_t)n_uniq + n_loop > e - b) {
+      if (tid == 0) { S.s_ok = 0; atomicOr(A.err, kGiErrBounds); }
+      break;
+    }
     const uint64_t sub_base = b + n_uniq + start, left_base = b + start;
     if (tid == 0) { S.s_m = 0; S.s_nl = 0; }
     const uint64_t clk0 = G.c_clk ? wall_clock64() : 0;
@@ -417,6 +443,11 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
     for (uint32_t ii = start + size; ii-- > start;) {  // pop order: descending position (Vec::pop)
       if (!S.s_ok) break;
       const uint32_t qi = G.rval2[ii];
+      if (qi >= n_loop) {  // uniform
+        if (tid == 0) { S.s_ok = 0; atomicOr(A.err, kGiErrBounds); }
+        __syncthreads();
+        break;
+      }
       const uint64_t r_off = A.row_off[b + qi];
       const uint32_t len = A.row_len[b + qi];
       const uint32_t *rk0 = A.rows.key + r_off;
@@ -431,7 +462,7 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
         __syncthreads();
         if (tid == 0) {
           uint32_t m = S.s_m, nl = S.s_nl;
-          if (!d_gi_serial(A, G, al0, sub_base, left_base, qi, rk0, rv0, len, m, nl, p4, by)) S.s_ok = 0;
+          if (!d_gi_serial(A, G, al0, sub_base, left_base, qi, rk0, rv0, len, m, nl, p4, by, e)) S.s_ok = 0;
           S.s_m = m;
           S.s_nl = nl;
         }
@@ -452,8 +483,12 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
           A.occ[s] = (int32_t)st;
         }
         const uint32_t at = gh_claim(S, s);
-        S.tv[at] = rv0[tid];
-        S.ts[at] = st;
+        if (at != kGhEmpty) {
+          S.tv[at] = rv0[tid];
+          S.ts[at] = st;
+        } else {
+          atomicOr(A.err, kGiErrBounds);
+        }
       }
       __syncthreads();
       if (wsd) {
@@ -489,6 +524,11 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
         if (merge) {
           // ---- conflict with holder(p): work = c2*work - c*R (:338-347), c = -v_p
           const uint64_t hdr = pst & ~kGiDel;
+          if (hdr >= A.pool_cap) {  // uniform: a state word that points past the pool
+            if (tid == 0) { S.s_ok = 0; atomicOr(A.err, kGiErrBounds); }
+            __syncthreads();
+            break;
+          }
           // header and right-hand side in one round trip: waves 2-3 load before the length is known
           const bool rlane = !wsd && lane >= 1 && hdr + lane < A.pool_cap;
           uint32_t K = 0;
@@ -498,20 +538,29 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
             R = A.pv[hdr + lane];
           }
           const uint32_t rl = uni32(A.pk[hdr]);
+          if (hdr + 1 + (uint64_t)rl > A.pool_cap) {  // uniform
+            if (tid == 0) { S.s_ok = 0; atomicOr(A.err, kGiErrBounds); }
+            __syncthreads();
+            break;
+          }
           if (rl > kGhRhsMax || live - 1 + rl > kGhRowMax) {  // could pass the table: the rest on one lane
-            if (tid == 0) { S.s_o = pool_alloc(A, al0, live); if (S.s_o == RS_NONE) S.s_ok = 0; }
+            if (tid == 0) { S.s_o = gi_alloc(A, al0, live); if (S.s_o == RS_NONE) S.s_ok = 0; }
             __syncthreads();
             if (S.s_ok) {
               const uint64_t o = S.s_o;
               if (wsd && wk < kGhTomb) {
                 const uint32_t r = gh_rank(S, wk);
-                A.pk[o + r] = wk;
-                A.pv[o + r] = wv;
+                if (r < live) {
+                  A.pk[o + r] = wk;
+                  A.pv[o + r] = wv;
+                } else {
+                  atomicOr(A.err, kGiErrBounds);
+                }
               }
               __syncthreads();
               if (tid == 0) {
                 uint32_t m = S.s_m, nl = S.s_nl;
-                if (!d_gi_serial(A, G, al0, sub_base, left_base, qi, A.pk + o, A.pv + o, live, m, nl, p4, by)) S.s_ok = 0;
+                if (!d_gi_serial(A, G, al0, sub_base, left_base, qi, A.pk + o, A.pv + o, live, m, nl, p4, by, e)) S.s_ok = 0;
                 S.s_m = m;
                 S.s_nl = nl;
               }
@@ -526,8 +575,12 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
             __syncthreads();
             if (wsd && wk < kGhTomb) {
               const uint32_t at = gh_claim(S, wk);
-              S.tv[at] = wv;
-              S.ts[at] = wst;
+              if (at != kGhEmpty) {
+                S.tv[at] = wv;
+                S.ts[at] = wst;
+              } else {
+                atomicOr(A.err, kGiErrBounds);
+              }
             }
             __syncthreads();
             if (wsd) {
@@ -558,8 +611,12 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
                 S.sj[at] = jj + 1;
               } else if (!fe_is_zero(Rj)) {  // a zero-valued RHS key ({0: 0}) only ever adds into the row
                 const uint32_t f = gh_claim(S, Kj);
-                S.ts[f] = st_r;
-                S.sj[f] = jj + 1;
+                if (f != kGhEmpty) {
+                  S.ts[f] = st_r;
+                  S.sj[f] = jj + 1;
+                } else {
+                  atomicOr(A.err, kGiErrBounds);
+                }
               }
             }
           } else if (wk < kGhTomb && slot != ps) {
@@ -614,14 +671,22 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
         }
         if (ps == kGhEmpty) {  // no takeable key: a leftover, unnormalised (:325-327)
           by += 36ull * live;
-          if (tid == 0) { S.s_o = pool_alloc(A, al0, live); if (S.s_o == RS_NONE) S.s_ok = 0; }
+          if (tid == 0) {
+            S.s_o = left_base + S.s_nl < e ? gi_alloc(A, al0, live) : RS_NONE;
+            if (S.s_o == RS_NONE) S.s_ok = 0;
+            if (left_base + S.s_nl >= e) atomicOr(A.err, kGiErrBounds);
+          }
           __syncthreads();
           if (S.s_ok) {
             const uint64_t o = S.s_o;
             if (wsd && wk < kGhTomb) {
               const uint32_t r = gh_rank(S, wk);
-              A.pk[o + r] = wk;
-              A.pv[o + r] = wv;
+              if (r < live) {
+                A.pk[o + r] = wk;
+                A.pv[o + r] = wv;
+              } else {
+                atomicOr(A.err, kGiErrBounds);
+              }
             }
             if (tid == 0) {
               A.l_off[left_base + S.s_nl] = o;
@@ -634,14 +699,22 @@ __global__ __launch_bounds__(kGhThreads) void k_gi_loop(ElimArgs A, GiantArgs G,
           const uint32_t sh = has0 ? 0u : 1u;  // {0: 0} is inserted when absent
           const uint32_t mm = live - 1 + sh;
           by += 36ull * mm;
-          if (tid == 0) { S.s_o = pool_alloc(A, al0, (uint64_t)mm + 1); if (S.s_o == RS_NONE) S.s_ok = 0; }
+          if (tid == 0) {
+            S.s_o = sub_base + S.s_m < e ? gi_alloc(A, al0, (uint64_t)mm + 1) : RS_NONE;
+            if (S.s_o == RS_NONE) S.s_ok = 0;
+            if (sub_base + S.s_m >= e) atomicOr(A.err, kGiErrBounds);
+          }
           __syncthreads();
           if (S.s_ok) {
             const uint64_t o = S.s_o;
             if (wsd && wk < kGhTomb && slot != ps) {
               const uint32_t r = gh_rank(S, wk) - (kp < wk ? 1u : 0u);
-              A.pk[o + 1 + sh + r] = wk;
-              A.pv[o + 1 + sh + r] = wv;
+              if (sh + r < mm) {
+                A.pk[o + 1 + sh + r] = wk;
+                A.pv[o + 1 + sh + r] = wv;
+              } else {
+                atomicOr(A.err, kGiErrBounds);
+              }
             }
             if (tid == 0) {
               const Fe cf = fneg(F, wpv);
@@ -704,6 +777,7 @@ __global__ void k_gi_gather(ElimArgs A, GiantArgs G, uint64_t c) {
     }
     if (li < G.c_nleft[k]) {
       const uint32_t qi = A.tmp[b + i];
+      if (qi >= n_loop) { atomicOr(A.err, kGiErrBounds); continue; }
       G.tl_off[qi] = A.l_off[b + i];
       G.tl_len[qi] = A.l_len[b + i];
       G.lmark[qi] = 1;

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RS_ABI_VERSION 8
+#define RS_ABI_VERSION 9
 
 enum rs_status {
   RS_OK = 0,
@@ -248,6 +248,10 @@ typedef struct rs_stats {
   double gather_ms;            /* the result's gathers: snapshots, late rows, the compact CSR */
   uint64_t gather_bytes;       /* 72 B an entry gathered (read + canonical write) + per-row selection */
   uint64_t gather_launches;
+  /* ABI 9: the host's share of the clustering (build_clusters): time the calling thread spent blocked
+   * in its read-backs and synchronisations and replaying the largest clusters' arena order, inside the
+   * span cluster_dev_ms brackets on the main stream */
+  double cluster_host_ms;
 } rs_stats;
 
 typedef struct rs_engine rs_engine;

@@ -1,10 +1,10 @@
-//! Raw bindings of `include/rs_simplify.h` (ABI 8), one item per C declaration, same order and
+//! Raw bindings of `include/rs_simplify.h` (ABI 9), one item per C declaration, same order and
 //! layout.  The safe wrapper a caller uses is `constraint_list_glue.rs` (the body that replaces
 //! `constraint_list::constraint_simplification::simplification`, constraint_simplification.rs:442).
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const RS_ABI_VERSION: c_int = 8;
+pub const RS_ABI_VERSION: c_int = 9;
 pub const RS_COMM_ID_BYTES: usize = 128;
 
 pub const RS_OK: c_int = 0;
@@ -217,6 +217,7 @@ pub struct rs_stats {
     pub gather_ms: f64,
     pub gather_bytes: u64,
     pub gather_launches: u64,
+    pub cluster_host_ms: f64,
 }
 
 #[repr(C)]

@@ -189,3 +189,28 @@ def test_hosthost_streamed_levels(level, rounds):
         got = rsio.output_arrays(engine().simplify(pin.c, fl))
         assert rsio.diff_output_arrays(got, ref) is None
     pin.free()
+
+
+def test_engine_calls_keep_caller_affinity():
+    """engine creation and calls run the calling thread on the GPU's NUMA-local CPUs only for
+    the duration of a call (threads the call starts inherit that); the caller's own mask is unchanged
+    after rs_engine_create and after every call, so a second engine (or a host thread pool created
+    later) is not narrowed by the first."""
+    import os
+    before = os.sched_getaffinity(0)  # pid 0: the calling thread's mask
+    e1, e2 = M.Engine(0), M.Engine(0)
+    try:
+        assert os.sched_getaffinity(0) == before
+        inp = M.Input.synth(0, 50_000, 5, "bn128")
+        fl = rsio.flags("O2")
+        got = rsio.output_arrays(e1.simplify(inp.c, fl))
+        assert os.sched_getaffinity(0) == before
+        e2.load(inp.c)
+        e2.run(fl)
+        assert rsio.diff_output_arrays(got, rsio.output_arrays(e2.fetch())) is None
+        assert os.sched_getaffinity(0) == before
+        inp.free()
+    finally:
+        e1.close()
+        e2.close()
+    assert os.sched_getaffinity(0) == before
