@@ -136,29 +136,58 @@ def kernel_profile():
     return rows, os.path.relpath(files[-1], ROOT)
 
 
-def link_probe(mib: int = 512):
+def link_probe(device: int, mib: int = 512):
     """The box's PCIe link between HBM and page-locked host memory: H2D and D2H of `mib` MiB in 32 MiB
-    chunks (the input's and the result stream's pattern), best of 3 each -- so a host -> host number can
-    be read against the link it ran on (torch tensors; freed before the measurement starts)."""
-    import torch
-    chunk = 32 << 20
-    dev = torch.empty(mib << 20, dtype=torch.uint8, device="cuda")
-    host = torch.empty(mib << 20, dtype=torch.uint8, pin_memory=True)
+    chunks on one stream (the input's and the result stream's pattern), best of 3 each -- so a host ->
+    host number can be read against the link it ran on.  Through the HIP runtime the library already
+    loaded (ctypes; no torch, whose bundled runtime would be a second one in the process)."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so.7")
+
+    def chk(rc, what):
+        if rc:
+            raise RuntimeError(f"{what}: hip error {rc}")
+    n, chunk = mib << 20, 32 << 20
+    dev, host, st = C.c_void_p(), C.c_void_p(), C.c_void_p()
+    chk(hip.hipSetDevice(device), "hipSetDevice")
+    chk(hip.hipMalloc(C.byref(dev), C.c_size_t(n)), "hipMalloc")
+    chk(hip.hipHostMalloc(C.byref(host), C.c_size_t(n), 0), "hipHostMalloc")
+    chk(hip.hipStreamCreateWithFlags(C.byref(st), 1), "hipStreamCreate")
     res = {}
-    for name, src, dst in (("h2d_GBps", host, dev), ("d2h_GBps", dev, host)):
-        best = 0.0
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for o in range(0, mib << 20, chunk):
-                dst[o:o + chunk].copy_(src[o:o + chunk], non_blocking=True)
-            torch.cuda.synchronize()
-            best = max(best, (mib << 20) / (time.perf_counter() - t0) / 1e9)
-        res[name] = round(best, 1)
-    del dev, host
-    torch.cuda.empty_cache()
-    res["what"] = f"{mib} MiB in 32 MiB chunks between HBM and pinned host memory, best of 3 (torch), before the timed region"
+    try:
+        for name, kind in (("h2d_GBps", 1), ("d2h_GBps", 2)):
+            best = 0.0
+            for _ in range(3):
+                chk(hip.hipStreamSynchronize(st), "sync")
+                t0 = time.perf_counter()
+                for o in range(0, n, chunk):
+                    d, h = C.c_void_p(dev.value + o), C.c_void_p(host.value + o)
+                    src, dst = (h, d) if kind == 1 else (d, h)
+                    chk(hip.hipMemcpyAsync(dst, src, C.c_size_t(min(chunk, n - o)), kind, st), "hipMemcpyAsync")
+                chk(hip.hipStreamSynchronize(st), "sync")
+                best = max(best, n / (time.perf_counter() - t0) / 1e9)
+            res[name] = round(best, 1)
+    finally:
+        hip.hipStreamDestroy(st)
+        hip.hipFree(dev)
+        hip.hipHostFree(host)
+    res["what"] = f"{mib} MiB in 32 MiB chunks between HBM and pinned host memory, best of 3, before the timed region"
     return res
+
+
+def hip_runtime():
+    """The HIP runtime and RCCL this process mapped (torch ships its own libamdhip64.so.7 with the same
+    SONAME: whichever loads first serves both; at N = 1 torch is not loaded)."""
+    libs = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for ln in f:
+                p = ln.split()[-1] if ln.strip() else ""
+                if any(x in p for x in ("libamdhip64", "librccl", "libhsa-runtime64")):
+                    libs.add(p)
+    except OSError:
+        pass
+    return sorted(libs)
 
 
 def pmc_traffic():
@@ -267,16 +296,22 @@ def timed_steps(eng, inp_c, fl, steps, barrier):
     barrier()
     t0 = time.perf_counter()
     out = None
+    per = {"step_ms": [], "cluster_ms": []}  # per-step spread (the line's value is total / K)
     for _ in range(steps):
+        ts = time.perf_counter()
         out = eng.simplify(inp_c, fl)
+        per["step_ms"].append((time.perf_counter() - ts) * 1000.0)
         st = eng.stats()
+        per["cluster_ms"].append(st.cluster_ms)
         for k, fm, fb, fn in KERNELS:
             acc[k][0] += getattr(st, fm)
             acc[k][1] += getattr(st, fb)
             acc[k][2] += getattr(st, fn)
         for k in tot:
-            tot[k] += getattr(st, k)
+            if k != "per_step":
+                tot[k] += getattr(st, k)
     barrier()
+    tot["per_step"] = per
     return time.perf_counter() - t0, acc, tot, out, eng.stats()
 
 
@@ -303,14 +338,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # N > 1: torch first.  torch bundles its own HIP runtime and RCCL; loaded first, the library binds to
+    # them (same SONAME), loaded after the library torch maps a second runtime beside /opt/rocm's and the
+    # two do not mix.  N = 1 needs no torch: the library runs on /opt/rocm's runtime, as under a Rust host.
     if world > 1:
         import torch
         import torch.distributed as dist_
         torch.cuda.set_device(local)
         dist_.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = dist_
-
     import circom_cvm_amd as M
+    M.abi.lib()
     sys.path.insert(0, os.path.join(ROOT, "tests"))
 
     def barrier():
@@ -323,7 +361,7 @@ def main():
     link = None
     if not args.no_link:
         try:
-            link = link_probe()
+            link = link_probe(local)
         except Exception as e:  # noqa: BLE001 -- a missing torch / device leaves the field out, not the bench
             link = {"error": str(e)[:200]}
     # ---- the headline: the metric circuit (ONE circuit over all ranks when N > 1), host -> host
@@ -513,8 +551,13 @@ def main():
         line["clustering"] = {"span_ms": round(acc["build_clusters (k_cl_*, pair sort, arena replays)"][0] / K, 3),
                               "host_wait_ms": round(tot["cluster_host_ms"] / K, 3),
                               "host_ms": round(tot["cluster_ms"] / K, 3)}
+        def spread(xs):
+            xs = sorted(xs)
+            return {"min": round(xs[0], 3), "median": round(xs[len(xs) // 2], 3), "max": round(xs[-1], 3)} if xs else None
+        line["per_step"] = {k: spread(v) for k, v in tot["per_step"].items()}
         if link is not None:
             line["link"] = link
+        line["hip_runtime"] = hip_runtime()
         if write is not None:
             line["write_r1cs"] = write
         if flat is not None:

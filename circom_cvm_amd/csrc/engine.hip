@@ -225,6 +225,7 @@ struct rs_engine {
   int device = 0;
   uint32_t n_cu = 256;  // compute units (resident grids)
   hipStream_t st = nullptr;
+  hipStream_t srd = nullptr;  // host reads (rd): non-blocking, from the pooled queues
   hipStream_t st2 = nullptr;  // the largest clusters' elimination chain runs here, beside the rest
   hipEvent_t evx[11] = {};    // [0] join-in, [1..4] head chain, [5] after the lane kernel, [6..7] the
                               // largest replays' fork / join, [8..9] the overlapped frames pass
@@ -609,6 +610,14 @@ static void load_abort(rs_engine *E) {
   if (E->comm) E->comm->fail();  // the other ranks leave their collectives with an error instead of waiting
 }
 
+// A synchronous device -> host read of data whose producers the caller has already synchronised, on the
+// engine's own non-blocking read stream (the engine's dedicated-queue streams block with the null
+// stream, which a plain hipMemcpy would use)
+static void rd(rs_engine *E, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return;
+  HC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, E->srd));
+  HC(hipStreamSynchronize(E->srd));
+}
 // H2D copy whose host buffer may be released right after the call: wait for it.
 static void h2d(rs_engine *E, void *dst, const void *src, size_t bytes) {
   if (!bytes) return;
@@ -2066,7 +2075,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
       E->stats.elim_big_ms += ms;  // wall of the workgroup kernels (both streams; the small ones run beside)
       E->stats.elim_small_ms += msm;
       unsigned long long b5[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      HC(hipMemcpy(b5, a.bytes, 64, hipMemcpyDeviceToHost));
+      rd(E, b5, a.bytes, 64);
       by = b5[0];
       E->stats.elim_kernel_ms += ms;
       E->stats.elim_kernel_launches++;
@@ -2096,7 +2105,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         E->stats.giant_ms += mg;
         E->stats.giant_launches++;
         uint32_t nmg = 0;
-        HC(hipMemcpy(&nmg, GA.scal + 5, 4, hipMemcpyDeviceToHost));
+        rd(E, &nmg, GA.scal + 5, 4);
         E->stats.giant_merges += nmg;
       }
       if (n_tail) {
@@ -4182,16 +4191,35 @@ int rs_engine_create(int device, rs_engine **eng) {
     E->near_n = near_gpu_cpus(device, &E->near_cpus);
     if (g_prof_env && E->near_n) fprintf(stderr, "[rs-prof] engine calls run on the GPU's %d local CPUs\n", E->near_n);
     E->n_cu = (uint32_t)prop.multiProcessorCount;
-    HC(hipStreamCreateWithFlags(&E->st, hipStreamNonBlocking));
+    // Streams and hardware queues.  HIP maps the normal-priority streams of a process round-robin onto
+    // a pool of GPU_MAX_HW_QUEUES (4) hardware queues, and two streams that share a queue execute in
+    // one order: a kernel on one waits for a barrier the other queued behind a copy.  Which engine
+    // stream shares the copy stream's queue depended on how many streams the process had created
+    // before the engine (tools/micro/qshare.hip on MI355X: none -> stg, one -> stx, two -> st), and with
+    // st there the whole clustering waits for the input's upload (the stc queue holds its check kernels
+    // behind the linear values' and the non-linear blocks' copies).  A stream with a CU mask gets a
+    // hardware queue of its own, so the copy stream -- the one stream whose kernels wait behind long
+    // copies -- is made with the full mask and shares its queue with nothing (RS_POOLED_STREAMS=1: a
+    // pooled one; RS_CUMASK_STREAMS=1: every normal-priority stream dedicated, measured no better).
+    // A CU-mask stream blocks with the null stream: nothing in a run uses it (E->srd takes host reads).
+    const bool pooled = getenv("RS_POOLED_STREAMS") != nullptr, all_masked = getenv("RS_CUMASK_STREAMS") != nullptr;
+    std::vector<uint32_t> cu_mask((E->n_cu + 31) / 32, 0u);
+    for (uint32_t c = 0; c < E->n_cu; ++c) cu_mask[c / 32] |= 1u << (c % 32);
+    auto mk_stream = [&](hipStream_t *sp, bool dedicated) {
+      if (pooled || !dedicated || hipExtStreamCreateWithCUMask(sp, (uint32_t)cu_mask.size(), cu_mask.data()) != hipSuccess)
+        HC(hipStreamCreateWithFlags(sp, hipStreamNonBlocking));
+    };
+    mk_stream(&E->st, all_masked);
+    HC(hipStreamCreateWithFlags(&E->srd, hipStreamNonBlocking));
     {  // the second stream carries the critical path (the largest clusters' chain): high priority
       int lo = 0, hi = 0;
       if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
           hipStreamCreateWithPriority(&E->st2, hipStreamNonBlocking, hi) != hipSuccess)
         HC(hipStreamCreateWithFlags(&E->st2, hipStreamNonBlocking));
     }
-    HC(hipStreamCreateWithFlags(&E->stc, hipStreamNonBlocking));
-    HC(hipStreamCreateWithFlags(&E->stx, hipStreamNonBlocking));
-    HC(hipStreamCreateWithFlags(&E->str, hipStreamNonBlocking));
+    mk_stream(&E->stc, true);
+    mk_stream(&E->stx, all_masked);
+    mk_stream(&E->str, all_masked);
     {  // the small clusters and the tail's second group: least priority, so the tail's first group (the
        // first frames pass's critical path) finds CUs before their wide finish does
       int lo = 0, hi = 0;
@@ -4200,7 +4228,7 @@ int rs_engine_create(int device, rs_engine **eng) {
         HC(hipStreamCreateWithFlags(&E->ste, hipStreamNonBlocking));
       if (g_prof_env) fprintf(stderr, "[rs-prof] stream priorities: least %d greatest %d\n", lo, hi);
     }
-    HC(hipStreamCreateWithFlags(&E->stg, hipStreamNonBlocking));
+    mk_stream(&E->stg, all_masked);
     for (auto &ev : E->evg) HC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     for (auto &g : E->evt)
       for (auto &ev : g) HC(hipEventCreate(&ev));
@@ -4266,6 +4294,7 @@ void rs_engine_destroy(rs_engine *E) {
   if (E->str) (void)hipStreamDestroy(E->str);
   if (E->ste) (void)hipStreamDestroy(E->ste);
   if (E->stg) (void)hipStreamDestroy(E->stg);
+  if (E->srd) (void)hipStreamDestroy(E->srd);
   for (auto &ev : E->evg)
     if (ev) (void)hipEventDestroy(ev);
   for (auto &g : E->evt)

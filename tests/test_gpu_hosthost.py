@@ -207,7 +207,7 @@ def test_engine_calls_keep_caller_affinity():
         assert os.sched_getaffinity(0) == before
         e2.load(inp.c)
         e2.run(fl)
-        assert rsio.diff_output_arrays(got, rsio.output_arrays(e2.fetch())) is None
+        assert rsio.diff_output_arrays(got, rsio.output_arrays(e2.fetch().c)) is None
         assert os.sched_getaffinity(0) == before
         inp.free()
     finally:

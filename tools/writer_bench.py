@@ -1,13 +1,49 @@
 """rs_engine_write_r1cs on the metric circuit's result: best of --reps writes into a temporary
-directory (RS_PROF=1 prints the device build / D2H + writers split)."""
+directory (RS_PROF=1 prints the device build / D2H + writers split), and the file system's own bound
+for a file of the same size written from host memory (no GPU): 1 and 4 pwrite threads in 32 MB chunks,
+with and without fallocate, in the same directory and in /dev/shm (tmpfs)."""
 import argparse
 import os
 import sys
 import tempfile
+import threading
 import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import circom_cvm_amd as M  # noqa: E402
+
+
+def fs_probe(dirname: str, size: int, threads: int, falloc: bool, reps: int = 3) -> float:
+    """GB/s of writing `size` bytes into a fresh file of `dirname` from a host buffer (best of reps)."""
+    chunk = 32 << 20
+    buf = bytearray(os.urandom(1 << 20)) * 32
+    mv = memoryview(buf)
+    best = 0.0
+    for _ in range(reps):
+        path = os.path.join(dirname, "probe.bin")
+        t0 = time.perf_counter()
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        if falloc:
+            os.posix_fallocate(fd, 0, size)
+        else:
+            os.ftruncate(fd, size)
+        offs = list(range(0, size, chunk))
+
+        def work(k):
+            for o in offs[k::threads]:
+                n = min(chunk, size - o)
+                os.pwrite(fd, mv[:n], o)
+        th = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        os.close(fd)
+        dt = time.perf_counter() - t0
+        os.unlink(path)
+        best = max(best, size / dt / 1e9)
+    return best
+
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=10_000_000)
@@ -28,5 +64,13 @@ with tempfile.TemporaryDirectory(dir=args.dir) as tmp:
         dt = (time.perf_counter() - t0) * 1000
         best = dt if best is None else min(best, dt)
     size = os.path.getsize(path)
-print(f"write_r1cs best {best:.1f} ms, {size / 1e6:.0f} MB, {size / best / 1e6:.2f} GB/s", flush=True)
+    os.unlink(path)
+    print(f"write_r1cs best {best:.1f} ms, {size / 1e6:.0f} MB, {size / best / 1e6:.2f} GB/s", flush=True)
+    for d in (tmp, "/dev/shm"):
+        for th, fa in ((1, False), (4, False), (4, True)):
+            try:
+                r = fs_probe(d, size, th, fa)
+                print(f"fs bound {d}: {th} writer(s){' + fallocate' if fa else ''}: {r:.2f} GB/s", flush=True)
+            except OSError as e:
+                print(f"fs bound {d}: {e}", flush=True)
 eng.close()
