@@ -167,6 +167,7 @@ SYMBOLS = [
     ("rs_engine_join_rccl", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     ("rs_group_create", C.c_void_p, [C.c_int]),
     ("rs_engine_join_group", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    ("rs_engine_join_host", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
     ("rs_group_destroy", None, [C.c_void_p]),
     ("rs_simplify_multi", C.c_int, [C.POINTER(RsInput), C.POINTER(RsFlags), C.c_int, C.POINTER(C.c_int),
                                     C.POINTER(C.POINTER(RsOutput))]),
@@ -276,6 +277,11 @@ class Engine:
 
     def join_group(self, group: Group, rank: int):
         check(lib().rs_engine_join_group(self._h, group._h, rank))
+
+    def join_host(self, world: int, rank: int, tag: str):
+        """Rank `rank` of a group of processes on one host (rs_engine_join_host: the test transport
+        whose collectives go through POSIX shared memory; collective, every rank passes `tag`)."""
+        check(lib().rs_engine_join_host(self._h, world, rank, tag.encode()))
 
     def load(self, inp: RsInput):
         check(lib().rs_engine_load(self._h, C.byref(inp)))

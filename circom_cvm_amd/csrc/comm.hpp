@@ -6,19 +6,25 @@
 // RHS offset/length, the leftovers, per cluster: #subs/#leftovers, and the pool entries those
 // offsets point at -- is then exchanged so every rank continues with the full map.
 //
-// Two transports behind one interface:
+// Three transports behind one interface:
 //   RcclComm  -- production: RCCL over xGMI, one communicator per engine, collectives on the
 //                engine's stream (allgatherv = grouped ncclBroadcast, one per root).
 //   LocalComm -- several engines in one process (threads; typically on ONE device): host-staged
 //                collectives behind a barrier.  It exists so the sharded path is testable on a
 //                one-GPU box, and it is what rs_simplify_multi uses when a device is listed twice.
+//   HostComm  -- one process per rank on one host (a test vehicle: RCCL refuses two ranks on one
+//                device): collectives staged through POSIX shared memory, a spin barrier in a shared
+//                control block; the shared result region is made by the same code as RcclComm's
+//                (shm_shared_host), so the multi-process result path runs on a one-GPU box.
 #pragma once
 
 #include <fcntl.h>
 #include <rccl/rccl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -70,6 +76,53 @@ struct ShmSeg {
   size_t cap = 0;
   bool registered = false;
 };
+static inline void shm_unmap(ShmSeg &g) {
+  if (!g.p) return;
+  if (g.registered) (void)hipHostUnregister(g.p);
+  munmap(g.p, g.cap);
+  g = ShmSeg{};
+}
+// The shared host region of a process-per-rank group (RcclComm, HostComm): collective; segment g grows
+// only (every rank passes the same size).  Rank 0 creates a POSIX shm object (name: a tag rank 0 chose,
+// sent with the first gather, the slot and a generation), every rank maps it and registers it with
+// HIP, and once every rank has it the name is unlinked.  nullptr (every rank alike) if any rank failed.
+static inline void *shm_shared_host(Comm &cm, ShmSeg &g, uint64_t &tag, uint64_t &gen, int slot, size_t bytes, hipStream_t st) {
+  if (g.p && g.cap >= bytes) return g.p;
+  if (!tag) tag = cm.gather_u64(cm.rank == 0 ? ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)&cm : 0, st)[0] | 1;
+  const size_t cap = std::max(bytes, g.cap + g.cap / 4);
+  shm_unmap(g);
+  char name[96];
+  snprintf(name, sizeof name, "/rs_simplify_%llx_%d_%llu", (unsigned long long)tag, slot, (unsigned long long)++gen);
+  int ok = 1;
+  if (cm.rank == 0) {
+    const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    ok = fd >= 0 && ftruncate(fd, (off_t)cap) == 0;
+    if (fd >= 0) close(fd);
+  }
+  ok = (int)cm.max_u64(ok ? 0 : 1, st) == 0;  // rank 0 created it (also the barrier before the opens)
+  void *p = MAP_FAILED;
+  if (ok) {
+    const int fd = shm_open(name, O_RDWR, 0600);
+    if (fd >= 0) {
+      p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      close(fd);
+    }
+  }
+  const bool mine = p != MAP_FAILED && hipHostRegister(p, cap, hipHostRegisterDefault) == hipSuccess;
+  ok = (int)cm.max_u64(mine ? 0 : 1, st) == 0;  // every rank mapped it: the name can go
+  if (cm.rank == 0) shm_unlink(name);
+  if (p != MAP_FAILED) {
+    g.p = p;
+    g.cap = cap;
+    g.registered = mine;
+  }
+  if (!ok) {
+    shm_unmap(g);
+    return nullptr;
+  }
+  return g.p;
+}
+
 struct RcclComm : Comm {
   ncclComm_t c = nullptr;
   uint64_t *d_scalar = nullptr;  // W u64 of device scratch for the scalar collectives
@@ -81,52 +134,12 @@ struct RcclComm : Comm {
     HC(hipMalloc((void **)&d_scalar, 8 * (size_t)w));
   }
   ~RcclComm() override {
-    for (ShmSeg &g : shm) unmap(g);
+    for (ShmSeg &g : shm) shm_unmap(g);
     if (d_scalar) (void)hipFree(d_scalar);
     if (c) (void)ncclCommDestroy(c);
   }
-  static void unmap(ShmSeg &g) {
-    if (!g.p) return;
-    if (g.registered) (void)hipHostUnregister(g.p);
-    munmap(g.p, g.cap);
-    g = ShmSeg{};
-  }
   void *shared_host(int slot, size_t bytes, hipStream_t st) override {
-    ShmSeg &g = shm[slot];
-    if (g.p && g.cap >= bytes) return g.p;
-    if (!shm_tag) shm_tag = gather_u64(rank == 0 ? ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)this : 0, st)[0] | 1;
-    const size_t cap = std::max(bytes, g.cap + g.cap / 4);
-    unmap(g);
-    char name[96];
-    snprintf(name, sizeof name, "/rs_simplify_%llx_%d_%llu", (unsigned long long)shm_tag, slot, (unsigned long long)++shm_gen);
-    int ok = 1;
-    if (rank == 0) {
-      const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
-      ok = fd >= 0 && ftruncate(fd, (off_t)cap) == 0;
-      if (fd >= 0) close(fd);
-    }
-    ok = (int)max_u64(ok ? 0 : 1, st) == 0;  // rank 0 created it (also the barrier before the opens)
-    void *p = MAP_FAILED;
-    if (ok) {
-      const int fd = shm_open(name, O_RDWR, 0600);
-      if (fd >= 0) {
-        p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-        close(fd);
-      }
-    }
-    const bool mine = p != MAP_FAILED && hipHostRegister(p, cap, hipHostRegisterDefault) == hipSuccess;
-    ok = (int)max_u64(mine ? 0 : 1, st) == 0;  // every rank mapped it: the name can go
-    if (rank == 0) shm_unlink(name);
-    if (p != MAP_FAILED) {
-      g.p = p;
-      g.cap = cap;
-      g.registered = mine;
-    }
-    if (!ok) {
-      unmap(g);
-      return nullptr;
-    }
-    return g.p;
+    return shm_shared_host(*this, shm[slot], shm_tag, shm_gen, slot, bytes, st);
   }
   void allgatherv(const void *send, void *recv, const std::vector<uint64_t> &counts, hipStream_t st) override {
     uint64_t off = 0;
@@ -158,6 +171,137 @@ struct RcclComm : Comm {
     HC(hipMemcpyAsync(r.data(), d_scalar, 8 * (size_t)world, hipMemcpyDeviceToHost, st));
     HC(hipStreamSynchronize(st));
     return r;
+  }
+};
+
+// ------------------------------------------------------------------ processes of one host (tests)
+// The control block every rank maps: a generation-counting spin barrier, one u64 per rank for the
+// scalar collectives, and a failure flag that releases the waiting ranks (RS_E_RCCL).
+struct HostCtl {
+  std::atomic<uint32_t> joined;
+  std::atomic<uint32_t> failed;
+  std::atomic<uint64_t> arrived;
+  std::atomic<uint64_t> gen;
+  uint64_t slot[256];
+};
+struct HostComm : Comm {
+  HostCtl *ctl = nullptr;
+  ShmSeg shm[4], stage;  // the result regions (slots) and the collectives' staging region
+  uint64_t shm_tag = 0, shm_gen = 0;
+  // every rank passes the same tag; rank 0 creates the control block, the others open it (up to 60 s)
+  HostComm(int w, int r, const char *tag) {
+    rank = r;
+    world = w;
+    char name[160];
+    snprintf(name, sizeof name, "/rs_hostcomm_%.120s", tag);
+    int fd = -1;
+    if (r == 0) {
+      shm_unlink(name);  // a crashed earlier run's object
+      fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd >= 0 && ftruncate(fd, sizeof(HostCtl)) != 0) { close(fd); fd = -1; }
+    } else {
+      for (int i = 0; i < 60000 && fd < 0; ++i) {
+        fd = shm_open(name, O_RDWR, 0600);
+        if (fd < 0) usleep(1000);
+        else {
+          struct stat sb;
+          if (fstat(fd, &sb) != 0 || (size_t)sb.st_size < sizeof(HostCtl)) { close(fd); fd = -1; usleep(1000); }
+        }
+      }
+    }
+    if (fd < 0) throw RsError(RS_E_RCCL, std::string("host transport: cannot open ") + name);
+    void *p = mmap(nullptr, sizeof(HostCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw RsError(RS_E_RCCL, "host transport: mmap");
+    ctl = (HostCtl *)p;  // a fresh object is zero-filled: counters at 0
+    ctl->joined.fetch_add(1);
+    for (int i = 0; i < 600000 && ctl->joined.load() < (uint32_t)w; ++i) usleep(100);
+    if (ctl->joined.load() < (uint32_t)w) throw RsError(RS_E_RCCL, "host transport: the other ranks did not join");
+    wait_all();
+    if (r == 0) shm_unlink(name);  // every rank has it mapped
+  }
+  ~HostComm() override {
+    for (ShmSeg &g : shm) shm_unmap(g);
+    shm_unmap(stage);
+    if (ctl) munmap(ctl, sizeof(HostCtl));
+  }
+  // the spin barrier (generation counting); a rank's failure releases the others with an error
+  void wait_all() {
+    const uint64_t g = ctl->gen.load();
+    if (ctl->arrived.fetch_add(1) + 1 == (uint64_t)world) {
+      ctl->arrived.store(0);
+      ctl->gen.fetch_add(1);
+      return;
+    }
+    for (uint64_t i = 0; ctl->gen.load() == g; ++i) {
+      if (ctl->failed.load()) throw RsError(RS_E_RCCL, "another rank of the host group failed");
+      if (i > 64) usleep(20);
+      if (i > 64 + 10000000ull) throw RsError(RS_E_RCCL, "host transport: barrier timed out");
+    }
+  }
+  void fail() override { if (ctl) ctl->failed.store(1); }
+  std::vector<uint64_t> gather_u64(uint64_t v, hipStream_t) override {
+    ctl->slot[rank] = v;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    wait_all();
+    std::vector<uint64_t> r(world);
+    for (int q = 0; q < world; ++q) r[q] = ((volatile uint64_t *)ctl->slot)[q];
+    wait_all();  // the slots may be rewritten only after every rank has read them
+    return r;
+  }
+  uint64_t max_u64(uint64_t v, hipStream_t st) override {
+    uint64_t m = 0;
+    for (uint64_t x : gather_u64(v, st)) m = std::max(m, x);
+    return m;
+  }
+  void barrier(hipStream_t st) override {
+    HC(hipStreamSynchronize(st));
+    wait_all();
+  }
+  void *shared_host(int slot, size_t bytes, hipStream_t st) override {
+    return shm_shared_host(*this, shm[slot], shm_tag, shm_gen, slot, bytes, st);
+  }
+  // every rank's block through the staging region: each copies its own in, every rank copies all out
+  void allgatherv(const void *send, void *recv, const std::vector<uint64_t> &counts, hipStream_t st) override {
+    uint64_t tot = 0, mine = 0;
+    for (int q = 0; q < world; ++q) {
+      if (q == rank) mine = tot;
+      tot += counts[q];
+    }
+    if (!tot) return;
+    uint8_t *h = (uint8_t *)shm_shared_host(*this, stage, shm_tag, shm_gen, 4, tot, st);
+    if (!h) throw RsError(RS_E_RCCL, "host transport: no staging region");
+    if (counts[rank]) HC(hipMemcpyAsync(h + mine, send, counts[rank], hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    wait_all();
+    uint64_t off = 0;
+    for (int q = 0; q < world; ++q) {
+      const bool in_place = q == rank && send == (const void *)((uint8_t *)recv + off);
+      if (counts[q] && !in_place) HC(hipMemcpyAsync((uint8_t *)recv + off, h + off, counts[q], hipMemcpyHostToDevice, st));
+      off += counts[q];
+    }
+    HC(hipStreamSynchronize(st));
+    wait_all();  // the region may be reused only after every rank has read it
+  }
+  void allreduce_sum(void *buf, uint64_t n, int elem_bytes, hipStream_t st) override {
+    if (!n) return;
+    const uint64_t nb = n * (uint64_t)elem_bytes;
+    uint8_t *h = (uint8_t *)shm_shared_host(*this, stage, shm_tag, shm_gen, 4, nb * (uint64_t)world, st);
+    if (!h) throw RsError(RS_E_RCCL, "host transport: no staging region");
+    HC(hipMemcpyAsync(h + nb * rank, buf, nb, hipMemcpyDeviceToHost, st));
+    HC(hipStreamSynchronize(st));
+    wait_all();
+    std::vector<uint8_t> acc(h, h + nb);
+    for (int q = 1; q < world; ++q) {
+      const uint8_t *b = h + nb * q;
+      if (elem_bytes == 8)
+        for (uint64_t i = 0; i < n; ++i) ((uint64_t *)acc.data())[i] += ((const uint64_t *)b)[i];
+      else
+        for (uint64_t i = 0; i < n; ++i) ((uint32_t *)acc.data())[i] += ((const uint32_t *)b)[i];
+    }
+    HC(hipMemcpyAsync(buf, acc.data(), nb, hipMemcpyHostToDevice, st));
+    HC(hipStreamSynchronize(st));
+    wait_all();
   }
 };
 

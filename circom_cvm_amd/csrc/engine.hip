@@ -4909,6 +4909,21 @@ int rs_engine_join_rccl(rs_engine *E, int world, int rank, const uint8_t id[RS_C
   }
 }
 
+int rs_engine_join_host(rs_engine *E, int world, int rank, const char *tag) {
+  try {
+    if (!E || !tag || world < 1 || world > 255 || rank < 0 || rank >= world) { set_error("bad world/rank/tag"); return RS_E_INVALID; }
+    HC(hipSetDevice(E->device));
+    E->comm.reset(new HostComm(world, rank, tag));
+    return RS_OK;
+  } catch (const RsError &e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::exception &e) {
+    set_error(e.what());
+    return RS_E_INTERNAL;
+  }
+}
+
 int rs_engine_inject_fault(rs_engine *E, int where) {
   if (!E || where < 0 || where > 1) { set_error("rs_engine_inject_fault: bad argument"); return RS_E_INVALID; }
   E->fault_at = where;

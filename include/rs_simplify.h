@@ -321,6 +321,12 @@ rs_group *rs_group_create(int world);
 int rs_engine_join_group(rs_engine *eng, rs_group *g, int rank);
 void rs_group_destroy(rs_group *g);
 int rs_simplify_multi(const rs_input *in, const rs_flags *fl, int n_devices, const int *devices, rs_output **out);
+/* ABI 9, a test transport: the ranks are processes of one host (e.g. two processes on ONE GPU, where RCCL
+ * refuses a second rank), their collectives staged through POSIX shared memory; every rank passes the
+ * same `tag` (a name for the group's control block).  The shared result region is made exactly as for
+ * RCCL ranks, so the one-GPU box runs the multi-process result path (shared host memory mapped and
+ * registered by every process, each rank's share streamed into it). */
+int rs_engine_join_host(rs_engine *eng, int world, int rank, const char *tag);
 
 /* Fault injection (tests; SURVEY 5 "failure detection / fault injection"): the engine's next
  * rs_engine_run / rs_engine_simplify fails with RS_E_INTERNAL at `where` (1: the start of the first

@@ -250,6 +250,8 @@ extern "C" {
     pub fn rs_engine_join_group(eng: *mut rs_engine, g: *mut rs_group, rank: c_int) -> c_int;
     pub fn rs_group_destroy(g: *mut rs_group);
     pub fn rs_simplify_multi(inp: *const rs_input, fl: *const rs_flags, n_devices: c_int, devices: *const c_int, out: *mut *mut rs_output) -> c_int;
+    /// Test transport: the ranks are processes of one host, collectives through POSIX shared memory.
+    pub fn rs_engine_join_host(eng: *mut rs_engine, world: c_int, rank: c_int, tag: *const c_char) -> c_int;
     /// Fault injection (tests): the engine's next run fails with RS_E_INTERNAL at `where_`.
     pub fn rs_engine_inject_fault(eng: *mut rs_engine, where_: c_int) -> c_int;
     pub fn rs_read_r1cs_o0(path: *const c_char, inp: *mut *mut rs_input) -> c_int;

@@ -363,3 +363,32 @@ if __name__ == "__main__":
     import sys
     if sys.argv[1:2] == ["20m"]:
         _run_20m(int(sys.argv[2]) if len(sys.argv) > 2 else 4)
+
+
+@pytest.mark.parametrize("kind,rows,world", [(0, 300_000, 2), (5, 200_000, 2), (2, 60_000, 3)])
+def test_two_process_host_transport(kind, rows, world):
+    """the multi-process path -- one process per rank, the shared result region created by
+    rank 0 as a POSIX shm object, mapped and hipHostRegister'ed by every process, each rank's share of
+    the result streamed into it -- run for real on one GPU: `world` processes on device 0 joined by the
+    host transport (rs_engine_join_host; RCCL refuses two ranks on one device, so its collectives go
+    through shared memory), host -> host three times and load/run/fetch once, every rank's view equal to
+    the oracle's."""
+    import os
+    import subprocess
+    import sys
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hostcomm_child.py")
+    tag = f"t{os.getpid()}_{kind}_{rows}_{world}"
+    procs = [subprocess.Popen([sys.executable, "-u", child, str(world), str(r), tag, str(kind), str(rows), "3"],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=240)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{out[-3000:]}"
+        assert f"rank {r} ok" in out
