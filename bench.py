@@ -175,6 +175,28 @@ def link_probe(device: int, mib: int = 512):
     return res
 
 
+def fs_write_bound(dirname: str, size: int, reps: int = 2) -> float:
+    """GB/s of the file system under `dirname` for a fresh file of `size` bytes written from host memory
+    (32 MB pwrites after fallocate, one writer, best of reps): the bound the .r1cs writer is held to."""
+    chunk = 32 << 20
+    mv = memoryview(bytearray(os.urandom(1 << 20)) * 32)
+    best = 0.0
+    for k in range(reps):
+        path = os.path.join(dirname, f"fs_probe{k}.bin")
+        t0 = time.perf_counter()
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        try:
+            os.posix_fallocate(fd, 0, size)
+        except OSError:
+            os.ftruncate(fd, size)
+        for o in range(0, size, chunk):
+            os.pwrite(fd, mv[:min(chunk, size - o)], o)
+        os.close(fd)
+        best = max(best, size / (time.perf_counter() - t0) / 1e9)
+        os.unlink(path)
+    return best
+
+
 def hip_runtime():
     """The HIP runtime and RCCL this process mapped (torch ships its own libamdhip64.so.7 with the same
     SONAME: whichever loads first serves both; at N = 1 torch is not loaded)."""
@@ -386,9 +408,14 @@ def main():
         with tempfile.TemporaryDirectory() as tmp:
             path = os.path.join(tmp, "bench_O2.r1cs")
             ms_w = eng.write_r1cs(path)
-            write = {"ms": round(ms_w, 2), "bytes": os.path.getsize(path),
+            nb = os.path.getsize(path)
+            os.unlink(path)
+            fsb = fs_write_bound(tmp, nb)
+            write = {"ms": round(ms_w, 2), "bytes": nb, "GBps": round(nb / ms_w / 1e6, 2),
+                     "fs_bound_GBps": round(fsb, 2), "of_fs_bound": round(nb / ms_w / 1e6 / max(fsb, 1e-9), 3),
                      "what": "rs_engine_write_r1cs: the last step's result as a .r1cs file (constraint section "
-                             "built on the device, streamed to a file in a temporary directory)"}
+                             "built on the device, streamed to a fresh file in a temporary directory); fs_bound: the "
+                             "same number of bytes written from host memory into a fresh file there (no GPU)"}
     # the DAG flattening that produces such an input, timed on its own
     flat = flatten_bench(args.seed, args.prime) if rank == 0 and not args.no_flatten else None
     # SURVEY 8(d) config 5's template replication (64-row instances sharing coefficients, wired

@@ -13,11 +13,23 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import circom_cvm_amd as M  # noqa: E402
 
 
-def fs_probe(dirname: str, size: int, threads: int, falloc: bool, reps: int = 3) -> float:
-    """GB/s of writing `size` bytes into a fresh file of `dirname` from a host buffer (best of reps)."""
+def pinned_buffer(nbytes: int):
+    """A page-locked buffer from the HIP runtime the library loaded (hipHostMalloc), as a memoryview."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so.7")
+    p = C.c_void_p()
+    if hip.hipHostMalloc(C.byref(p), C.c_size_t(nbytes), 0):
+        raise OSError("hipHostMalloc failed")
+    buf = (C.c_uint8 * nbytes).from_address(p.value)
+    C.memset(p, 7, nbytes)
+    return memoryview(buf).cast("B")
+
+
+def fs_probe(dirname: str, size: int, threads: int, falloc: bool, reps: int = 3, pinned: bool = False) -> float:
+    """GB/s of writing `size` bytes into a fresh file of `dirname` from a host buffer (best of reps);
+    pinned: the source is page-locked memory from hipHostMalloc (the writer's staging buffers)."""
     chunk = 32 << 20
-    buf = bytearray(os.urandom(1 << 20)) * 32
-    mv = memoryview(buf)
+    mv = pinned_buffer(chunk) if pinned else memoryview(bytearray(os.urandom(1 << 20)) * 32)
     best = 0.0
     for _ in range(reps):
         path = os.path.join(dirname, "probe.bin")
@@ -67,10 +79,11 @@ with tempfile.TemporaryDirectory(dir=args.dir) as tmp:
     os.unlink(path)
     print(f"write_r1cs best {best:.1f} ms, {size / 1e6:.0f} MB, {size / best / 1e6:.2f} GB/s", flush=True)
     for d in (tmp, "/dev/shm"):
-        for th, fa in ((1, False), (4, False), (4, True)):
+        for th, fa, pn in ((1, False, False), (4, False, False), (4, True, False), (1, False, True), (4, True, True)):
             try:
-                r = fs_probe(d, size, th, fa)
-                print(f"fs bound {d}: {th} writer(s){' + fallocate' if fa else ''}: {r:.2f} GB/s", flush=True)
+                r = fs_probe(d, size, th, fa, pinned=pn)
+                print(f"fs bound {d}: {th} writer(s){' + fallocate' if fa else ''}{' from pinned memory' if pn else ''}: "
+                      f"{r:.2f} GB/s", flush=True)
             except OSError as e:
                 print(f"fs bound {d}: {e}", flush=True)
 eng.close()
