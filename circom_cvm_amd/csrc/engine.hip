@@ -2451,22 +2451,6 @@ static void debug_check_round(rs_engine *E, const RoundArgs &ra, uint64_t n, uin
 // 159.8-160.3 / 155.5-156.0 / 158.4 ms; chunks alternating over two streams -- two copy engines --
 // 49.0 vs 49.6 ms on the metric circuit but 164.9 vs 157.6 ms templated: the run's own copies wait
 // behind both engines)
-// The result stream's device -> host copy as a kernel writing page-locked host memory (RS_D2H_KERNEL=1):
-// 16-byte stores when both ends are 16-byte aligned, else 4-byte ones; a system-scope fence so the host
-// sees the bytes once the kernel has completed.
-__global__ __launch_bounds__(256) void k_copy_to_host(const uint8_t *src, uint8_t *dst, uint64_t n) {
-  const uint64_t t = gtid(), T = gstride();
-  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
-    const uint64_t n16 = n / 16;
-    for (uint64_t i = t; i < n16; i += T) reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
-    for (uint64_t i = 16 * n16 + t; i < n; i += T) dst[i] = src[i];
-  } else {
-    const uint64_t n4 = n / 4;
-    for (uint64_t i = t; i < n4; i += T) reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(src)[i];
-    for (uint64_t i = 4 * n4 + t; i < n; i += T) dst[i] = src[i];
-  }
-  __threadfence_system();
-}
 static void snap_join(rs_engine *E) {
   {
     std::lock_guard<std::mutex> lk(E->snap_m);
@@ -2512,12 +2496,7 @@ static void snap_start(rs_engine *E) {
       for (size_t o = 0; o < j.bytes; o += chunk, ++k) {
         const size_t n = std::min(chunk, j.bytes - o);
         if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
-        static const bool d2h_kernel = getenv("RS_D2H_KERNEL") != nullptr;
-        if (d2h_kernel && !(E->comm && E->comm->world > 1)) {
-          hipLaunchKernelGGL(k_copy_to_host, dim3(64), dim3(256), 0, E->stx, (const uint8_t *)j.src + o, (uint8_t *)j.dst + o, (uint64_t)n);
-          if (hipGetLastError() != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
-          if (hipEventRecord(E->ev_chunk[k & 1], E->stx) != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
-        } else if (hipMemcpyAsync((uint8_t *)j.dst + o, (const uint8_t *)j.src + o, n, hipMemcpyDeviceToHost, E->stx) != hipSuccess ||
+        if (hipMemcpyAsync((uint8_t *)j.dst + o, (const uint8_t *)j.src + o, n, hipMemcpyDeviceToHost, E->stx) != hipSuccess ||
             hipEventRecord(E->ev_chunk[k & 1], E->stx) != hipSuccess) {
           E->snap_rc = RS_E_HIP;
           break;
