@@ -354,6 +354,8 @@ def main():
     ap.add_argument("--no-o1", action="store_true", help="skip the --O1 extra (the metric circuit at circom's default level)")
     ap.add_argument("--no-linear1m", action="store_true", help="skip BASELINE configs[1] (1 M purely linear rows, one run)")
     ap.add_argument("--no-link", action="store_true", help="skip the PCIe link probe")
+    ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-resident extra (profiling passes: host -> host steps only)")
+    ap.add_argument("--no-write", action="store_true", help="skip the .r1cs writer extra")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,7 +405,7 @@ def main():
         got = rsio.output_arrays(out)  # copy of the last timed step's result (the view is reused)
     # the last result written as .r1cs by the device writer (8(d): write timed apart)
     write = None
-    if rank == 0:
+    if rank == 0 and not args.no_write:
         import tempfile
         with tempfile.TemporaryDirectory() as tmp:
             path = os.path.join(tmp, "bench_O2.r1cs")
@@ -472,13 +474,15 @@ def main():
             import rsio
             o1["_arrays"] = rsio.output_arrays(o1out)  # checked against the oracle below, then dropped
     # ---- extra: the same engine with the input resident in HBM (rs_engine_run only)
-    eng.load(pin.c)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.run(fl)
-    barrier()
-    dt_hbm, _ = reduce_over_ranks(dist, time.perf_counter() - t0, n_rows, "cuda")
+    dt_hbm = None
+    if not args.no_hbm:
+        eng.load(pin.c)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.run(fl)
+        barrier()
+        dt_hbm, _ = reduce_over_ranks(dist, time.perf_counter() - t0, n_rows, "cuda")
     eng.close()
     pin.free()
     # ---- extra at N > 1: independent circuits per rank (weak scaling, no data-path collective)
@@ -555,9 +559,9 @@ def main():
                           "d2h": round(tot["d2h_ms"] / K, 3), "host_total": round(tot["host_total_ms"] / K, 3)},
             "last_step": {k: round(getattr(last, k), 2) for k in
                           ("eq_ms", "cluster_ms", "elim_ms", "subst_ms", "final_ms", "rounds")},
-            "hbm_resident": {"value": round(n_rows * K / dt_hbm, 1), "unit": "constraints/s",
-                             "ms_per_step": round(dt_hbm * 1000.0 / K, 3),
-                             "what": "rs_engine_run: input already in HBM -> result in HBM (no PCIe)"},
+            "hbm_resident": None if dt_hbm is None else
+            {"value": round(n_rows * K / dt_hbm, 1), "unit": "constraints/s", "ms_per_step": round(dt_hbm * 1000.0 / K, 3),
+             "what": "rs_engine_run: input already in HBM -> result in HBM (no PCIe)"},
         }
         if prof_rows:
             # the same kernel in the committed rocprofv3 summary: its average launch and the roofline

@@ -6,8 +6,8 @@
 #   5. write-request sizes (TCC_EA0_WRREQ / _64B) of the same kernels
 #   6. FETCH_SIZE and WRITE_SIZE passes of the templated circuit (config_bench, one call)
 #   7. the counters' calibration on known byte counts in this library's access patterns (pmc_calib)
-# The metric PMC passes run `bench.py --steps 1 --warmup 0`: one timed step plus the HBM-resident leg's one
-# run, so a kernel's dispatch count there is twice its launches per step (pmc_traffic.py --steps 2).
+# The metric PMC passes run `bench.py --steps 1 --warmup 0 --no-hbm --no-write`: the one timed host -> host
+# step and nothing else, so a kernel's dispatch count there is its launches per step (pmc_traffic.py --steps 1).
 # Outputs land in gpurun_out/<tag>/; tools/pmc_calib.py and tools/pmc_traffic.py turn them into
 # profiles/<tag>_pmc_calib.json, <tag>_pmc_traffic.json and <tag>_templated_pmc_traffic.json on the CPU side.
 # usage: bash tools/profile_round.sh <tag>
@@ -16,7 +16,7 @@ TAG=${1:-round4}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --no-cpu --no-flatten --no-templated --no-o1 --no-linear1m"
+B="python3 bench.py --no-cpu --no-flatten --no-templated --no-o1 --no-linear1m --no-link"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- \
   $B --steps 5 --warmup 2 > $OUT/trace_bench.log 2>&1
 echo "trace done"
@@ -24,13 +24,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
   python3 tools/config_bench.py --reps 3 templated10M > $OUT/trace_tmpl.log 2>&1
 echo "templated trace done"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o f -- \
-  $B --steps 1 --warmup 0 > $OUT/pmc_fetch.log 2>&1
+  $B --steps 1 --warmup 0 --no-hbm --no-write > $OUT/pmc_fetch.log 2>&1
 echo "fetch done"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o w -- \
-  $B --steps 1 --warmup 0 > $OUT/pmc_write.log 2>&1
+  $B --steps 1 --warmup 0 --no-hbm --no-write > $OUT/pmc_write.log 2>&1
 echo "write done"
 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $OUT/pmc_wrreq -o q -- \
-  $B --steps 1 --warmup 0 > $OUT/pmc_wrreq.log 2>&1
+  $B --steps 1 --warmup 0 --no-hbm --no-write > $OUT/pmc_wrreq.log 2>&1
 echo "wrreq done"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_tfetch -o f -- \
   python3 tools/config_bench.py --reps 1 templated10M > $OUT/pmc_tfetch.log 2>&1
