@@ -2580,7 +2580,12 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     E->kg[g].n = 0;
     E->kg[g].bytes = 0;
   }
-  E->A.defer = false;  // an exchange a failed run left mid-way
+  if (E->A.defer || !E->A.graveyard.empty()) {  // an exchange a failed run left mid-way: its deferred frees
+    for (hipStream_t q : {E->st, E->st2, E->stc, E->ste, E->stg})  // (nothing still reads them)
+      if (q) (void)hipStreamSynchronize(q);
+    E->A.defer = false;
+    E->A.flush();
+  }
   double T0 = now_ms();
   bool apply_linear = !fl->flag_s;
   uint64_t no_rounds = fl->no_rounds;
@@ -4747,8 +4752,29 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
       if (E->n_wires) tail.insert(tail.end(), (const uint8_t *)hw2l.data(), (const uint8_t *)(hw2l.data() + E->n_wires));
       if (with_gates) tail.insert(tail.end(), gates.begin(), gates.end());
     }
-    const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (fd < 0) throw RsError(RS_E_INVALID, std::string("cannot write ") + path);
+    constexpr uint64_t kChunk = 32ull << 20;
+    constexpr int kBufs = 8, kThreads = 4;
+    const uint64_t nch = (dev_bytes + kChunk - 1) / kChunk;
+    // everything that can throw before the file exists: the pinned buffers, the events (a
+    // throw between open() and the guarded block leaked the fd or destroyed joinable threads)
+    uint8_t *pool = nch ? (uint8_t *)pin_get(E, 11, kBufs * kChunk) : nullptr;
+    struct Events {
+      hipEvent_t e[kBufs] = {};
+      ~Events() {
+        for (hipEvent_t x : e)
+          if (x) (void)hipEventDestroy(x);
+      }
+    } evs;
+    hipEvent_t *evb = evs.e;
+    for (int b = 0; b < kBufs; ++b) HC(hipEventCreateWithFlags(&evb[b], hipEventDisableTiming));
+    struct Fd {
+      int fd;
+      ~Fd() {
+        if (fd >= 0) close(fd);
+      }
+    } file{open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644)};
+    if (file.fd < 0) throw RsError(RS_E_INVALID, std::string("cannot write ") + path);
+    const int fd = file.fd;
     std::atomic<bool> io_err{false};
     auto pwrite_all = [&](const uint8_t *p, uint64_t len, uint64_t off) {
       while (len) {
@@ -4765,21 +4791,33 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
     if (posix_fallocate(fd, 0, (off_t)fsize) != 0 && ftruncate(fd, (off_t)fsize) != 0) io_err = true;
     pwrite_all(head.data(), head.size(), 0);
     pwrite_all(tail.data(), tail.size(), img_off + dev_bytes);
-    constexpr uint64_t kChunk = 32ull << 20;
-    constexpr int kBufs = 8, kThreads = 4;
-    const uint64_t nch = (dev_bytes + kChunk - 1) / kChunk;
-    uint8_t *pool = nch ? (uint8_t *)pin_get(E, 11, kBufs * kChunk) : nullptr;
-    hipEvent_t evb[kBufs];
-    for (int b = 0; b < kBufs; ++b) HC(hipEventCreateWithFlags(&evb[b], hipEventDisableTiming));
     std::mutex mu;
     std::condition_variable cv;
     std::deque<uint64_t> work;       // chunks whose D2H is enqueued
     std::vector<char> written(nch, 0);
-    uint64_t n_written = 0;
     bool closing = false;
-    std::vector<std::thread> th;
+    // the writer threads are joined on every way out of this scope (a throw included): closing drains
+    // them, and the guard lives after everything they reference
+    struct Writers {
+      std::vector<std::thread> th;
+      std::mutex &mu;
+      std::condition_variable &cv;
+      bool &closing;
+      std::deque<uint64_t> &work;
+      void stop(bool drop) {
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          closing = true;
+          if (drop) work.clear();
+        }
+        cv.notify_all();
+        for (auto &x : th)
+          if (x.joinable()) x.join();
+      }
+      ~Writers() { stop(true); }
+    } writers{{}, mu, cv, closing, work};
     for (int t = 0; t < kThreads && (uint64_t)t < nch; ++t)
-      th.emplace_back([&]() {
+      writers.th.emplace_back([&]() {
         for (;;) {
           uint64_t i;
           {
@@ -4795,46 +4833,27 @@ int rs_engine_write_r1cs(rs_engine *E, const char *path, const char *o0_r1cs) {
           {
             std::lock_guard<std::mutex> lk(mu);
             written[i] = 1;
-            ++n_written;
           }
           cv.notify_all();
         }
       });
     const uint8_t *src = (const uint8_t *)img;
-    try {
-      for (uint64_t i = 0; i < nch; ++i) {
-        if (i >= (uint64_t)kBufs) {  // the buffer's previous chunk is on disk
-          std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] { return written[i - kBufs] != 0; });
-        }
-        const uint64_t off = i * kChunk, len = std::min(kChunk, dev_bytes - off);
-        HC(hipMemcpyAsync(pool + (i % kBufs) * kChunk, src + off, len, hipMemcpyDeviceToHost, st));
-        HC(hipEventRecord(evb[i % kBufs], st));
-        {
-          std::lock_guard<std::mutex> lk(mu);
-          work.push_back(i);
-        }
-        cv.notify_all();
+    for (uint64_t i = 0; i < nch; ++i) {
+      if (i >= (uint64_t)kBufs) {  // the buffer's previous chunk is on disk
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return written[i - kBufs] != 0; });
       }
-    } catch (...) {
+      const uint64_t off = i * kChunk, len = std::min(kChunk, dev_bytes - off);
+      HC(hipMemcpyAsync(pool + (i % kBufs) * kChunk, src + off, len, hipMemcpyDeviceToHost, st));
+      HC(hipEventRecord(evb[i % kBufs], st));
       {
         std::lock_guard<std::mutex> lk(mu);
-        closing = true;
-        work.clear();
+        work.push_back(i);
       }
       cv.notify_all();
-      for (auto &x : th) x.join();
-      for (int b = 0; b < kBufs; ++b) (void)hipEventDestroy(evb[b]);
-      close(fd);
-      throw;
     }
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      closing = true;
-    }
-    cv.notify_all();
-    for (auto &x : th) x.join();
-    for (int b = 0; b < kBufs; ++b) (void)hipEventDestroy(evb[b]);
+    writers.stop(false);  // every chunk written
+    file.fd = -1;
     if (close(fd) != 0) io_err = true;
     if (io_err) throw RsError(RS_E_INVALID, "write error");
     if (g_prof_env)
