@@ -348,23 +348,6 @@ __device__ __forceinline__ uint32_t gh_rank(const GhSmem &S, uint32_t key) {
   }
   return r;
 }
-// min over the wave (every lane active), by DPP: quad swaps, half-row and row mirrors, then the row
-// broadcasts; lane 63 ends with the minimum.  The compiler's own lowering of a divergent LDS atomic
-// (one iteration per active lane) cost hundreds of cycles per merge.
-template <int ctrl, int rmask>
-__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
-  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, ctrl, rmask, 0xf, false);
-  return o < v ? o : v;
-}
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-  v = dpp_min_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
-  v = dpp_min_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
-  v = dpp_min_step<0x141, 0xf>(v);  // row_half_mirror
-  v = dpp_min_step<0x140, 0xf>(v);  // row_mirror
-  v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
-  v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
 // a slot wave's share of a pivot reduction into set q: the wave's candidate by DPP (take_signal_4:
 // the smallest deleted key; take_signal_3: the largest takeable key), written with its state and
 // value by the lane that holds it, so the decision needs one LDS round trip and no atomics

@@ -346,12 +346,8 @@ __device__ __forceinline__ void sp_reduce(const ElimArgs &A, SpecSmem<NW> &S, ui
         const bool tkb = s2 != kStForb;
         // p4: the smallest deleted key; p3: the largest takeable key, if deleted
         const bool c = p4 ? (tkb && (s2 & kStDel)) : tkb;
-        uint32_t kk = c ? key[e] : (p4 ? 0xffffffffu : 0u);
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-          const uint32_t o2 = (uint32_t)__shfl_xor((int)kk, d);
-          kk = p4 ? (o2 < kk ? o2 : kk) : (o2 > kk ? o2 : kk);
-        }
+        // p4: the wave minimum; p3: the maximum as the minimum of the complements (DPP, every lane active)
+        const uint32_t kk = p4 ? wave_min_u32(c ? key[e] : 0xffffffffu) : ~wave_min_u32(c ? ~key[e] : 0xffffffffu);
         const uint64_t own = __ballot(c && key[e] == kk);
         if (own && (p4 ? kk < cand || cand == RS_NONE : kk > cand || cand == RS_NONE)) {
           cand = kk;
@@ -494,13 +490,10 @@ __device__ __forceinline__ uint32_t sp_commit(const ElimArgs &A, SpecSmem<NW> &S
     }
   }
   uint32_t oi = RS_NONE;
-  if (p4) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      const unsigned long long w = __shfl_xor(best, d);
-      best = w < best ? w : best;
-    }
-    if (best != ~0ull) oi = 0xffffffffu - (uint32_t)(best & 0xffffffffu);
+  if (p4) {  // the minimum of (occurrences << 32 | ~index): the high words' minimum, then the low words' among it
+    const uint32_t mh = wave_min_u32((uint32_t)(best >> 32));
+    const uint32_t ml = wave_min_u32((uint32_t)(best >> 32) == mh ? (uint32_t)best : 0xffffffffu);
+    if (((unsigned long long)mh << 32 | ml) != ~0ull) oi = 0xffffffffu - ml;
   } else {
 #pragma unroll
     for (int e = 0; e < E; ++e)
