@@ -696,8 +696,7 @@ __device__ inline void fw_batch(const FrameWaveArgs &A, FwLds &L, uint32_t lane,
     const uint32_t g = 3 * lane;
     rmax = max((uint32_t)(L.g_e0[g + 1] - L.g_e0[g]), max((uint32_t)(L.g_e0[g + 2] - L.g_e0[g + 1]), (uint32_t)(L.g_e0[g + 3] - L.g_e0[g + 2])));
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d));
+  rmax = ~wave_min_u32(~rmax);  // the wave's maximum (DPP)
   if (rmax > kFwRunsRank) {
     uint32_t rounds = 0;
     while ((1u << rounds) < rmax) ++rounds;

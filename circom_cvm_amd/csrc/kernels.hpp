@@ -1630,13 +1630,10 @@ __device__ __forceinline__ void d_big_main_cluster(const ElimArgs &A, const uint
             } else if (dm) {
               oi = __ffsll((long long)dm) - 1;
             } else {
-              unsigned long long v = tk ? ((unsigned long long)(uint32_t)oc << 32) | (0xffffffffu - tid) : ~0ull;
-#pragma unroll
-              for (int d = 32; d >= 1; d >>= 1) {
-                unsigned long long w = __shfl_xor(v, d);
-                v = w < v ? w : v;
-              }
-              oi = 0xffffffffu - (uint32_t)(v & 0xffffffffu);
+              // min of (occurrences << 32 | ~index): the high words' DPP minimum, then the low words' among it
+              const uint32_t vh = tk ? (uint32_t)oc : 0xffffffffu, vl = tk ? 0xffffffffu - tid : 0xffffffffu;
+              const uint32_t mh = wave_min_u32(vh);
+              oi = 0xffffffffu - wave_min_u32(vh == mh ? vl : 0xffffffffu);
             }
             conflict = (dm >> oi) & 1ull;
             hs = __shfl(hsl, (int)oi);
