@@ -335,17 +335,19 @@ __global__ __launch_bounds__(64) void k_cl_replay_wave(const uint64_t *cl_off, c
 }
 
 // what the host replay of clusters ids[0..n) needs to fetch their pair streams: (first row, rows,
-// first pair, pairs, rows whose order matters) per cluster
+// first pair, pairs, rows whose order matters, the cluster) per cluster
+constexpr int kMetaW = 6;
 __global__ void k_replay_meta(const uint64_t *cl_off, const uint32_t *ids, uint64_t n, const uint64_t *q_off,
                               const uint32_t *n_ordered, uint64_t *meta) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
     const uint32_t c = ids[i];
     const uint64_t b = cl_off[c], e = cl_off[c + 1];
-    meta[5 * i] = b;
-    meta[5 * i + 1] = e - b;
-    meta[5 * i + 2] = q_off[b];
-    meta[5 * i + 3] = q_off[e] - q_off[b];
-    meta[5 * i + 4] = n_ordered[c];
+    meta[kMetaW * i] = b;
+    meta[kMetaW * i + 1] = e - b;
+    meta[kMetaW * i + 2] = q_off[b];
+    meta[kMetaW * i + 3] = q_off[e] - q_off[b];
+    meta[kMetaW * i + 4] = n_ordered[c];
+    meta[kMetaW * i + 5] = c;
   }
 }
 

@@ -1137,6 +1137,9 @@ struct DevClusters {
   // host copy of the sorted size keys of the kHeadLimit largest clusters (k_cl_sizekey: size in the
   // high word, inverted; the cluster index in the low word)
   std::vector<uint64_t> top_keys;
+  // clusters the host replay found order-free (every row consumed by the uniques phase, d_cl_order_free):
+  // no ordered loop at all, so a giant among them skips the giant path (it only sorted empty lists)
+  std::unordered_set<uint32_t> order_free;
   bool timed = false;  // evc[0..1] bracket the clustering kernels
   uint64_t alg = 0;    // their algorithmic bytes
 };
@@ -1356,11 +1359,11 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
     // its row order (d_cl_order_free), copied on the device; the rest are replayed on the host (their
     // offsets, pair streams and rows in one pinned staging block, the orders back from it)
     const uint64_t nh = hc[4];
-    uint64_t *d_meta = A.get<uint64_t>("cl.rmeta", 5 * nh);
+    uint64_t *d_meta = A.get<uint64_t>("cl.rmeta", kMetaW * nh);
     launch(E->str, k_replay_meta, nh, (const uint64_t *)D.cl_off, (const uint32_t *)(sorted + hc[3]), nh,
            (const uint64_t *)q_off, (const uint32_t *)n_ordered, d_meta);
-    uint64_t *meta = (uint64_t *)pin_get(E, 16, 40 * nh);
-    HC(hipMemcpyAsync(meta, d_meta, 40 * nh, hipMemcpyDeviceToHost, E->str));
+    uint64_t *meta = (uint64_t *)pin_get(E, 16, 8 * kMetaW * nh);
+    HC(hipMemcpyAsync(meta, d_meta, 8 * kMetaW * nh, hipMemcpyDeviceToHost, E->str));
     sync(E->str);
     mark("replay meta");
     HC(hipEventRecord(E->evx[6], st));
@@ -1368,14 +1371,15 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
     std::vector<uint64_t> todo;
     uint64_t tot_q = 0, tot_n = 0;
     for (uint64_t i = 0; i < nh; ++i) {
-      const uint64_t rb = meta[5 * i], qn = meta[5 * i + 1];
-      if (qn >= 350 && qn < 1000000 && !old_heur && meta[5 * i + 4] == 0) {  // d_cl_order_free
+      const uint64_t rb = meta[kMetaW * i], qn = meta[kMetaW * i + 1];
+      if (qn >= 350 && qn < 1000000 && !old_heur && meta[kMetaW * i + 4] == 0) {  // d_cl_order_free
+        D.order_free.insert((uint32_t)meta[kMetaW * i + 5]);
         HC(hipMemcpyAsync(D.perm + rb, srow + rb, 4 * qn, hipMemcpyDeviceToDevice, E->st2));
         continue;
       }
       todo.push_back(i);
       tot_n += qn;
-      tot_q += meta[5 * i + 3];
+      tot_q += meta[kMetaW * i + 3];
     }
     const uint64_t nt = todo.size();
     if (nt) {
@@ -1385,12 +1389,12 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
       uint32_t *hst = (uint32_t *)(qo + tot_n + nt), *hsrow = hst + tot_q, *hperm = hsrow + tot_n;
       std::vector<uint64_t> o_q(nt), o_n(nt), o_o(nt);
       for (uint64_t t = 0, oq = 0, on = 0, o = 0; t < nt; ++t) {
-        const uint64_t i = todo[t], rb = meta[5 * i], qn = meta[5 * i + 1], np = meta[5 * i + 3];
+        const uint64_t i = todo[t], rb = meta[kMetaW * i], qn = meta[kMetaW * i + 1], np = meta[kMetaW * i + 3];
         o_q[t] = oq;
         o_n[t] = on;
         o_o[t] = o;
         HC(hipMemcpyAsync(qo + o, q_off + rb, 8 * (qn + 1), hipMemcpyDeviceToHost, E->str));
-        if (np) HC(hipMemcpyAsync(hst + oq, stream + meta[5 * i + 2], 4 * np, hipMemcpyDeviceToHost, E->str));
+        if (np) HC(hipMemcpyAsync(hst + oq, stream + meta[kMetaW * i + 2], 4 * np, hipMemcpyDeviceToHost, E->str));
         HC(hipMemcpyAsync(hsrow + on, srow + rb, 4 * qn, hipMemcpyDeviceToHost, E->str));
         oq += np;
         on += qn;
@@ -1402,7 +1406,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
       auto work = [&] {  // a few host threads, largest cluster first (the list is size-ordered)
         for (uint64_t t; (t = next_t.fetch_add(1)) < nt;) {
           const uint64_t *qoi = qo + o_o[t], q0 = qoi[0];
-          const uint32_t n_i = (uint32_t)meta[5 * todo[t] + 1];
+          const uint32_t n_i = (uint32_t)meta[kMetaW * todo[t] + 1];
           std::vector<uint64_t> rel(n_i + 1);
           for (uint32_t k = 0; k <= n_i; ++k) rel[k] = qoi[k] - q0;
           host_replay(n_i, rel.data(), hst + o_q[t], hsrow + o_n[t], hperm + o_n[t]);
@@ -1419,7 +1423,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
       mark("replayed");
       for (uint64_t t = 0; t < nt; ++t) {
         const uint64_t i = todo[t];
-        HC(hipMemcpyAsync(D.perm + meta[5 * i], hperm + o_n[t], 4 * meta[5 * i + 1], hipMemcpyHostToDevice, E->st2));
+        HC(hipMemcpyAsync(D.perm + meta[kMetaW * i], hperm + o_n[t], 4 * meta[kMetaW * i + 1], hipMemcpyHostToDevice, E->st2));
       }
       sync(E->st2);  // the staging block is reused by the next round's replay
       mark("orders back");
@@ -1714,7 +1718,7 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     uint64_t giant_rows_sum = 0;
     for (uint64_t i = 0; i < std::min<uint64_t>(n_big, kHeadLimit) && i < D.top_keys.size(); ++i) {
       const uint64_t r = (0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull;
-      if (r >= kGiantRows) giant_rows_sum += r;
+      if (r >= kGiantRows && !D.order_free.count((uint32_t)(D.top_keys[i] & 0xffffffffull))) giant_rows_sum += r;
     }
     if (!getenv("RS_GI_NOPOOL")) want = std::max<uint64_t>(want, 192 * giant_rows_sum);
   }
@@ -1796,7 +1800,9 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
     // component loops of giant_loop.hpp on their own stream; k_big_spec skips them
     std::vector<uint64_t> giants;  // head positions
     for (uint64_t i = 0; i < n_head && i < D.top_keys.size(); ++i)
-      if (((0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull) >= kGiantRows) giants.push_back(i);
+      if (((0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull) >= kGiantRows &&
+          !D.order_free.count((uint32_t)(D.top_keys[i] & 0xffffffffull)))  // (an order-free one has no loop rows)
+        giants.push_back(i);
     uint64_t giant_rows = 0;
     for (uint64_t i : giants) giant_rows = std::max<uint64_t>(giant_rows, (0xffffffffull - (D.top_keys[i] >> 32)) & 0x7fffffffull);
     GiantArgs GA{};
