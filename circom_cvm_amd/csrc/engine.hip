@@ -1068,26 +1068,6 @@ static void fetch_pool_maps(rs_engine *E, const std::vector<uint64_t> &off, cons
 }
 
 // D2H keys of pool maps (no values)
-static void fetch_pool_keys(rs_engine *E, const std::vector<uint64_t> &off, const std::vector<uint32_t> &len,
-                            const uint32_t *pk, std::vector<uint32_t> &keys, std::vector<uint64_t> &optr) {
-  const uint64_t n = off.size();
-  optr.assign(n + 1, 0);
-  for (uint64_t i = 0; i < n; ++i) optr[i + 1] = optr[i] + len[i];
-  const uint64_t tot = optr[n];
-  keys.resize(tot);
-  if (tot == 0) return;
-  uint64_t *d_off = E->A.get<uint64_t>("fp.off", n);
-  uint32_t *d_len = E->A.get<uint32_t>("fp.len", n);
-  uint64_t *d_optr = E->A.get<uint64_t>("fp.optr", n + 1);
-  uint32_t *d_k = E->A.get<uint32_t>("fp.k", tot);
-  h2d(E, d_off, off.data(), 8 * n);
-  h2d(E, d_len, len.data(), 4 * n);
-  h2d(E, d_optr, optr.data(), 8 * (n + 1));
-  launch(E->st, k_pool_keys, 64 * n, (const uint64_t *)d_off, (const uint32_t *)d_len, (const uint64_t *)d_optr, n, pk, d_k);
-  HC(hipMemcpyAsync(keys.data(), d_k, 4 * tot, hipMemcpyDeviceToHost, E->st));
-  HC(hipStreamSynchronize(E->st));
-}
-
 static bool is_zero4(const uint64_t *v) { return (v[0] | v[1] | v[2] | v[3]) == 0; }
 
 
@@ -3820,15 +3800,30 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (another) {
         double Tq = now_ms();
         need_usig();
-        // this round's batch of appends: every substitution's `from` and RHS keys (no values)
+        // this round's batch of appends: every substitution's `from` and RHS keys (no values).  The
+        // keys are copied on the device now (the next round's elimination reuses the pool) and come to
+        // the host only if a later round resolves a list through this batch -- most never do (the
+        // templated circuit's round 2: 9.8 ms of D2H and host copies saved per call)
         MapLists::Batch B;
-        std::vector<uint64_t> uoff(nU);
-        std::vector<uint32_t> ulen(nU);
-        HC(hipMemcpyAsync(uoff.data(), d_uoff, 8 * nU, hipMemcpyDeviceToHost, st));
-        HC(hipMemcpyAsync(ulen.data(), d_ulen, 4 * nU, hipMemcpyDeviceToHost, st));
-        HC(hipStreamSynchronize(st));
-        fetch_pool_keys(E, uoff, ulen, P.pk, B.keys, B.ptr);
         B.from = usig;
+        const size_t bi = ML.batches.size();
+        const std::string bn = "ml." + std::to_string(bi);
+        uint64_t *d_optr = A.get<uint64_t>(bn + ".ptr", nU + 1);
+        uint64_t *d_len64 = A.get<uint64_t>(bn + ".len", nU + 1);
+        launch(st, k_u32_to_u64, nU, (const uint32_t *)d_ulen, d_len64, nU);
+        HC(hipMemsetAsync(d_len64 + nU, 0, 8, st));
+        const uint64_t tot = excl_scan_u64(E, d_len64, d_optr, nU + 1, "mlb");
+        uint32_t *d_keys = A.get<uint32_t>(bn + ".keys", std::max<uint64_t>(tot, 1));
+        if (tot)
+          launch(st, k_pool_keys, 64 * nU, (const uint64_t *)d_uoff, (const uint32_t *)d_ulen, (const uint64_t *)d_optr, nU,
+                 (const uint32_t *)P.pk, d_keys);
+        B.load = [E, d_optr, d_keys, nU, tot](MapLists::Batch &Bt) {
+          Bt.ptr.resize(nU + 1);
+          Bt.keys.resize(tot);
+          HC(hipMemcpyAsync(Bt.ptr.data(), d_optr, 8 * (nU + 1), hipMemcpyDeviceToHost, E->st));
+          if (tot) HC(hipMemcpyAsync(Bt.keys.data(), d_keys, 4 * tot, hipMemcpyDeviceToHost, E->st));
+          HC(hipStreamSynchronize(E->st));
+        };
         ML.add_batch(std::move(B));
         E->stats.map_ms += now_ms() - Tq;
       }

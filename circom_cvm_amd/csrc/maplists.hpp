@@ -31,6 +31,9 @@ struct MapLists {
   struct Batch {
     std::vector<uint32_t> from, keys;  // the round's ordered `from` list; RHS keys of substitution j
     std::vector<uint64_t> ptr;         // are keys[ptr[j], ptr[j + 1])
+    // keys / ptr may be fetched on first use (the engine keeps a device copy and most rounds' lists
+    // are never read); `load` fills them, once
+    std::function<void(Batch &)> load;
   };
   using Lists = std::unordered_map<uint32_t, std::vector<uint32_t>>;
   Lists minit;                  // initial lists (ascending storage rows), for the queried signals only
@@ -47,6 +50,11 @@ struct MapLists {
   const Lists &index(size_t bi) {
     if (bidx.size() < batches.size()) bidx.resize(batches.size());
     Lists &ix = bidx[bi];
+    if (batches[bi].load) {  // a lazily fetched batch: its keys now
+      auto ld = std::move(batches[bi].load);
+      batches[bi].load = nullptr;
+      ld(batches[bi]);
+    }
     if (ix.empty() && !batches[bi].keys.empty()) {
       const Batch &B = batches[bi];
       for (uint64_t j = 0; j < B.from.size(); ++j)
