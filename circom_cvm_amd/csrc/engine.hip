@@ -337,7 +337,7 @@ struct rs_engine {
   hipEvent_t evc[2] = {};
   hipEvent_t evgt[3] = {};
   hipEvent_t ev_sm[3] = {};   // its start / k_eliminate done / its work done (the tail's second group too)
-  hipEvent_t ev_chunk[2] = {};
+  hipEvent_t ev_chunk[8] = {};
   // rs_stats groups timed launch by launch: [0] input checks (copy stream), [1] ragged conversion and
   // the linear rows' frames, [2] result gathers (snapshots, late rows, the compact CSR)
   KGroup kg[3];
@@ -627,6 +627,7 @@ static void h2d(rs_engine *E, void *dst, const void *src, size_t bytes) {
 
 // ---------------------------------------------------------------- scans
 static void *pin_get(rs_engine *E, int slot, size_t bytes);
+constexpr size_t kPinRb = 128;  // pinned slot 18: small read-backs (one size everywhere: never reallocated)
 static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, uint64_t n, const char *tag,
                               double *waited = nullptr) {
   if (n == 0) return 0;
@@ -634,7 +635,7 @@ static uint64_t excl_scan_u64(rs_engine *E, const uint64_t *in, uint64_t *out, u
   HC(rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), E->st));
   void *tmp = E->A.get<uint8_t>(std::string("scan.tmp.") + tag, tb);
   HC(rocprim::exclusive_scan(tmp, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), E->st));
-  uint64_t *h = (uint64_t *)pin_get(E, 18, 64) + 4;  // pinned read-back words [4..5] (no staged copy)
+  uint64_t *h = (uint64_t *)pin_get(E, 18, kPinRb) + 4;  // pinned read-back words [4..5] (no staged copy)
   HC(hipMemcpyAsync(h, in + n - 1, 8, hipMemcpyDeviceToHost, E->st));
   HC(hipMemcpyAsync(h + 1, out + n - 1, 8, hipMemcpyDeviceToHost, E->st));
   const double t0 = waited ? now_ms() : 0.0;
@@ -651,18 +652,28 @@ struct U3 {
 struct U3Plus {
   __host__ __device__ U3 operator()(const U3 &x, const U3 &y) const { return U3{x.a + y.a, x.b + y.b, x.c + y.c}; }
 };
-static U3 excl_scan_u3(rs_engine *E, const U3 *in, U3 *out, uint64_t n, const char *tag) {
-  if (n == 0) return U3{0, 0, 0};
-  size_t tb = 0;
-  const U3 zero{0, 0, 0};
-  HC(rocprim::exclusive_scan(nullptr, tb, in, out, zero, (size_t)n, U3Plus(), E->st));
-  void *tmp = E->A.get<uint8_t>(std::string("scan3.tmp.") + tag, tb);
-  HC(rocprim::exclusive_scan(tmp, tb, in, out, zero, (size_t)n, U3Plus(), E->st));
-  U3 li, lo;
-  HC(hipMemcpyAsync(&li, in + n - 1, sizeof(U3), hipMemcpyDeviceToHost, E->st));
-  HC(hipMemcpyAsync(&lo, out + n - 1, sizeof(U3), hipMemcpyDeviceToHost, E->st));
+// the total through pinned read-back words [8..13]; x (optional): two more device words read in the
+// same round trip (an earlier device-only scan's last input and output), their sum into *x_sum
+static U3 excl_scan_u3(rs_engine *E, const U3 *in, U3 *out, uint64_t n, const char *tag, const uint64_t *x_in = nullptr,
+                       const uint64_t *x_out = nullptr, uint64_t *x_sum = nullptr) {
+  if (n == 0 && !x_sum) return U3{0, 0, 0};
+  uint64_t *h = (uint64_t *)pin_get(E, 18, kPinRb) + 8;
+  if (n) {
+    size_t tb = 0;
+    const U3 zero{0, 0, 0};
+    HC(rocprim::exclusive_scan(nullptr, tb, in, out, zero, (size_t)n, U3Plus(), E->st));
+    void *tmp = E->A.get<uint8_t>(std::string("scan3.tmp.") + tag, tb);
+    HC(rocprim::exclusive_scan(tmp, tb, in, out, zero, (size_t)n, U3Plus(), E->st));
+    HC(hipMemcpyAsync(h, in + n - 1, sizeof(U3), hipMemcpyDeviceToHost, E->st));
+    HC(hipMemcpyAsync(h + 3, out + n - 1, sizeof(U3), hipMemcpyDeviceToHost, E->st));
+  }
+  if (x_sum) {
+    HC(hipMemcpyAsync(h + 6, x_in, 8, hipMemcpyDeviceToHost, E->st));
+    HC(hipMemcpyAsync(h + 7, x_out, 8, hipMemcpyDeviceToHost, E->st));
+  }
   HC(hipStreamSynchronize(E->st));
-  return U3Plus()(li, lo);
+  if (x_sum) *x_sum = h[6] + h[7];
+  return n ? U3{h[0] + h[3], h[1] + h[4], h[2] + h[5]} : U3{0, 0, 0};
 }
 #include "flatten.hpp"
 #include "output.hpp"
@@ -1248,7 +1259,7 @@ static DevClusters gpu_clusters(rs_engine *E, const DRows &V, int old_heur, cons
   HC(hipMemsetAsync(stat, 0, 64, st));
   launch_capped(st, k_cl_count, n, 1024, V, npairs, stat);
   uint64_t *poff = A.get<uint64_t>("cl.poff", n);
-  unsigned long long *hs = (unsigned long long *)pin_get(E, 18, 64);  // pinned: no staged copy
+  unsigned long long *hs = (unsigned long long *)pin_get(E, 18, kPinRb);  // pinned: no staged copy
   HC(hipMemcpyAsync(hs, stat, 16, hipMemcpyDeviceToHost, st));
   const uint64_t P = excl_scan_u64(E, npairs, poff, n, "cl1", &hw);  // (its read-back synchronises)
   mark("pairs");
@@ -2462,7 +2473,11 @@ static void snap_start(rs_engine *E) {
   E->snap_rc = 0;
   E->snap_closed = false;
   E->snap_thread = std::thread([E]() {
-    constexpr size_t chunk = 32ull << 20;
+    // 128 MiB chunks, two in flight (host -> host medians 44.1-44.3 ms against 44.5-45.6 with 32 MiB
+    // chunks, tools/r6_snap_ab.sh): small copies on the other streams are not held behind them
+    // (tools/micro/copyq.hip), and fewer chunks leave fewer gaps between them on the link
+    static const size_t chunk = (getenv("RS_SNAP_CHUNK_MB") ? strtoull(getenv("RS_SNAP_CHUNK_MB"), nullptr, 10) : 128ull) << 20;
+    static const int depth = std::max(1, std::min(8, getenv("RS_SNAP_DEPTH") ? atoi(getenv("RS_SNAP_DEPTH")) : 2));
     if (hipSetDevice(E->device) != hipSuccess) { E->snap_rc = RS_E_HIP; return; }
     int k = 0;
     double prof_ms = 0.0, prof_b = 0.0;
@@ -2481,9 +2496,9 @@ static void snap_start(rs_engine *E) {
       const double tj = g_prof_env ? now_ms() : 0.0;
       for (size_t o = 0; o < j.bytes; o += chunk, ++k) {
         const size_t n = std::min(chunk, j.bytes - o);
-        if (k >= 2 && hipEventSynchronize(E->ev_chunk[k & 1]) != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
+        if (k >= depth && hipEventSynchronize(E->ev_chunk[k % depth]) != hipSuccess) { E->snap_rc = RS_E_HIP; break; }
         if (hipMemcpyAsync((uint8_t *)j.dst + o, (const uint8_t *)j.src + o, n, hipMemcpyDeviceToHost, E->stx) != hipSuccess ||
-            hipEventRecord(E->ev_chunk[k & 1], E->stx) != hipSuccess) {
+            hipEventRecord(E->ev_chunk[k % depth], E->stx) != hipSuccess) {
           E->snap_rc = RS_E_HIP;
           break;
         }
@@ -3000,7 +3015,18 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     U3 *elen = A.get<U3>("so.elen", n_nl);
     Comm *CM = E->comm.get();
     const bool shard = CM && CM->world > 1;
-    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, shard ? E->nl_lo : (uint64_t)0, shard ? E->nl_hi : hi_rows, so_early, elen);
+    // the gather reads copies of the selected rows' views: the second pass and later rounds re-point rows
+    const DRows *src[3] = {&sa, &sb, &sc};
+    const char *nm[3] = {"so.a", "so.b", "so.c"};
+    DRows cp[3];
+    ViewCopy vc;
+    for (int q = 0; q < 3; ++q) {
+      cp[q] = *src[q];
+      cp[q].off = vc.off[q] = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
+      cp[q].len = vc.len[q] = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
+    }
+    launch(st, k_snap_flags, n_nl, sa, sb, sc, late, n_nl, shard ? E->nl_lo : (uint64_t)0, shard ? E->nl_hi : hi_rows, so_early, elen,
+           vc);
     const U3 et = excl_scan_u3(E, elen, so_eoff, n_nl, "so");
     // single engine: the lconst rows so far (final as they enter the heap) go behind the C part
     E->lc_snap_n = shard ? 0 : lc.n;
@@ -3016,17 +3042,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
         E->stream_out = false;
         return;
       }
-    }
-    // the gather reads copies of the row views: the second pass and later rounds re-point rows
-    const DRows *src[3] = {&sa, &sb, &sc};
-    const char *nm[3] = {"so.a", "so.b", "so.c"};
-    DRows cp[3];
-    for (int q = 0; q < 3; ++q) {
-      cp[q] = *src[q];
-      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
-      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
-      HC(hipMemcpyAsync(cp[q].off, src[q]->off, 8 * n_nl, hipMemcpyDeviceToDevice, st));
-      HC(hipMemcpyAsync(cp[q].len, src[q]->len, 4 * n_nl, hipMemcpyDeviceToDevice, st));
     }
     HC(hipEventRecord(E->ev_snap0, st));
     HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
@@ -3078,7 +3093,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (!E->snap_on || !nl_late || !n_late || (E->comm && E->comm->world > 1)) return;
     HC(hipStreamWaitEvent(st, E->ev_snap, 0));  // the first snapshot's gathers read the flags rewritten here
     U3 *elen = A.get<U3>("so.elen", n_nl), *eoff2 = A.get<U3>("so.eoff2", n_nl);
-    launch(st, k_snap_lens2, n_nl, sa, sb, sc, (const uint64_t *)nl_late, n_nl, elen);
+    const DRows *src[3] = {&sa, &sb, &sc};
+    const char *nm[3] = {"so2.a", "so2.b", "so2.c"};
+    DRows cp[3];  // copies of the selected rows' views (the rounds re-point rows)
+    ViewCopy vc;
+    for (int q = 0; q < 3; ++q) {
+      cp[q] = *src[q];
+      cp[q].off = vc.off[q] = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
+      cp[q].len = vc.len[q] = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
+    }
+    launch(st, k_snap_lens2, n_nl, sa, sb, sc, (const uint64_t *)nl_late, n_nl, elen, vc);
     const U3 et = excl_scan_u3(E, elen, eoff2, n_nl, "so2");
     const uint64_t e2[3] = {et.a, et.b, et.c};
     for (int q = 0; q < 3; ++q) E->snap_hint[q] = std::max(E->snap_hint[q], E->snap_e[q] + e2[q]);
@@ -3086,16 +3110,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (E->snap_e[q] + e2[q] > E->snap_cap[q]) return;  // no room this time (the hint grows the next run's)
     launch(st, k_snap_mark2, n_nl, (const uint64_t *)nl_late, (const U3 *)elen, (const U3 *)eoff2,
            U3{E->snap_e[0], E->snap_e[1], E->snap_e[2]}, n_nl, so_early, so_eoff);
-    const DRows *src[3] = {&sa, &sb, &sc};
-    const char *nm[3] = {"so2.a", "so2.b", "so2.c"};
-    DRows cp[3];
-    for (int q = 0; q < 3; ++q) {  // copies of the row views (the rounds re-point rows)
-      cp[q] = *src[q];
-      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
-      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
-      HC(hipMemcpyAsync(cp[q].off, src[q]->off, 8 * n_nl, hipMemcpyDeviceToDevice, st));
-      HC(hipMemcpyAsync(cp[q].len, src[q]->len, 4 * n_nl, hipMemcpyDeviceToDevice, st));
-    }
     HC(hipEventRecord(E->ev_snap0, st));
     HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
     for (int q = 0; q < 3; ++q) {
@@ -3127,7 +3141,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     if (!E->snap_on || (E->comm && E->comm->world > 1)) return;
     HC(hipStreamWaitEvent(st, E->ev_snap, 0));  // the first half's gathers read the flags rewritten here
     U3 *elen = A.get<U3>("so.elenh", n_nl), *eoffh = A.get<U3>("so.eoffh", n_nl);
-    launch(st, k_snap_lens_rng, n_nl, sa, sb, sc, (const uint64_t *)nl_late, h, n_nl, n_nl, elen);
+    const DRows *src[3] = {&sa, &sb, &sc};
+    const char *nm[3] = {"soh.a", "soh.b", "soh.c"};
+    DRows cp[3];  // copies of the selected rows' views (the second pass and the rounds re-point rows)
+    ViewCopy vc;
+    for (int q = 0; q < 3; ++q) {
+      cp[q] = *src[q];
+      cp[q].off = vc.off[q] = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
+      cp[q].len = vc.len[q] = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
+    }
+    launch(st, k_snap_lens_rng, n_nl, sa, sb, sc, (const uint64_t *)nl_late, h, n_nl, n_nl, elen, vc);
     const U3 et = excl_scan_u3(E, elen, eoffh, n_nl, "soh");
     const uint64_t e2[3] = {et.a, et.b, et.c};
     for (int q = 0; q < 3; ++q) E->snap_hint[q] = std::max(E->snap_hint[q], E->snap_e[q] + e2[q]);
@@ -3135,16 +3158,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (E->snap_e[q] + e2[q] > E->snap_cap[q]) return;
     launch(st, k_snap_mark_sel, n_nl, (const U3 *)elen, (const U3 *)eoffh, U3{E->snap_e[0], E->snap_e[1], E->snap_e[2]}, n_nl,
            so_early, so_eoff);
-    const DRows *src[3] = {&sa, &sb, &sc};
-    const char *nm[3] = {"soh.a", "soh.b", "soh.c"};
-    DRows cp[3];
-    for (int q = 0; q < 3; ++q) {  // copies of the row views (the second pass and the rounds re-point rows)
-      cp[q] = *src[q];
-      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_nl);
-      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_nl);
-      HC(hipMemcpyAsync(cp[q].off + h, src[q]->off + h, 8 * (n_nl - h), hipMemcpyDeviceToDevice, st));
-      HC(hipMemcpyAsync(cp[q].len + h, src[q]->len + h, 4 * (n_nl - h), hipMemcpyDeviceToDevice, st));
-    }
     HC(hipEventRecord(E->ev_snap0, st));
     HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));
     for (int q = 0; q < 3; ++q) {
@@ -3181,12 +3194,14 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     a.hmark = hmark;
     a.late = nl_late;
     launch(st, k_nl_count, n, a);
-    if (phase == 1) {  // the skipped rows, listed for the second pass
-      n_late = excl_scan_u64(E, nl_late, nl_lpos, n_nl, "nll");
+    const bool lists = phase == 1 && n_nl;
+    if (lists) {  // the skipped rows, listed for the second pass (their count comes back with the heap's)
+      dev_scan_u64(E, nl_late, nl_lpos, n_nl, st, "nll");
       launch(st, k_scatter_ids, n_nl, (const uint64_t *)nl_late, (const uint64_t *)nl_lpos, n_nl, nl_lids);
     }
     launch(st, k_pack3, n, (const uint64_t *)ca, (const uint64_t *)cb, (const uint64_t *)cc, n, cap3);
-    const U3 t3 = excl_scan_u3(E, cap3, sc3, n, "nl");
+    const U3 t3 = lists ? excl_scan_u3(E, cap3, sc3, n, "nl", nl_late + n_nl - 1, nl_lpos + n_nl - 1, &n_late)
+                        : excl_scan_u3(E, cap3, sc3, n, "nl");
     if (g_prof_env) fprintf(stderr, "[rs-prof] nl phase %d: %llu rows, %llu heap entries\n", phase, (unsigned long long)n,
                             (unsigned long long)(t3.a + t3.b + t3.c));
     heap_reserve(t3.a + t3.b + t3.c);
@@ -3412,7 +3427,16 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
     // the earlier snapshots' gathers read the early flags / offsets this one rewrites, and its own buffers
     HC(hipStreamWaitEvent(st, E->ev_snap, 0));
     U3 *elen = A.get<U3>("so.rlen", n_st), *eoff3 = A.get<U3>("so.roff", n_st);
-    launch(st, k_snap_lens_round, n_st, pa, pb, pc, touched, turn, (const uint32_t *)st_ids, (const uint8_t *)so_early, n_st, elen);
+    const DRows *src[3] = {&pa, &pb, &pc};
+    const char *nm[3] = {"sor.a", "sor.b", "sor.c"};
+    DRows cp[3];  // copies of the selected rows' views (a later round re-points rows)
+    ViewCopy vc;
+    for (int q = 0; q < 3; ++q) {
+      cp[q] = *src[q];
+      cp[q].off = vc.off[q] = A.get<uint64_t>(std::string(nm[q]) + ".off", n_st);
+      cp[q].len = vc.len[q] = A.get<uint32_t>(std::string(nm[q]) + ".len", n_st);
+    }
+    launch(st, k_snap_lens_round, n_st, pa, pb, pc, touched, turn, (const uint32_t *)st_ids, (const uint8_t *)so_early, n_st, elen, vc);
     const U3 et = excl_scan_u3(E, elen, eoff3, n_st, "sor");
     const uint64_t e3[3] = {et.a, et.b, et.c};
     if (!(e3[0] | e3[1] | e3[2])) return;
@@ -3421,16 +3445,6 @@ static void engine_run(rs_engine *E, const rs_flags *fl) {
       if (E->snap_e[q] + e3[q] > E->snap_cap[q]) return;
     launch(st, k_snap_mark_round, n_st, (const uint32_t *)st_ids, (const U3 *)elen, (const U3 *)eoff3,
            U3{E->snap_e[0], E->snap_e[1], E->snap_e[2]}, n_st, so_early, so_eoff, so_dirty);
-    const DRows *src[3] = {&pa, &pb, &pc};
-    const char *nm[3] = {"sor.a", "sor.b", "sor.c"};
-    DRows cp[3];
-    for (int q = 0; q < 3; ++q) {  // copies of the row views (a later round re-points rows)
-      cp[q] = *src[q];
-      cp[q].off = A.get<uint64_t>(std::string(nm[q]) + ".off", n_st);
-      cp[q].len = A.get<uint32_t>(std::string(nm[q]) + ".len", n_st);
-      HC(hipMemcpyAsync(cp[q].off, src[q]->off, 8 * n_st, hipMemcpyDeviceToDevice, st));
-      HC(hipMemcpyAsync(cp[q].len, src[q]->len, 4 * n_st, hipMemcpyDeviceToDevice, st));
-    }
     // the previous snapshot's gathers still read their view copies and elen / offsets (stc is in order)
     HC(hipEventRecord(E->ev_snap0, st));
     HC(hipStreamWaitEvent(E->stc, E->ev_snap0, 0));

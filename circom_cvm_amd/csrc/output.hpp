@@ -13,27 +13,46 @@
 
 __device__ __forceinline__ uint64_t u3_sel(const U3 &x, int q) { return q == 0 ? x.a : (q == 1 ? x.b : x.c); }
 
+// The gathers of a snapshot run on the copy stream while the main stream goes on and may re-point
+// rows (the second pass, the rounds): they read a copy of the selected rows' views, which the kernel
+// that selects them writes (the other rows' entries are left as they were).
+struct ViewCopy {
+  uint64_t *off[3];
+  uint32_t *len[3];
+};
+__device__ __forceinline__ void view_copy(const ViewCopy &v, const DRows &a, const DRows &b, const DRows &c, uint64_t i,
+                                          uint32_t la, uint32_t lb, uint32_t lc) {
+  v.off[0][i] = a.off[i];
+  v.off[1][i] = b.off[i];
+  v.off[2][i] = c.off[i];
+  v.len[0][i] = la;
+  v.len[1][i] = lb;
+  v.len[2][i] = lc;
+}
+
 // early[i]: non-linear row i is done (not left to a second pass) and stayed non-linear -- a
 // storage row (non_linear_utils.rs:6-31: A or B non-empty); elen[i]: its part lengths (0
 // when not early).  Sharded: only the rows [lo, hi) this rank copies to the host count.
 __global__ void k_snap_flags(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, uint64_t lo, uint64_t hi, uint8_t *early,
-                             U3 *elen) {
+                             U3 *elen, ViewCopy vc) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
     const bool done = (!late || !late[i]) && i >= lo && i < hi;
     const uint32_t la = done ? a.len[i] : 0, lb = done ? b.len[i] : 0, lc = done ? c.len[i] : 0;
     const bool ok = (la | lb) != 0;  // k_flag_linear: linear iff A and B are both empty
     early[i] = ok ? 1 : 0;
     elen[i] = ok ? U3{la, lb, lc} : U3{0, 0, 0};
+    if (ok) view_copy(vc, a, b, c, i, la, lb, lc);
   }
 }
 
 // The second snapshot: the rows the second frames pass did (late[i]) that stayed storage rows --
 // elen[i] their part lengths (else 0); once they fit behind the first snapshot, k_snap_mark2 makes
 // them early at base + their offsets.
-__global__ void k_snap_lens2(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, U3 *elen) {
+__global__ void k_snap_lens2(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t n, U3 *elen, ViewCopy vc) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
     const bool ok = late[i] && (a.len[i] | b.len[i]) != 0;
     elen[i] = ok ? U3{a.len[i], b.len[i], c.len[i]} : U3{0, 0, 0};
+    if (ok) view_copy(vc, a, b, c, i, a.len[i], b.len[i], c.len[i]);
   }
 }
 __global__ void k_snap_mark2(const uint64_t *late, const U3 *elen, const U3 *eoff2, U3 base, uint64_t n, uint8_t *early,
@@ -48,10 +67,12 @@ __global__ void k_snap_mark2(const uint64_t *late, const U3 *elen, const U3 *eof
 // The first pass in two halves (single engine): the second half's rows [lo, hi) that are done and
 // stayed storage rows -- elen[i] their part lengths (else 0); k_snap_mark_sel makes every row with
 // lengths early at base + its offset.
-__global__ void k_snap_lens_rng(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t lo, uint64_t hi, uint64_t n, U3 *elen) {
+__global__ void k_snap_lens_rng(DRows a, DRows b, DRows c, const uint64_t *late, uint64_t lo, uint64_t hi, uint64_t n, U3 *elen,
+                                ViewCopy vc) {
   for (uint64_t i = gtid(); i < n; i += gstride()) {
     const bool ok = i >= lo && i < hi && !(late && late[i]) && (a.len[i] | b.len[i]) != 0;
     elen[i] = ok ? U3{a.len[i], b.len[i], c.len[i]} : U3{0, 0, 0};
+    if (ok) view_copy(vc, a, b, c, i, a.len[i], b.len[i], c.len[i]);
   }
 }
 __global__ void k_snap_mark_sel(const U3 *elen, const U3 *eoff2, U3 base, uint64_t n, uint8_t *early, U3 *eoff) {
@@ -87,10 +108,11 @@ __global__ void k_snap_gather(FieldP F, DRows R, const uint8_t *early, const U3 
 // makes them early at base + their offsets (by non-linear row nl_of[r]) and clean again;
 // k_snap_gather_st copies them.  (A later round may still rewrite one: dirty again, late at the end.)
 __global__ void k_snap_lens_round(DRows a, DRows b, DRows c, const uint8_t *touched, const int32_t *turn, const uint32_t *nl_of,
-                                  const uint8_t *early, uint64_t n, U3 *elen) {
+                                  const uint8_t *early, uint64_t n, U3 *elen, ViewCopy vc) {
   for (uint64_t r = gtid(); r < n; r += gstride()) {
     const bool ok = (touched[r] || !early[nl_of[r]]) && turn[r] < 0 && (a.len[r] | b.len[r]) != 0;
     elen[r] = ok ? U3{a.len[r], b.len[r], c.len[r]} : U3{0, 0, 0};
+    if (ok) view_copy(vc, a, b, c, r, a.len[r], b.len[r], c.len[r]);
   }
 }
 __global__ void k_snap_mark_round(const uint32_t *nl_of, const U3 *elen, const U3 *eoff3, U3 base, uint64_t n, uint8_t *early,
