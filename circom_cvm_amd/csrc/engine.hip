@@ -1903,7 +1903,8 @@ static void run_linear_simplification(rs_engine *E, const DRows &view, int old_h
         // (their ordered loops are the tail's latency), the rest -- most of the composition work,
         // which fills the GPU -- beside them on the small clusters' stream, after k_eliminate.  One
         // launch per kernel over all of them made every finish wait for the largest loops.
-        const uint64_t n_t1 = n_tail > kTailSplit + kTailSplit / 4 ? kTailSplit : n_tail, n_t2 = n_tail - n_t1;
+        static const uint64_t split = getenv("RS_TAIL_SPLIT") ? strtoull(getenv("RS_TAIL_SPLIT"), nullptr, 10) : kTailSplit;
+        const uint64_t n_t1 = n_tail > split + split / 4 ? split : n_tail, n_t2 = n_tail - n_t1;
         n_tgroups = n_t2 ? 2 : 1;
         auto tail_group = [&](hipStream_t s, ElimArgs g, const uint32_t *ids, uint64_t n, const char *cls_name, int grp) {
           const bool timed = grp == 0;
