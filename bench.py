@@ -365,11 +365,20 @@ def main():
     # N > 1: torch first.  torch bundles its own HIP runtime and RCCL; loaded first, the library binds to
     # them (same SONAME), loaded after the library torch maps a second runtime beside /opt/rocm's and the
     # two do not mix.  N = 1 needs no torch: the library runs on /opt/rocm's runtime, as under a Rust host.
+    # RS_BENCH_HOSTCOMM=1: a one-GPU rehearsal of the N > 1 path -- every rank on device 0, joined over
+    # the host transport (rs_engine_join_host; RCCL refuses two ranks on one device), torch's own
+    # collectives over gloo.  The driver's N > 1 runs never set it.
+    rehearse = world > 1 and os.environ.get("RS_BENCH_HOSTCOMM") == "1"
+    red_dev = "cpu" if rehearse else "cuda"
     if world > 1:
         import torch
         import torch.distributed as dist_
-        torch.cuda.set_device(local)
-        dist_.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            local = 0
+            dist_.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist_.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = dist_
     import circom_cvm_amd as M
     M.abi.lib()
@@ -393,12 +402,14 @@ def main():
     n_rows = inp.rows()
     pin = M.PinnedInput(inp.c)
     eng = M.Engine(local)
-    if world > 1:
+    if rehearse:
+        eng.join_host(world, rank, "bench" + os.environ.get("MASTER_PORT", "0"))
+    elif world > 1:
         eng.join_rccl(world, rank, share_comm_id(dist, rank, M.comm_unique_id))
     for _ in range(args.warmup):
         eng.simplify(pin.c, fl)
     dt, acc, tot, out, last = timed_steps(eng, pin.c, fl, args.steps, barrier)
-    dt, _ = reduce_over_ranks(dist, dt, n_rows, "cuda")
+    dt, _ = reduce_over_ranks(dist, dt, n_rows, red_dev)
     got = None
     if rank == 0 and not args.no_cpu:
         import rsio
@@ -407,17 +418,22 @@ def main():
     write = None
     if rank == 0 and not args.no_write:
         import tempfile
-        with tempfile.TemporaryDirectory() as tmp:
-            path = os.path.join(tmp, "bench_O2.r1cs")
-            ms_w = eng.write_r1cs(path)
-            nb = os.path.getsize(path)
-            os.unlink(path)
-            fsb = fs_write_bound(tmp, nb)
-            write = {"ms": round(ms_w, 2), "bytes": nb, "GBps": round(nb / ms_w / 1e6, 2),
-                     "fs_bound_GBps": round(fsb, 2), "of_fs_bound": round(nb / ms_w / 1e6 / max(fsb, 1e-9), 3),
-                     "what": "rs_engine_write_r1cs: the last step's result as a .r1cs file (constraint section "
-                             "built on the device, streamed to a fresh file in a temporary directory); fs_bound: the "
-                             "same number of bytes written from host memory into a fresh file there (no GPU)"}
+        try:
+            with tempfile.TemporaryDirectory() as tmp:
+                path = os.path.join(tmp, "bench_O2.r1cs")
+                ms_w = eng.write_r1cs(path)
+                nb = os.path.getsize(path)
+                os.unlink(path)
+                fsb = fs_write_bound(tmp, nb)
+                write = {"ms": round(ms_w, 2), "bytes": nb, "GBps": round(nb / ms_w / 1e6, 2),
+                         "fs_bound_GBps": round(fsb, 2), "of_fs_bound": round(nb / ms_w / 1e6 / max(fsb, 1e-9), 3),
+                         "what": "rs_engine_write_r1cs: the last step's result as a .r1cs file (constraint section "
+                                 "built on the device, streamed to a fresh file in a temporary directory); fs_bound: the "
+                                 "same number of bytes written from host memory into a fresh file there (no GPU)"}
+        except Exception as e:  # noqa: BLE001 -- N > 1: an extra's failure is reported in the line, not fatal
+            if world == 1:
+                raise
+            write = {"error": str(e)[:300]}
     # the DAG flattening that produces such an input, timed on its own
     flat = flatten_bench(args.seed, args.prime) if rank == 0 and not args.no_flatten else None
     # SURVEY 8(d) config 5's template replication (64-row instances sharing coefficients, wired
@@ -482,7 +498,7 @@ def main():
         for _ in range(args.steps):
             eng.run(fl)
         barrier()
-        dt_hbm, _ = reduce_over_ranks(dist, time.perf_counter() - t0, n_rows, "cuda")
+        dt_hbm, _ = reduce_over_ranks(dist, time.perf_counter() - t0, n_rows, red_dev)
     eng.close()
     pin.free()
     # ---- extra at N > 1: independent circuits per rank (weak scaling, no data-path collective)
@@ -494,7 +510,7 @@ def main():
         for _ in range(args.warmup):
             weng.simplify(wpin.c, fl)
         wdt, _, _, _, _ = timed_steps(weng, wpin.c, fl, args.steps, barrier)
-        wdt, wrows = reduce_over_ranks(dist, wdt, winp.rows(), "cuda")
+        wdt, wrows = reduce_over_ranks(dist, wdt, winp.rows(), red_dev)
         weng.close()
         wpin.free()
         winp.free()
@@ -607,7 +623,17 @@ def main():
             line["o1"] = o1
         if weak is not None:
             line["weak_shards"] = weak
-        if not args.no_cpu:
+        if not args.no_cpu and world > 1:
+            # N > 1: the oracle only as the checker of rank 0's view of the whole result (the CPU
+            # baseline is an N = 1 field)
+            import rsio
+            ref, _ = rsio.oracle_arrays(inp.c, rsio.flags("O2"), threads=args.cpu_threads or cpu_threads())
+            diff = rsio.diff_output_arrays(got, ref)
+            line["cpu_baseline"] = None
+            line["bit_exact"] = diff is None
+            if diff is not None:
+                line["bit_exact_diff"] = diff
+        elif not args.no_cpu:
             threads = args.cpu_threads or cpu_threads()
             cb, ref, alg = cpu_baseline(M, inp, threads, args.cpu_j1_rows, args.seed, args.prime)
             line["cpu_baseline"] = cb

@@ -392,3 +392,47 @@ def test_two_process_host_transport(kind, rows, world):
     for r, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{out[-3000:]}"
         assert f"rank {r} ok" in out
+
+
+def test_sharded_engine_writes_r1cs():
+    """bench.py's N > 1 line has rank 0 write its result with the device writer
+    (rs_engine_write_r1cs) after a sharded host -> host call: on every rank of a sharded group the
+    file is byte-identical to the host writer's over the same engine's (whole, shared) result."""
+    import ctypes as C
+    import os
+    import tempfile
+
+    from circom_cvm_amd import abi
+
+    world = 2
+    inp = M.Input.synth(0, 300_000, 42)
+    fl = rsio.flags("O2")
+    engs = group(world)
+    outs, errs = [None] * world, [None] * world
+
+    def work(r):
+        try:
+            outs[r] = engs[r].simplify(inp.c, fl)
+        except Exception as ex:  # noqa: BLE001 -- reported below
+            errs[r] = ex
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=280)
+        assert not t.is_alive(), "sharded simplify hung"
+    for e in errs:
+        if e is not None:
+            raise e
+    with tempfile.TemporaryDirectory() as tmp:
+        ph, pd = os.path.join(tmp, "h.r1cs"), os.path.join(tmp, "d.r1cs")
+        for r in range(world):
+            abi.check(abi.lib().rs_write_r1cs(ph.encode(), C.byref(inp.c), C.byref(outs[r])))
+            assert engs[r].write_r1cs(pd) > 0
+            with open(ph, "rb") as f:
+                a = f.read()
+            with open(pd, "rb") as f:
+                b = f.read()
+            assert len(a) == len(b), f"rank {r}"
+            assert a == b, f"rank {r}"
